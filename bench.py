@@ -1,0 +1,257 @@
+"""Benchmark: denoising steps/s of the conditional-DDPM sampler on MI355X.
+
+Workload (BASELINE.json configs[1] restated on the reference model, SURVEY.md
+8d "R2"): ConditionalDiffusionModel(29, 128) (the only denoiser the reference
+has), batch 64 members per GPU, condition (64, 14, 4693) fp32, T = 1000,
+faithful mode -- the condition encoder is re-evaluated at every step exactly as
+the reference's sample_model does (ERT_Conditional_Diffusion.py:108-118).
+
+A step = one reverse update of all B members (encoder + head + update).  The
+timed region replays captured hipGraphs of whole chains / chain segments with
+inputs already resident in HBM; exactly --steps steps are timed between a
+barrier + synchronize on each side, max over ranks.  One process per GPU
+(torchrun); members are sharded (rank r owns global members r*B..r*B+B-1,
+noise keyed by global member id) and the only collective on the data path is
+one RCCL broadcast of the conditioning tensor from rank 0 before timing.
+
+Extra objects on the JSON line:
+  roofline      the strip kernel (conv1+conv2+pool partials), timed per launch
+                with HIP events on the launching stream; fp32 MFMA-bound.
+  cpu_baseline  the reference algorithm on PyTorch-CPU (oracle/ref_torch.py,
+                bit-identical to the reference) on rank 0, bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ert-conditional-diffusion-model_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import ertdiff  # noqa: E402
+from ertdiff import _lib  # noqa: E402
+
+METRIC = "denoising-steps/sec (64×64, batch 64) at 1/2/4/8 GPUs; conv HBM GB/s vs roofline"
+L_MEAS = 4693
+P = 29
+# Algorithmic work of the strip kernel per member:
+CONV_FLOP_PER_MEMBER = 6_308_736 + 14_426_112
+# ... and of one full faithful step per member incl. Linear layers
+STEP_FLOP_PER_MEMBER = 20_864_384
+COND_BYTES_PER_MEMBER = 14 * L_MEAS * 4
+PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
+PEAK_BF16_TFLOPS = 2500.0    # dense bf16 MFMA
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=64, help="members per GPU")
+    ap.add_argument("--T", type=int, default=1000)
+    ap.add_argument("--mode", choices=["faithful", "hoisted"], default="faithful")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-hoisted", action="store_true", help="skip the secondary hoisted timing")
+    ap.add_argument("--roofline-reps", type=int, default=200)
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def make_plans(model, cond, sched, T, B, mode, seed, member_offset):
+    """Full-chain plan plus lazily built segment plans (t_first = T-1)."""
+    cache = {}
+
+    def plan(n_run):
+        if n_run not in cache:
+            cache[n_run] = ertdiff.SamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=n_run,
+                                               mode=mode, seed=seed, member_offset=member_offset, B=B)
+        return cache[n_run]
+    return plan
+
+
+def run_steps(plan_of, n_steps, T, x_T):
+    """Enqueue exactly n_steps denoising steps as whole chains + one partial chain."""
+    done = 0
+    while done < n_steps:
+        n = min(T, n_steps - done)
+        p = plan_of(n)
+        p.x.copy_(x_T)
+        p.launch()
+        done += n
+
+
+def time_steps(plan_of, n_steps, T, x_T, world, dev):
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_steps(plan_of, n_steps, T, x_T)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    return el
+
+
+def strip_kernel_roofline(model, cond, B, precision, reps, dev):
+    """Average duration of the encoder strip kernel, HIP events on its stream."""
+    L = cond.shape[2]
+    packed = model.packed_weights(dev)
+    ws = model.workspace(dev, B, L, 0, _lib.OP_FORWARD)
+    w = model.weights_struct()
+    prec = _lib.PREC_BF16 if precision == "bf16" else _lib.PREC_FP32
+    stream = torch.cuda.current_stream(dev)
+
+    def launch():
+        _lib.check(_lib.lib().ertd_encoder_strips(ctypes.byref(w), packed.data_ptr(), cond.data_ptr(),
+                                                  14 * L, B, L, prec, ws.data_ptr(), ws.numel(),
+                                                  stream.cuda_stream), "encoder_strips")
+    for _ in range(20):
+        launch()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    for i in range(reps):
+        starts[i].record(stream)
+        launch()
+        ends[i].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
+    avg_ms = sum(ms) / len(ms)
+    flop = CONV_FLOP_PER_MEMBER * B
+    achieved = flop / (avg_ms * 1e-3) / 1e12
+    peak = PEAK_BF16_TFLOPS if precision == "bf16" else PEAK_FP32_TFLOPS
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "strip_kernel_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        key = f"B{B}_{precision}"
+        if key in rec:
+            traffic = rec[key]["hbm_bytes_per_launch"]
+    return {"kernel": "enc_fp32_kernel" if precision == "fp32" else "enc_bf16_kernel",
+            "bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "avg_us": round(avg_ms * 1e3, 3), "median_us": round(ms[len(ms) // 2] * 1e3, 3),
+            "algorithmic_flop_per_launch": flop,
+            "algorithmic_bytes_per_launch": COND_BYTES_PER_MEMBER * B,
+            "hbm_gbs_algorithmic": round(COND_BYTES_PER_MEMBER * B / (avg_ms * 1e-3) / 1e9, 1)}
+
+
+def cpu_baseline(seconds, B, T, mode):
+    """Reference algorithm on PyTorch-CPU (the oracle restatement, which is
+    bit-identical to ERT_Conditional_Diffusion.py's sample_model), bounded."""
+    from oracle import ref_torch as RT
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(1042)
+    cond = torch.rand(B, 14, L_MEAS, generator=g)
+    torch.manual_seed(42)
+    W = {k: v.detach() for k, v in ertdiff.ConditionalDiffusionModel(P, 128).state_dict().items()}
+    noise = torch.randn(T, B, P, generator=torch.Generator().manual_seed(2042))
+    hoist = mode == "hoisted"
+    RT.sample(cond, W, T, noise, encoder_every_step=not hoist, max_steps=2)  # warm
+    t0 = time.perf_counter()
+    RT.sample(cond, W, T, noise, encoder_every_step=not hoist, max_steps=3)
+    per = (time.perf_counter() - t0) / 3
+    n = int(max(3, min(T, seconds / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    RT.sample(cond, W, T, noise, encoder_every_step=not hoist, max_steps=n)
+    el = time.perf_counter() - t0
+    return {"value": round(n / el, 3), "unit": "denoising-steps/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} of {T} steps of the reference sampler ({'hoisted' if hoist else 'faithful'}), "
+                      f"B={B}, cond (B,14,{L_MEAS}) fp32, torch {torch.__version__} CPU, {threads} threads",
+            "seconds": round(el, 2)}
+
+
+def main():
+    a = parse()
+    rank, world, dev = setup_dist()
+    B, T = a.batch, a.T
+    torch.manual_seed(42)
+    model = ertdiff.ConditionalDiffusionModel(P, 128).to(dev).eval()
+    model.precision = a.precision
+    # synthetic conditioning batch in the MinMax domain [0,1) (:257-261); one
+    # RCCL broadcast from rank 0 is the only collective on the data path
+    g = torch.Generator(device=dev).manual_seed(1042)
+    cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
+    if world > 1:
+        dist.broadcast(cond, src=0)
+    sched = ertdiff.get_diffusion_schedule(T, device=dev)
+    offset = rank * B
+    x_T = ertdiff.philox_normal(B, P, T, 1, 2042, offset, dev)
+
+    plan_of = make_plans(model, cond, sched, T, B, a.mode, 2042, offset)
+    run_steps(plan_of, a.warmup, T, x_T)              # untimed warmup (also builds plans)
+    if a.steps % T:
+        plan_of(a.steps % T)                           # build the partial plan before timing
+    torch.cuda.synchronize(dev)
+    el = time_steps(plan_of, a.steps, T, x_T, world, dev)
+    value = world * a.steps / el
+
+    extra = {}
+    if not a.no_hoisted and a.mode == "faithful":
+        hplan = make_plans(model, cond, sched, T, B, "hoisted", 2042, offset)
+        run_steps(hplan, T, T, x_T)
+        hel = time_steps(hplan, T, T, x_T, world, dev)
+        extra["hoisted_steps_per_s"] = round(world * T / hel, 1)
+    roof = strip_kernel_roofline(model, cond, B, a.precision, a.roofline_reps, dev)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a.cpu_seconds, B, T, "faithful")
+        if "hoisted_steps_per_s" in extra:
+            hc = cpu_baseline(max(3.0, a.cpu_seconds / 3), B, T, "hoisted")
+            extra["cpu_hoisted_steps_per_s"] = hc["value"]
+    if rank == 0:
+        step_s = el / a.steps
+        extra.update({
+            "member_steps_per_s": round(value * B, 1),
+            "step_tflops": round(STEP_FLOP_PER_MEMBER * B / step_s / 1e12 * world, 2),
+            "vs_cpu_baseline": round(value / cpu["value"], 1) if cpu else None,
+        })
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "denoising-steps/sec",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(step_s * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32" if a.precision == "fp32" else "bf16-operand/f32",
+            "data": "synthetic: cond U[0,1) (B,14,4693), seed-42 default-init weights, philox noise",
+            "config": {"workload": f"R2: ConditionalDiffusionModel(29,128) {a.mode} DDPM sampling, "
+                                   f"cond ({B},14,{L_MEAS}), T={T}",
+                       "global_batch": B * world, "members_per_gpu": B, "T": T, "mode": a.mode,
+                       "precision": a.precision, "parallelism": f"dp{world} (member shards)"},
+            "roofline": roof, "cpu_baseline": cpu, "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,285 @@
+// extern "C" entry points of libertdiff_hip.so (declared in include/ertdiff.h).
+// Every shape is validated on the host before anything is enqueued.
+#include <cstring>
+#include <new>
+
+#include "ertd_common.h"
+
+using namespace ertd;
+
+namespace {
+
+constexpr size_t ALIGN = 256;
+inline size_t align_up(size_t n) { return (n + ALIGN - 1) / ALIGN * ALIGN; }
+
+struct Ws {
+  float* partial;
+  float* U;
+  float* V;
+  float* cond_emb;
+};
+
+size_t ws_layout(int B, int L, int T, int op, void* base, Ws* out) {
+  const int L2 = conv_len(conv_len(L));
+  const size_t S = (size_t)n_strips(L2);
+  size_t off = 0;
+  char* p = (char*)base;
+  Ws w{};
+  w.partial = (float*)(p + off);
+  off += align_up((size_t)B * S * C2 * sizeof(float));
+  if (op == ERTD_OP_SAMPLE) {
+    w.U = (float*)(p + off);
+    off += align_up((size_t)B * H * sizeof(float));
+    w.V = (float*)(p + off);
+    off += align_up((size_t)(T > 0 ? T : 1) * H * sizeof(float));
+    w.cond_emb = (float*)(p + off);
+    off += align_up((size_t)B * H * sizeof(float));
+  }
+  if (out) *out = w;
+  return off;
+}
+
+bool weights_ok(const ertd_weights* w) {
+  if (!w) return false;
+  if (!w->enc0_w || !w->enc0_b || !w->enc2_w || !w->enc2_b || !w->enc6_w || !w->enc6_b ||
+      !w->time_w || !w->time_b || !w->mlp0_w || !w->mlp0_b || !w->mlp2_w || !w->mlp2_b)
+    return false;
+  return w->param_dim >= 1 && w->param_dim <= PMAX && w->hidden_dim == H;
+}
+
+inline int rc(hipError_t e) { return e == hipSuccess ? ERTD_OK : (int)e; }
+
+#define ERTD_TRY(expr)                  \
+  do {                                  \
+    const hipError_t e_ = (expr);       \
+    if (e_ != hipSuccess) return (int)e_; \
+  } while (0)
+
+int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond,
+                   long long cstride, int B, int L, int num_steps, int t_first, int n_run,
+                   const float* c1, const float* c2, const float* sigma, const float* freq,
+                   const float* noise, uint64_t seed, uint32_t member_offset, int mode,
+                   int precision, float* x_inout, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (!weights_ok(w) || !packed || !cond || !c1 || !c2 || !sigma || !freq || !x_inout || !ws)
+    return ERTD_EINVAL;
+  if (B < 1 || L < 1 || num_steps < 1 || (mode != ERTD_MODE_HOISTED && mode != ERTD_MODE_FAITHFUL))
+    return ERTD_EINVAL;
+  if (precision != ERTD_PREC_FP32 && precision != ERTD_PREC_BF16) return ERTD_EINVAL;
+  if (t_first < 0 || t_first >= num_steps || n_run < 1 || n_run > t_first + 1) return ERTD_EINVAL;
+  if (cstride != 0 && cstride < (long long)CIN * L) return ERTD_EINVAL;
+  Ws W;
+  if (ws_layout(B, L, num_steps, ERTD_OP_SAMPLE, ws, &W) > ws_bytes) return ERTD_ENOSPC;
+  const int t_last = t_first - n_run + 1;
+  const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
+  if (mode == ERTD_MODE_HOISTED) {
+    ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, cstride, B, L, precision,
+                                   W.partial, s));
+    ERTD_TRY(launch_hoist_prep(*w, packed, W.partial, S, L2, B, W.U, W.cond_emb, s));
+    ERTD_TRY(launch_time_table(*w, packed, freq, t_last, n_run, W.V + (size_t)t_last * H, s));
+    ERTD_TRY(launch_hoisted_sampler(*w, packed, W.U, W.V, c1, c2, sigma, noise, num_steps, t_first,
+                                    n_run, seed, member_offset, B, x_inout, s));
+    return ERTD_OK;
+  }
+  HeadArgs a{};
+  a.partial = W.partial;
+  a.S = S;
+  a.L2 = L2;
+  a.freq = freq;
+  a.x_in = x_inout;
+  a.c1 = c1;
+  a.c2 = c2;
+  a.sigma = sigma;
+  a.noise = noise;
+  a.num_steps = num_steps;
+  a.seed = seed;
+  a.member_offset = member_offset;
+  a.B = B;
+  a.x_out = x_inout;
+  for (int t = t_first; t >= t_last; --t) {
+    a.t_scalar = t;
+    ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, cstride, B, L, precision,
+                                   W.partial, s));
+    ERTD_TRY(launch_head(*w, packed, a, s));
+  }
+  return ERTD_OK;
+}
+
+}  // namespace
+
+struct ertd_plan {
+  hipStream_t stream = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+extern "C" {
+
+int ertd_version(void) { return 1; }
+
+const char* ertd_error_string(int code) {
+  switch (code) {
+    case ERTD_OK: return "ok";
+    case ERTD_EINVAL: return "invalid argument (shape, null pointer or unsupported dimension)";
+    case ERTD_ENOSPC: return "workspace too small";
+    case ERTD_ENOGPU: return "no usable gfx950 device";
+    default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
+  }
+}
+
+int ertd_device_ok(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  return strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+size_t ertd_workspace_bytes(int B, int L, int P, int T, int op) {
+  (void)P;
+  if (B < 1 || L < 1) return 0;
+  return ws_layout(B, L, T, op, nullptr, nullptr);
+}
+
+size_t ertd_packed_floats(void) { return (size_t)PACKED_FLOATS_ALL; }
+
+int ertd_pack_weights(const ertd_weights* w, float* packed, void* stream) {
+  if (!weights_ok(w) || !packed) return ERTD_EINVAL;
+  return rc(launch_pack(*w, packed, (hipStream_t)stream));
+}
+
+int ertd_timestep_embedding(const int64_t* t, int B, int dim, const float* freq, float* out,
+                            void* stream) {
+  if (!t || !freq || !out || B < 1 || dim < 4) return ERTD_EINVAL;
+  return rc(launch_timestep_embedding(t, B, dim, freq, out, (hipStream_t)stream));
+}
+
+int ertd_q_sample(const float* x0, const int64_t* t, const float* noise, const float* alpha_bar,
+                  int B, int P, float* out, void* stream) {
+  if (!x0 || !t || !noise || !alpha_bar || !out || B < 1 || P < 1) return ERTD_EINVAL;
+  return rc(launch_q_sample(x0, t, noise, alpha_bar, B, P, out, (hipStream_t)stream));
+}
+
+int ertd_encoder_fwd(const ertd_weights* w, const float* packed, const float* cond, int B, int L,
+                     int precision, float* cond_emb, void* ws, size_t ws_bytes, void* stream) {
+  if (!weights_ok(w) || !packed || !cond || !cond_emb || !ws || B < 1 || L < 1) return ERTD_EINVAL;
+  if (precision != ERTD_PREC_FP32 && precision != ERTD_PREC_BF16) return ERTD_EINVAL;
+  // the hoisted-mode prep kernel also yields cond_emb; U goes to a scratch slot after partial
+  const size_t need = ws_layout(B, L, 1, ERTD_OP_SAMPLE, nullptr, nullptr);
+  if (need > ws_bytes) return ERTD_ENOSPC;
+  Ws W;
+  ws_layout(B, L, 1, ERTD_OP_SAMPLE, ws, &W);
+  hipStream_t s = (hipStream_t)stream;
+  const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
+  ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, (long long)CIN * L, B, L,
+                                 precision, W.partial, s));
+  return rc(launch_hoist_prep(*w, packed, W.partial, S, L2, B, W.U, cond_emb, s));
+}
+
+int ertd_encoder_strips(const ertd_weights* w, const float* packed, const float* cond,
+                        long long cond_stride, int B, int L, int precision, void* ws,
+                        size_t ws_bytes, void* stream) {
+  if (!weights_ok(w) || !packed || !cond || !ws || B < 1 || L < 1) return ERTD_EINVAL;
+  if (precision != ERTD_PREC_FP32 && precision != ERTD_PREC_BF16) return ERTD_EINVAL;
+  if (cond_stride != 0 && cond_stride < (long long)CIN * L) return ERTD_EINVAL;
+  Ws W;
+  if (ws_layout(B, L, 0, ERTD_OP_FORWARD, ws, &W) > ws_bytes) return ERTD_ENOSPC;
+  return rc(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, cond_stride, B, L, precision,
+                                  W.partial, (hipStream_t)stream));
+}
+
+int ertd_forward(const ertd_weights* w, const float* packed, const float* x, const int64_t* t,
+                 const float* cond, int B, int L, const float* freq, int precision, float* out,
+                 float* cond_emb_out, float* t_emb_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!weights_ok(w) || !packed || !x || !t || !cond || !freq || !out || !ws || B < 1 || L < 1)
+    return ERTD_EINVAL;
+  if (precision != ERTD_PREC_FP32 && precision != ERTD_PREC_BF16) return ERTD_EINVAL;
+  Ws W;
+  if (ws_layout(B, L, 0, ERTD_OP_FORWARD, ws, &W) > ws_bytes) return ERTD_ENOSPC;
+  hipStream_t s = (hipStream_t)stream;
+  const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
+  ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, (long long)CIN * L, B, L,
+                                 precision, W.partial, s));
+  HeadArgs a{};
+  a.partial = W.partial;
+  a.S = S;
+  a.L2 = L2;
+  a.freq = freq;
+  a.x_in = x;
+  a.t_vec = t;
+  a.B = B;
+  a.eps_out = out;
+  a.cond_emb_out = cond_emb_out;
+  a.t_emb_out = t_emb_out;
+  return rc(launch_head(*w, packed, a, s));
+}
+
+int ertd_sample(const ertd_weights* w, const float* packed, const float* cond,
+                long long cond_stride, int B, int L, int num_steps, int t_first, int n_run,
+                const float* c1, const float* c2, const float* sigma, const float* freq,
+                const float* noise, uint64_t seed, uint32_t member_offset, int mode,
+                int precision, float* x_inout, void* ws, size_t ws_bytes, void* stream) {
+  return enqueue_sample(w, packed, cond, cond_stride, B, L, num_steps, t_first, n_run, c1, c2,
+                        sigma, freq, noise, seed, member_offset, mode, precision, x_inout, ws,
+                        ws_bytes, (hipStream_t)stream);
+}
+
+int ertd_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t, int tag,
+                       float* out, void* stream) {
+  if (!out || B < 1 || P < 1 || P > PMAX || t < 0) return ERTD_EINVAL;
+  return rc(launch_philox_normal(seed, member_offset, B, P, t, tag, out, (hipStream_t)stream));
+}
+
+int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const float* cond,
+                            long long cond_stride, int B, int L, int num_steps, int t_first,
+                            int n_run, const float* c1, const float* c2, const float* sigma,
+                            const float* freq, const float* noise, uint64_t seed,
+                            uint32_t member_offset, int mode, int precision, float* x_inout,
+                            void* ws, size_t ws_bytes, ertd_plan** plan) {
+  if (!plan) return ERTD_EINVAL;
+  *plan = nullptr;
+  ertd_plan* p = new (std::nothrow) ertd_plan();
+  if (!p) return ERTD_EINVAL;
+  hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete p;
+    return (int)e;
+  }
+  e = hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    ertd_plan_destroy(p);
+    return (int)e;
+  }
+  const int r = enqueue_sample(w, packed, cond, cond_stride, B, L, num_steps, t_first, n_run, c1,
+                               c2, sigma, freq, noise, seed, member_offset, mode, precision,
+                               x_inout, ws, ws_bytes, p->stream);
+  e = hipStreamEndCapture(p->stream, &p->graph);
+  if (r != ERTD_OK || e != hipSuccess) {
+    ertd_plan_destroy(p);
+    return r != ERTD_OK ? r : (int)e;
+  }
+  e = hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    ertd_plan_destroy(p);
+    return (int)e;
+  }
+  *plan = p;
+  return ERTD_OK;
+}
+
+int ertd_plan_launch(ertd_plan* plan, void* stream) {
+  if (!plan || !plan->exec) return ERTD_EINVAL;
+  return rc(hipGraphLaunch(plan->exec, (hipStream_t)stream));
+}
+
+int ertd_plan_destroy(ertd_plan* plan) {
+  if (!plan) return ERTD_OK;
+  if (plan->exec) (void)hipGraphExecDestroy(plan->exec);
+  if (plan->graph) (void)hipGraphDestroy(plan->graph);
+  if (plan->stream) (void)hipStreamDestroy(plan->stream);
+  delete plan;
+  return ERTD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,116 @@
+// Shared device helpers and launch declarations for libertdiff_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ertdiff.h"
+
+namespace ertd {
+
+// ---- model geometry (ERT_Conditional_Diffusion.py:133-153) -------------------
+constexpr int CIN = 14;        // ERT surveys = Conv1d in_channels
+constexpr int C1 = 32;         // conv1 out channels
+constexpr int C2 = 64;         // conv2 out channels
+constexpr int H = 128;         // hidden_dim
+constexpr int PMAX = 32;       // largest supported param_dim
+constexpr int K1 = CIN * 3;    // conv1 contraction (42)
+constexpr int K2 = C1 * 3;     // conv2 contraction (96)
+
+// ---- encoder strip geometry ---------------------------------------------------
+// One workgroup (4 waves) turns a strip of J conv2 outputs of one member into a
+// 64-channel partial pool sum.  conv2 output j needs conv1 outputs 2j-1..2j+1,
+// which need cond positions 4j-3..4j+3, so a strip starting at j0 reads cond
+// positions [4*j0-3, 4*j0-3+XU).
+constexpr int J = 63;          // conv2 outputs per strip (64-wide MFMA tile, 1 pad row)
+constexpr int XU = 4 * 65;     // cond positions staged per strip (260)
+constexpr int XS = 68;         // LDS row stride of the 4-phase cond image (floats)
+constexpr int HS = 68;         // LDS row stride of the conv1 even/odd images (floats)
+constexpr int STEPS1 = K1 / 2; // 32x32x2 MFMA k-steps for conv1 (21)
+constexpr int STEPS2 = K2 / 2; // ... for conv2 (48)
+// packed fragment-order weights: W1f[21][64] then W2f[2][48][64] (floats)
+constexpr int PACK_W1 = 0;
+constexpr int PACK_W2 = STEPS1 * 64;
+constexpr int PACK_FLOATS = PACK_W2 + 2 * STEPS2 * 64;
+// bf16 packing (second region): W1h[3][64] x 8 bf16, W2h[2][6][64] x 8 bf16
+constexpr int PACKH_OFF = PACK_FLOATS;                    // in floats
+constexpr int PACKH_W1_STEPS = 3;                         // ceil(42/16)
+constexpr int PACKH_W2_STEPS = 6;                         // 96/16
+constexpr int PACKH_FLOATS = (PACKH_W1_STEPS + 2 * PACKH_W2_STEPS) * 64 * 4;  // 8 bf16 = 4 floats
+constexpr int PACK_TOTAL = PACK_FLOATS + PACKH_FLOATS;
+
+__host__ __device__ constexpr int conv_len(int L) { return (L - 1) / 2 + 1; }
+__host__ __device__ constexpr int n_strips(int L2) { return (L2 + J - 1) / J; }
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+// ---- Philox4x32-10 counter RNG --------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)M0 * c.x;
+    const uint64_t p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// Standard normal for element `o` of member `member` at step `t`.  Counter
+// (o/4, member, t, tag), key = seed; Box-Muller on (x,y) and (z,w).
+__device__ inline float philox_normal(uint64_t seed, uint32_t member, uint32_t t, uint32_t tag, int o) {
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)(o >> 2), member, t, tag}, (uint32_t)seed,
+                                (uint32_t)(seed >> 32));
+  const bool second = (o & 2) != 0;
+  const uint32_t a = second ? r.z : r.x;
+  const uint32_t b = second ? r.w : r.y;
+  const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0,1]
+  const float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);           // [0,1)
+  const float rad = sqrtf(-2.0f * logf(u1));
+  float s, c;
+  sincospif(2.0f * u2, &s, &c);
+  return (o & 1) ? rad * s : rad * c;
+}
+
+// ---- launch declarations (defined in encoder.hip / head.hip / train.hip) ------
+// `packed` is the ertd_pack_weights() buffer (conv fragments + k-major dense weights).
+constexpr int DENSE_FLOATS = C2 * H + H * H + (PMAX + 2 * H) * H;
+constexpr int PACKED_FLOATS_ALL = PACK_TOTAL + DENSE_FLOATS;
+
+hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s);
+hipError_t launch_encoder_strips(const float* packed, const float* b1, const float* b2,
+                                 const float* cond, long long cstride, int B, int L,
+                                 int precision, float* partial, hipStream_t s);
+struct HeadArgs {
+  const float* partial; int S; int L2;
+  const float* freq;
+  const float* x_in; const int64_t* t_vec; int t_scalar;
+  const float* c1; const float* c2; const float* sigma; const float* noise;
+  int num_steps; uint64_t seed; uint32_t member_offset; int B;
+  float* x_out; float* eps_out; float* cond_emb_out; float* t_emb_out;
+};
+hipError_t launch_head(const ertd_weights& w, const float* packed, const HeadArgs& a, hipStream_t s);
+hipError_t launch_hoist_prep(const ertd_weights& w, const float* packed, const float* partial,
+                             int S, int L2, int B, float* U, float* cond_emb_out, hipStream_t s);
+hipError_t launch_time_table(const ertd_weights& w, const float* packed, const float* freq,
+                             int t_lo, int n, float* V, hipStream_t s);
+hipError_t launch_hoisted_sampler(const ertd_weights& w, const float* packed, const float* U,
+                                  const float* V, const float* c1, const float* c2,
+                                  const float* sigma, const float* noise, int num_steps,
+                                  int t_first, int n_run, uint64_t seed, uint32_t member_offset,
+                                  int B, float* x, hipStream_t s);
+hipError_t launch_timestep_embedding(const int64_t* t, int B, int dim, const float* freq,
+                                     float* out, hipStream_t s);
+hipError_t launch_q_sample(const float* x0, const int64_t* t, const float* noise,
+                           const float* alpha_bar, int B, int P, float* out, hipStream_t s);
+hipError_t launch_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t,
+                                int tag, float* out, hipStream_t s);
+
+}  // namespace ertd

@@ -1,0 +1,21 @@
+"""ertdiff -- MI355X (gfx950) drop-in for the denoising hot path of
+pnnl/ERT-Conditional-Diffusion-Model (ERT_Conditional_Diffusion.py).
+
+Same names, signatures and state_dict format as the reference module; the
+compute runs in hand-written HIP kernels (libertdiff_hip.so, C ABI in
+include/ertdiff.h).  There is no CPU fallback: device work on a non-gfx950
+device raises.
+"""
+from .data import (DiffusionDataset, bounds_mask, check_param_bounds, inverse_transform,
+                   load_best_model, save_checkpoint, transform_to_unconstrained)
+from .model import STATE_KEYS, ConditionalDiffusionModel, get_timestep_embedding, q_sample
+from .sampler import SamplerPlan, as_ertdiff_model, draw_reference_noise, philox_normal, sample_model
+from .schedule import get_diffusion_schedule, step_tables, timestep_frequencies
+
+__all__ = [
+    "ConditionalDiffusionModel", "get_timestep_embedding", "get_diffusion_schedule", "q_sample",
+    "sample_model", "SamplerPlan", "philox_normal", "draw_reference_noise", "as_ertdiff_model",
+    "step_tables", "timestep_frequencies", "transform_to_unconstrained", "inverse_transform",
+    "DiffusionDataset", "check_param_bounds", "bounds_mask", "load_best_model",
+    "save_checkpoint", "STATE_KEYS",
+]

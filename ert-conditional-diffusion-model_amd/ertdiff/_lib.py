@@ -1,0 +1,140 @@
+"""ctypes binding of libertdiff_hip.so (C ABI: include/ertdiff.h).
+
+torch is imported first on purpose: the torch wheel ships its own
+libamdhip64.so.7, and loading our library afterwards makes its NEEDED entry
+resolve to that already-loaded runtime, so streams and device pointers are
+shared with torch.
+
+There is no CPU fallback anywhere in the product: if the library is missing
+or no gfx950 device is visible, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch  # noqa: F401  (must precede the CDLL load, see above)
+
+LIB_NAME = "libertdiff_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+ERTD_OK = 0
+ERTD_EINVAL = -1
+ERTD_ENOSPC = -2
+ERTD_ENOGPU = -3
+OP_FORWARD, OP_SAMPLE, OP_TRAIN = 0, 1, 2
+MODE_HOISTED, MODE_FAITHFUL = 0, 1
+PREC_FP32, PREC_BF16 = 0, 1
+HIDDEN = 128
+PMAX = 32
+CIN = 14
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+
+
+class ErtdWeights(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "enc0_w", "enc0_b", "enc2_w", "enc2_b", "enc6_w", "enc6_b",
+        "time_w", "time_b", "mlp0_w", "mlp0_b", "mlp2_w", "mlp2_b")] + [
+        ("param_dim", ctypes.c_int), ("hidden_dim", ctypes.c_int)]
+
+
+# Exported symbol -> (restype, argtypes).  Every name declared in include/ertdiff.h.
+_VP, _I, _U32, _U64, _SZ, _F = (ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32,
+                                ctypes.c_uint64, ctypes.c_size_t, ctypes.c_float)
+_W = ctypes.POINTER(ErtdWeights)
+SIGNATURES = {
+    "ertd_version": (_I, []),
+    "ertd_error_string": (ctypes.c_char_p, [_I]),
+    "ertd_device_ok": (_I, []),
+    "ertd_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),
+    "ertd_packed_floats": (_SZ, []),
+    "ertd_pack_weights": (_I, [_W, _VP, _VP]),
+    "ertd_timestep_embedding": (_I, [_VP, _I, _I, _VP, _VP, _VP]),
+    "ertd_q_sample": (_I, [_VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
+    "ertd_encoder_fwd": (_I, [_W, _VP, _VP, _I, _I, _I, _VP, _VP, _SZ, _VP]),
+    "ertd_encoder_strips": (_I, [_W, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _VP, _SZ, _VP]),
+    "ertd_forward": (_I, [_W, _VP, _VP, _VP, _VP, _I, _I, _VP, _I, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "ertd_sample": (_I, [_W, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I, _VP, _VP, _VP, _VP,
+                         _VP, _U64, _U32, _I, _I, _VP, _VP, _SZ, _VP]),
+    "ertd_philox_normal": (_I, [_U64, _U32, _I, _I, _I, _I, _VP, _VP]),
+    "ertd_sample_plan_create": (_I, [_W, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I, _VP, _VP,
+                                     _VP, _VP, _VP, _U64, _U32, _I, _I, _VP, _VP, _SZ,
+                                     ctypes.POINTER(_VP)]),
+    "ertd_plan_launch": (_I, [_VP, _VP]),
+    "ertd_plan_destroy": (_I, [_VP]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the shared library and bind every exported symbol (CPU-safe)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        _load_error = (f"{LIB_NAME} not found at {path}; build it with "
+                       "`python ert-conditional-diffusion-model_amd/build.py`")
+        raise RuntimeError(_load_error)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib() -> ctypes.CDLL:
+    return load()
+
+
+def check(code: int, what: str) -> None:
+    if code != ERTD_OK:
+        msg = lib().ertd_error_string(code).decode()
+        raise RuntimeError(f"ertdiff: {what} failed ({code}): {msg}")
+
+
+_device_checked = {}
+
+
+def require_device(*tensors: torch.Tensor) -> torch.device:
+    """All tensors on one gfx950 device; raises otherwise (no CPU fallback)."""
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "ertdiff runs only on an MI355X (gfx950) device; got a tensor on "
+                f"'{t.device}'.  Move the model and inputs to 'cuda' first.")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"ertdiff: tensors on different devices ({dev} vs {t.device})")
+    if dev is None:
+        raise RuntimeError("ertdiff: no device tensor given")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _device_checked:
+        with torch.cuda.device(idx):
+            _device_checked[idx] = bool(lib().ertd_device_ok())
+    if not _device_checked[idx]:
+        raise RuntimeError(f"ertdiff: device {idx} is not a gfx950 (MI355X) GPU")
+    return torch.device("cuda", idx)
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def f32c(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"ertdiff: {name} must be float32, got {t.dtype}")
+    return t.contiguous()

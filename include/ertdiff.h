@@ -1,0 +1,163 @@
+/*
+ * ertdiff.h -- C ABI of libertdiff_hip.so, the MI355X (gfx950) implementation
+ * of the conditional-DDPM denoising hot path of pnnl/ERT-Conditional-Diffusion-Model.
+ *
+ * The reference has no native code and no FFI: its hot path is the Python call
+ * surface in ERT_Conditional_Diffusion.py.  Each entry point below replaces the
+ * ATen work behind one of those Python functions; the Python drop-in module
+ * (ert-conditional-diffusion-model_amd/ertdiff) binds them with ctypes, see
+ * INTEGRATION.md.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is DEVICE memory owned by the caller (torch tensors);
+ *     the library never allocates or frees device memory on these paths and
+ *     keeps no global state besides cached kernel handles;
+ *   - float tensors are fp32, row-major contiguous; timesteps are int64;
+ *   - work is enqueued on `stream` (a hipStream_t passed as void*) with no
+ *     host synchronisation, so calls may be captured into a hipGraph;
+ *   - return 0 on success, a negative ERTD_E* code for bad arguments (checked
+ *     on the host BEFORE anything is launched), or a positive hipError_t.
+ *
+ * Shapes: B = batch (members), L = measurements per survey (4693 in the
+ * reference), C_in = 14 surveys, P = param_dim (29 in the reference, 1..32
+ * supported), H = hidden_dim (128; the only value the reference uses).
+ */
+#ifndef ERTDIFF_H
+#define ERTDIFF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ERTD_OK 0
+#define ERTD_EINVAL (-1)   /* bad shape / null pointer / unsupported dim */
+#define ERTD_ENOSPC (-2)   /* workspace too small */
+#define ERTD_ENOGPU (-3)   /* no gfx950 device / kernel image unavailable */
+
+#define ERTD_CIN 14
+#define ERTD_HIDDEN 128
+#define ERTD_PMAX 32
+
+/* Pointers to the 12 state_dict tensors of ConditionalDiffusionModel
+ * (ERT_Conditional_Diffusion.py:133-153), in state_dict order.          */
+typedef struct ertd_weights {
+  const float* enc0_w; /* condition_encoder.0.weight (32,14,3)   */
+  const float* enc0_b; /* condition_encoder.0.bias   (32)        */
+  const float* enc2_w; /* condition_encoder.2.weight (64,32,3)   */
+  const float* enc2_b; /* condition_encoder.2.bias   (64)        */
+  const float* enc6_w; /* condition_encoder.6.weight (128,64)    */
+  const float* enc6_b; /* condition_encoder.6.bias   (128)       */
+  const float* time_w; /* time_embed.0.weight        (128,128)   */
+  const float* time_b; /* time_embed.0.bias          (128)       */
+  const float* mlp0_w; /* mlp.0.weight               (128,P+256) */
+  const float* mlp0_b; /* mlp.0.bias                 (128)       */
+  const float* mlp2_w; /* mlp.2.weight               (P,128)     */
+  const float* mlp2_b; /* mlp.2.bias                 (P)         */
+  int param_dim;       /* P */
+  int hidden_dim;      /* H, must be 128 */
+} ertd_weights;
+
+/* Workspace ops for ertd_workspace_bytes(). */
+#define ERTD_OP_FORWARD 0
+#define ERTD_OP_SAMPLE 1
+#define ERTD_OP_TRAIN 2
+
+/* Sampler modes. */
+#define ERTD_MODE_HOISTED 0  /* condition encoder once, persistent T-loop   */
+#define ERTD_MODE_FAITHFUL 1 /* encoder re-evaluated every step (reference) */
+
+/* Encoder operand precision. */
+#define ERTD_PREC_FP32 0
+#define ERTD_PREC_BF16 1 /* bf16 conv operands, fp32 accumulate/state */
+
+int ertd_version(void);
+const char* ertd_error_string(int code);
+/* 1 when a gfx950 device is visible and the kernels load, else 0. */
+int ertd_device_ok(void);
+
+/* Bytes of caller-provided device workspace an op needs.
+ * T = number of sampler steps (ignored for FORWARD).                      */
+size_t ertd_workspace_bytes(int B, int L, int P, int T, int op);
+/* Floats of packed (MFMA fragment-order) encoder weights. */
+size_t ertd_packed_floats(void);
+
+/* Re-lay the two Conv1d weights into MFMA fragment order (once per weight
+ * update).  packed: ertd_packed_floats() floats.                          */
+int ertd_pack_weights(const ertd_weights* w, float* packed, void* stream);
+
+/* get_timestep_embedding (ERT_Conditional_Diffusion.py:80-88) on device.
+ * freq: (dim/2) float32 frequencies exp(-i*ln(1e4)/(dim/2-1)) computed on the
+ * host with the reference's float32 expression; out: (B, dim).            */
+int ertd_timestep_embedding(const int64_t* t, int B, int dim, const float* freq,
+                            float* out, void* stream);
+
+/* q_sample (ERT_Conditional_Diffusion.py:96-99): out = sqrt(ab[t])*x0 + sqrt(1-ab[t])*noise. */
+int ertd_q_sample(const float* x0, const int64_t* t, const float* noise,
+                  const float* alpha_bar, int B, int P, float* out, void* stream);
+
+/* condition_encoder (ERT_Conditional_Diffusion.py:133-142): cond (B,14,L) ->
+ * cond_emb (B,128).                                                       */
+int ertd_encoder_fwd(const ertd_weights* w, const float* packed, const float* cond,
+                     int B, int L, int precision, float* cond_emb,
+                     void* ws, size_t ws_bytes, void* stream);
+
+/* The encoder's strip kernel alone (conv1 -> ReLU -> conv2 -> ReLU -> per-strip
+ * pool sums), writing partial (B, n_strips, 64) into ws.  This is the hot
+ * kernel of every step; exposed so callers can time it in isolation.      */
+int ertd_encoder_strips(const ertd_weights* w, const float* packed, const float* cond,
+                        long long cond_stride, int B, int L, int precision,
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* ConditionalDiffusionModel.forward (ERT_Conditional_Diffusion.py:155-164):
+ * x (B,P), t (B,) int64, cond (B,14,L) -> out (B,P).  freq as above (H/2).
+ * cond_emb_out / t_emb_out: optional (B,128) intermediates (NULL to skip). */
+int ertd_forward(const ertd_weights* w, const float* packed, const float* x,
+                 const int64_t* t, const float* cond, int B, int L, const float* freq,
+                 int precision, float* out, float* cond_emb_out, float* t_emb_out,
+                 void* ws, size_t ws_bytes, void* stream);
+
+/* sample_model's reverse loop (ERT_Conditional_Diffusion.py:107-119).
+ *   cond (B,14,L) with member stride cond_stride floats (14*L when each
+ *     member has its own condition, 0 when all members share one).
+ *   num_steps: schedule length n of the call (reference: num_steps or T).
+ *   Runs steps t = t_first, t_first-1, ..., t_first-n_run+1 (reference:
+ *     t_first = n-1, n_run = n); x_inout (B,P) carries the state in/out, so a
+ *     chain may be split into segments.
+ *   c1, c2, sigma: (num_steps) float32 per-step scalars, index t, formed on
+ *     the host with the reference's expressions (:111-118; sigma already
+ *     multiplied by temperature).
+ *   noise: NULL -> counter-based Philox keyed by (seed, member_offset+b, t);
+ *     else (num_steps, B, P) injected draws in reference order: noise[k] is
+ *     the z used at t = num_steps-k (noise[0] = x_T is not read).
+ *   mode: ERTD_MODE_HOISTED / ERTD_MODE_FAITHFUL (bit-identical outputs).  */
+int ertd_sample(const ertd_weights* w, const float* packed, const float* cond,
+                long long cond_stride, int B, int L, int num_steps, int t_first, int n_run,
+                const float* c1, const float* c2, const float* sigma, const float* freq,
+                const float* noise, uint64_t seed, uint32_t member_offset, int mode,
+                int precision, float* x_inout, void* ws, size_t ws_bytes, void* stream);
+
+/* Standard normals from the sampler's Philox stream: out (B,P) for members
+ * member_offset..+B-1 at step `t`, stream tag `tag` (0 = step noise z_t,
+ * 1 = initial x_T).                                                       */
+int ertd_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t,
+                       int tag, float* out, void* stream);
+
+/* hipGraph plans: capture one full ertd_sample call (all kernels of all
+ * steps) once, replay with ertd_plan_launch.  Buffers are bound at creation. */
+typedef struct ertd_plan ertd_plan;
+int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const float* cond,
+                            long long cond_stride, int B, int L, int num_steps, int t_first,
+                            int n_run, const float* c1, const float* c2, const float* sigma,
+                            const float* freq, const float* noise, uint64_t seed,
+                            uint32_t member_offset, int mode, int precision, float* x_inout,
+                            void* ws, size_t ws_bytes, ertd_plan** plan);
+int ertd_plan_launch(ertd_plan* plan, void* stream);
+int ertd_plan_destroy(ertd_plan* plan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ERTDIFF_H */

@@ -1,0 +1,148 @@
+"""Host-side logic of the product (CPU only): API surface, C-ABI exports,
+schedule tables, data transforms, checkpoint format, loud failure off-GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import ertdiff
+from ertdiff import _lib
+from conftest import ROOT
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    hdr = open(os.path.join(ROOT, "include", "ertdiff.h")).read()
+    declared = set(re.findall(r"\b(ertd_[a-z_0-9]+)\s*\(", hdr))
+    assert declared, "no entry points parsed from include/ertdiff.h"
+    for name in sorted(declared):
+        assert hasattr(lib, name), f"{name} declared in ertdiff.h but not exported"
+    assert declared == set(_lib.SIGNATURES), "ctypes bindings out of sync with the header"
+
+
+def test_library_host_queries():
+    lib = _lib.load()
+    assert lib.ertd_version() >= 1
+    assert lib.ertd_packed_floats() > 0
+    assert lib.ertd_error_string(-1).decode().startswith("invalid argument")
+    assert lib.ertd_workspace_bytes(0, 4693, 29, 10, 1) == 0
+    n64 = lib.ertd_workspace_bytes(64, 4693, 29, 1000, _lib.OP_SAMPLE)
+    # partial pool sums: 64 members x 19 strips x 64 channels + U + V + cond_emb
+    assert n64 >= 4 * (64 * 19 * 64 + 64 * 128 + 1000 * 128 + 64 * 128)
+    assert lib.ertd_workspace_bytes(64, 4693, 29, 0, _lib.OP_FORWARD) < n64
+
+
+def test_invalid_args_rejected_before_launch():
+    lib = _lib.load()
+    w = _lib.ErtdWeights()  # null pointers
+    assert lib.ertd_pack_weights(w, None, None) == _lib.ERTD_EINVAL
+    assert lib.ertd_q_sample(None, None, None, None, 4, 29, None, None) == _lib.ERTD_EINVAL
+    assert lib.ertd_philox_normal(1, 0, 0, 29, 0, 0, None, None) == _lib.ERTD_EINVAL
+
+
+def test_state_dict_and_init_match_reference(golden_weights):
+    torch.manual_seed(42)
+    m = ertdiff.ConditionalDiffusionModel(param_dim=29, hidden_dim=128)
+    sd = m.state_dict()
+    assert list(sd.keys()) == list(golden_weights.keys()) == ertdiff.STATE_KEYS
+    for k, v in golden_weights.items():
+        assert np.array_equal(sd[k].numpy(), v), k
+    assert sum(p.numel() for p in m.parameters()) == 72765
+    # Adam indexes parameters by position: same order as the reference module
+    assert [n for n, _ in m.named_parameters()] == ertdiff.STATE_KEYS
+
+
+def test_no_cpu_fallback(golden_weights):
+    m = ertdiff.ConditionalDiffusionModel(29, 128)
+    x = torch.zeros(2, 29)
+    t = torch.zeros(2, dtype=torch.long)
+    c = torch.zeros(2, 14, 50)
+    with torch.no_grad(), pytest.raises(RuntimeError, match="gfx950"):
+        m(x, t, c)
+    with pytest.raises(RuntimeError, match="gfx950"):
+        ertdiff.get_timestep_embedding(t, 128)
+    with pytest.raises(RuntimeError, match="gfx950"):
+        ertdiff.q_sample(x, t, x, torch.ones(10))
+    b, a, ab = ertdiff.get_diffusion_schedule(10)
+    with pytest.raises(RuntimeError, match="gfx950"):
+        ertdiff.sample_model(m, c, 10, b, a, ab, 29, "cpu")
+
+
+@pytest.mark.parametrize("T", [50, 500, 1000])
+def test_schedule_and_step_tables(T, sched_kat):
+    b, a, ab = ertdiff.get_diffusion_schedule(T, beta_start=1e-4, beta_end=0.02)
+    assert np.array_equal(b.numpy(), sched_kat[f"T{T}_betas"])
+    assert np.array_equal(ab.numpy(), sched_kat[f"T{T}_alpha_bar"])
+    tab = ertdiff.step_tables(b, a, ab, T, temperature=1.0).numpy()
+    assert np.array_equal(tab[0], sched_kat[f"T{T}_c1"].astype(np.float32))
+    assert np.array_equal(tab[1], sched_kat[f"T{T}_c2"])
+    assert np.array_equal(tab[2], sched_kat[f"T{T}_sigma"].astype(np.float32))
+
+
+def test_update_rule_fp32_semantics(sched_kat):
+    """The device update c1*(x - c2*eps) + sigma*z with float32 c1/sigma (one
+    rounding per op) reproduces torch's scalar arithmetic bit for bit."""
+    import math
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((64, 29)).astype(np.float32)
+    eps = rng.standard_normal((64, 29)).astype(np.float32)
+    z = rng.standard_normal((64, 29)).astype(np.float32)
+    b, a, ab = ertdiff.get_diffusion_schedule(1000)
+    tab = ertdiff.step_tables(b, a, ab, 1000, temperature=0.7).numpy()
+    for t_ in (999, 500, 1):
+        coef = (1 - a[t_]) / (math.sqrt(1 - ab[t_]) + 1e-8)
+        ref = (1.0 / math.sqrt(a[t_])) * (torch.from_numpy(x) - coef * torch.from_numpy(eps))
+        ref = ref + math.sqrt(b[t_]) * 0.7 * torch.from_numpy(z)
+        c1, c2, sg = (np.float32(v) for v in tab[:, t_])
+        got = c1 * (x - c2 * eps) + sg * z  # numpy float32: one rounding per op
+        assert np.array_equal(got, ref.numpy())
+
+
+def test_freq_table_matches_reference_expression(fwd_kat):
+    f = ertdiff.schedule._freq_cpu(128)
+    t = torch.from_numpy(fwd_kat["temb_t"])
+    emb = torch.cat([torch.sin(t.float()[:, None] * f[None]), torch.cos(t.float()[:, None] * f[None])], 1)
+    assert torch.equal(emb, torch.from_numpy(fwd_kat["temb_dim128"]))
+
+
+def test_transforms_and_bounds(postproc_kat):
+    k = postproc_kat
+    assert np.array_equal(ertdiff.transform_to_unconstrained(k["x"], 0.0, 1.0), k["unc"])
+    assert np.array_equal(ertdiff.inverse_transform(k["unc"], 0.0, 1.0), k["inv"])
+    xt = torch.from_numpy(k["xt"])
+    assert torch.equal(ertdiff.transform_to_unconstrained(xt, 0.0, 1.0), torch.from_numpy(k["unc_t"]))
+    assert torch.equal(ertdiff.inverse_transform(torch.from_numpy(k["unc_t"]), 0.0, 1.0),
+                       torch.from_numpy(k["inv_t"]))
+    valid = ertdiff.check_param_bounds(k["sets"], k["limits"], verbose=False)
+    assert np.array_equal(valid, k["valid"])
+    assert ertdiff.check_param_bounds(k["sets"][~k["mask"]], k["limits"], verbose=False) is None
+
+
+def test_dataset_contract():
+    rng = np.random.default_rng(3)
+    params = rng.uniform(0, 1, (5, 29, 1))
+    ert = rng.uniform(0, 1, (5, 4693, 14)).astype(np.float32)
+    ds = ertdiff.DiffusionDataset(params, ert)
+    x0, c = ds[2]
+    assert x0.shape == (29,) and c.shape == (14, 4693)
+    assert torch.equal(c, torch.from_numpy(ert[2].T.copy()))
+    batch = torch.utils.data.default_collate([ds[i] for i in range(3)])
+    assert batch[1].is_contiguous() and batch[1].shape == (3, 14, 4693)
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    torch.manual_seed(0)
+    m = ertdiff.ConditionalDiffusionModel(29)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    path = tmp_path / "best_model.pt"
+    ertdiff.save_checkpoint(path, m, opt, epoch=3, best_val_loss=0.25, train_history=[1.0, 0.5],
+                            val_history=[0.9, 0.25], param_dim=29)
+    m2 = ertdiff.ConditionalDiffusionModel(29)
+    opt2 = torch.optim.Adam(m2.parameters(), lr=1e-4)
+    ck = ertdiff.load_best_model(path, m2, opt2)
+    assert set(ck) == {"epoch", "model_state_dict", "optimizer_state_dict", "best_val_loss",
+                       "train_history", "val_history", "param_dim"}
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, m2.state_dict()[k])
