@@ -75,7 +75,7 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
     ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, cstride, B, L, precision,
                                    W.partial, s));
     ERTD_TRY(launch_hoist_prep(*w, packed, W.partial, S, L2, B, W.U, W.cond_emb, s));
-    ERTD_TRY(launch_time_table(*w, packed, freq, t_last, n_run, W.V + (size_t)t_last * H, s));
+    ERTD_TRY(launch_time_table(*w, packed, freq, t_last, n_run, W.V, s));
     ERTD_TRY(launch_hoisted_sampler(*w, packed, W.U, W.V, c1, c2, sigma, noise, num_steps, t_first,
                                     n_run, seed, member_offset, B, x_inout, s));
     return ERTD_OK;

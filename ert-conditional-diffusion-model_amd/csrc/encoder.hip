@@ -95,12 +95,40 @@ hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // fp32 strip kernel
 // ---------------------------------------------------------------------------
+// The cond image is dead once conv1's MFMAs have run, so the conv1 output
+// images alias it: 17.9 KB per workgroup -> 8 workgroups (32 waves) per CU.
 struct EncSmem {
-  float X[4][CIN][XS];  // 4-phase cond image (15,232 B)
-  float E[C1][HS];      // conv1 output, even p (8,704 B)
-  float O[C1][HS];      // conv1 output, odd p  (8,704 B) -- must follow E
-  float red[2][C2];     // q-tile partial pool sums
+  union {
+    float X[4][CIN][XS];  // 4-phase cond image (15,232 B)
+    struct {
+      float E[C1][HS];    // conv1 output, even p (8,704 B)
+      float O[C1][HS];    // conv1 output, odd p  (8,704 B) -- must follow E
+    };
+  };
+  float red[2][C2];       // q-tile partial pool sums
 };
+
+// Stage cond[b][:, pos0 : pos0+260] into X[u&3][c][u>>2] (zero outside [0,L)).
+// Thread tid owns u = tid for all 14 channels (+ u = 256..259 on threads 0..55):
+// every load is issued before the first LDS write.
+template <typename Tx, typename Cvt>
+__device__ __forceinline__ void stage_cond(Tx (*X)[CIN][XS], const float* __restrict__ cb, int L,
+                                           int pos0, int tid, Cvt cvt) {
+  float v[CIN];
+  const int pos = pos0 + tid;
+  const bool in = pos >= 0 && pos < L;
+#pragma unroll
+  for (int c = 0; c < CIN; ++c) v[c] = in ? cb[(size_t)c * L + pos] : 0.f;
+  float vt = 0.f;
+  const int tc = tid >> 2, tu = 256 + (tid & 3);
+  if (tid < CIN * 4) {
+    const int p2 = pos0 + tu;
+    vt = (p2 >= 0 && p2 < L) ? cb[(size_t)tc * L + p2] : 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < CIN; ++c) X[tid & 3][c][tid >> 2] = cvt(v[c]);
+  if (tid < CIN * 4) X[tu & 3][tc][tu >> 2] = cvt(vt);
+}
 
 template <int PAR>
 __device__ __forceinline__ void conv1_tile(f32x16& acc, const float (&a1)[STEPS1], const float* xb) {
@@ -135,17 +163,10 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
 
   // ---- stage cond[b][:, 4j0-3 : 4j0-3+260] into the 4-phase image (zero padded)
   const float* cb = cond + (long long)b * cstride;
-  const int pos0 = 4 * j0 - 3;
-  for (int idx = tid; idx < CIN * XU; idx += 256) {
-    const int c = idx / XU, u = idx - c * XU;
-    const int pos = pos0 + u;
-    const float v = (pos >= 0 && pos < L) ? cb[(size_t)c * L + pos] : 0.f;
-    sm.X[u & 3][c][u >> 2] = v;
-  }
-  if (tid < C1) sm.E[tid][64] = 0.f;  // read only by the pad row q=63
+  stage_cond(sm.X, cb, L, 4 * j0 - 3, tid, [](float v) { return v; });
   __syncthreads();
 
-  // ---- conv1 + bias + ReLU -> E / O (never leaves LDS)
+  // ---- conv1 + bias + ReLU -> E / O (never leaves LDS; aliases X)
   {
     const int par = wave >> 1, mt = wave & 1;
     const int m = mt * 32 + l32;
@@ -153,6 +174,8 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
     const float* xb = &sm.X[0][0][0] + 7 * h * XS + m;
     if (par == 0) conv1_tile<0>(acc, a1, xb);
     else conv1_tile<1>(acc, a1, xb);
+    __syncthreads();  // every wave has read X: the images may now overwrite it
+    if (tid < C1) sm.E[tid][64] = 0.f;  // read only by the pad row q=63
     float* dst = par ? &sm.O[0][0] : &sm.E[0][0];
     const int i = 2 * j0 - 1 + 2 * m + par;       // global conv1 position
     const bool valid = (i >= 0) && (i < L1);      // outside -> conv2's zero padding
@@ -210,9 +233,13 @@ __device__ __forceinline__ unsigned short f2bf(float v) {
 }
 
 struct EncSmemH {
-  unsigned short X[4][CIN][XS];  // 4-phase cond image, bf16
-  unsigned short E[C1][HS];
-  unsigned short O[C1][HS];
+  union {
+    unsigned short X[4][CIN][XS];  // 4-phase cond image, bf16
+    struct {
+      unsigned short E[C1][HS];
+      unsigned short O[C1][HS];
+    };
+  };
   float red[2][C2];
 };
 
@@ -231,14 +258,7 @@ __global__ __launch_bounds__(256) void enc_bf16_kernel(const float* __restrict__
   const bf16x8* ph = reinterpret_cast<const bf16x8*>(packed + PACKH_OFF);
 
   const float* cb = cond + (long long)b * cstride;
-  const int pos0 = 4 * j0 - 3;
-  for (int idx = tid; idx < CIN * XU; idx += 256) {
-    const int c = idx / XU, u = idx - c * XU;
-    const int pos = pos0 + u;
-    const float v = (pos >= 0 && pos < L) ? cb[(size_t)c * L + pos] : 0.f;
-    sm.X[u & 3][c][u >> 2] = f2bf(v);
-  }
-  if (tid < C1) sm.E[tid][64] = 0;
+  stage_cond(sm.X, cb, L, 4 * j0 - 3, tid, [](float v) { return f2bf(v); });
   __syncthreads();
 
   // conv1: A = W1 (row o = l32, k = 16*st + 8h + e), B = X[k][m]
@@ -260,6 +280,8 @@ __global__ __launch_bounds__(256) void enc_bf16_kernel(const float* __restrict__
       }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc, 0, 0, 0);
     }
+    __syncthreads();  // X fully consumed before the aliased images are written
+    if (tid < C1) sm.E[tid][64] = 0;
     unsigned short* dst = par ? &sm.O[0][0] : &sm.E[0][0];
     const int i = 2 * j0 - 1 + 2 * m + par;
     const bool valid = (i >= 0) && (i < L1);

@@ -30,19 +30,43 @@ __device__ __forceinline__ DenseT dense_ptrs(const float* packed) {
   return d;
 }
 
-// out_j = init + sum_{k<N} WT[k][j] * v[k]: sequential fma chain in k.
+// ---- dense layers: 2-way split-k ------------------------------------------------
+// Each output j of a 128-wide layer is produced by two threads q = 0, 1: thread q
+// runs a sequential fma chain over k in [q*N/2, (q+1)*N/2) (q = 0 starts from the
+// bias), the two partials are added (p0 + p1).  The weights of a thread's half
+// are loaded into registers at kernel start, so a whole layer costs one global
+// latency round.  Faithful head, hoist_prep and time_table all use these
+// functions with the same (j, q) layout: bit-identical results.
 template <int N>
-__device__ __forceinline__ float dotT(const float* __restrict__ WT, const float* v, float init, int j) {
+struct HalfW {
+  float w[N / 2];
+};
+template <int N>
+__device__ __forceinline__ void load_half(HalfW<N>& r, const float* __restrict__ WT, int j, int q) {
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) r.w[k] = WT[(q * (N / 2) + k) * H + j];
+}
+template <int N>
+__device__ __forceinline__ float chain_half(const HalfW<N>& r, const float* v, float init, int q) {
   float acc = init;
-#pragma unroll 16
-  for (int k = 0; k < N; ++k) acc = fmaf(WT[k * H + j], v[k], acc);
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) acc = fmaf(r.w[k], v[q * (N / 2) + k], acc);
   return acc;
 }
 
-// Pool finish: mean over L2 of the per-strip sums, strips summed in order.
-__device__ __forceinline__ float pool_mean(const float* __restrict__ partial, int b, int S, int L2, int c) {
+// Pool finish: 8 interleaved strip groups (group g sums strips g, g+8, ...),
+// combined in group order, divided by L2.
+constexpr int POOL_GROUPS = 8;
+__device__ __forceinline__ float pool_group(const float* __restrict__ partial, int b, int S, int c,
+                                            int g) {
   float acc = 0.f;
-  for (int s = 0; s < S; ++s) acc += partial[((size_t)b * S + s) * C2 + c];
+  for (int s = g; s < S; s += POOL_GROUPS) acc += partial[((size_t)b * S + s) * C2 + c];
+  return acc;
+}
+__device__ __forceinline__ float pool_combine(const float (*pg)[C2], int c, int L2) {
+  float acc = pg[0][c];
+#pragma unroll
+  for (int g = 1; g < POOL_GROUPS; ++g) acc += pg[g][c];
   return acc / (float)L2;
 }
 
@@ -53,39 +77,46 @@ __device__ __forceinline__ float sinusoid(float tf, const float* __restrict__ fr
   return k < half ? sinf(a) : cosf(a);
 }
 
-// cond_emb_j and u_j (thread j < 128); m in LDS.
-__device__ __forceinline__ float cond_emb_j(const DenseT& d, const ertd_weights& w, const float* m, int j) {
-  return fmaxf(dotT<C2>(d.W3T, m, w.enc6_b[j], j), 0.f);
+// Weights of the condition branch (cond_emb, u) and of the time branch (t_emb, v).
+struct CondW {
+  HalfW<C2> w3;  // condition_encoder.6
+  HalfW<H> w0c;  // mlp.0, cond_emb columns
+};
+struct TimeW {
+  HalfW<H> wt;   // time_embed.0
+  HalfW<H> w0t;  // mlp.0, t_emb columns
+};
+__device__ __forceinline__ void load_cond_w(CondW& r, const DenseT& d, int P, int j, int q) {
+  load_half<C2>(r.w3, d.W3T, j, q);
+  load_half<H>(r.w0c, d.W0T + (size_t)(P + H) * H, j, q);
 }
-__device__ __forceinline__ float u_j(const DenseT& d, const ertd_weights& w, const float* c, int j) {
-  return dotT<H>(d.W0T + (size_t)(w.param_dim + H) * H, c, w.mlp0_b[j], j);
-}
-// t_emb_j and v_j (thread j < 128); e / te in LDS.
-__device__ __forceinline__ float t_emb_j(const DenseT& d, const ertd_weights& w, const float* e, int j) {
-  return fmaxf(dotT<H>(d.WtT, e, w.time_b[j], j), 0.f);
-}
-__device__ __forceinline__ float v_j(const DenseT& d, const ertd_weights& w, const float* te, int j) {
-  return dotT<H>(d.W0T + (size_t)w.param_dim * H, te, 0.f, j);
+__device__ __forceinline__ void load_time_w(TimeW& r, const DenseT& d, int P, int j, int q) {
+  load_half<H>(r.wt, d.WtT, j, q);
+  load_half<H>(r.w0t, d.W0T + (size_t)P * H, j, q);
 }
 
 // ---- per-wave step body --------------------------------------------------------
+// One wave per member.  Lane l holds hidden units l and l+64 of mlp.0 and, for
+// mlp.2, output o = l>>1 over the k-half (l&1): eps_o is one 64-term fma chain
+// per half against h broadcast from LDS, the halves joined by one lane swap
+// (a commutative add, so both lanes of a pair hold identical bits).
 struct StepRegs {
   float w0x_lo[PMAX], w0x_hi[PMAX];  // W0[lane][k], W0[lane+64][k]  (k < P)
-  float w2_lo[PMAX], w2_hi[PMAX];    // W2[o][lane], W2[o][lane+64]  (o < P)
+  float w2h[H / 2];                  // W2[lane>>1][64*(lane&1) + k]  (o < P)
   float bo;                          // b2[lane>>1]
 };
 
 __device__ __forceinline__ void load_step_regs(StepRegs& R, const float* __restrict__ W0T,
                                                const float* __restrict__ W2,
                                                const float* __restrict__ b2, int P, int lane) {
+  const int o = lane >> 1, half = lane & 1;
 #pragma unroll
   for (int k = 0; k < PMAX; ++k) {
     R.w0x_lo[k] = k < P ? W0T[k * H + lane] : 0.f;
     R.w0x_hi[k] = k < P ? W0T[k * H + 64 + lane] : 0.f;
-    R.w2_lo[k] = k < P ? W2[k * H + lane] : 0.f;
-    R.w2_hi[k] = k < P ? W2[k * H + 64 + lane] : 0.f;
   }
-  const int o = lane >> 1;
+#pragma unroll
+  for (int k = 0; k < H / 2; ++k) R.w2h[k] = o < P ? W2[o * H + 64 * half + k] : 0.f;
   R.bo = o < P ? b2[o] : 0.f;
 }
 
@@ -97,8 +128,9 @@ __device__ __forceinline__ void broadcast_x(float (&xs)[PMAX], float xv, int P) 
 }
 
 // eps for o = lane>>1 given the pre-activations of hidden units lane, lane+64.
+// hbuf: this wave's 128-float LDS scratch.
 __device__ __forceinline__ float step_eps(const StepRegs& R, float w_lo, float w_hi,
-                                          const float (&xs)[PMAX], int P, int lane) {
+                                          const float (&xs)[PMAX], int P, int lane, float* hbuf) {
   float a_lo = w_lo, a_hi = w_hi;
 #pragma unroll
   for (int k = 0; k < PMAX; ++k) {
@@ -107,25 +139,16 @@ __device__ __forceinline__ float step_eps(const StepRegs& R, float w_lo, float w
       a_hi = fmaf(R.w0x_hi[k], xs[k], a_hi);
     }
   }
-  const float h_lo = fmaxf(a_lo, 0.f), h_hi = fmaxf(a_hi, 0.f);
-  // per-lane partials of all 32 outputs, then a fixed butterfly reduce-scatter:
-  // level i pairs lane bit (5-i) with output bit (4-i); lane l ends with o = l>>1.
-  float v[32];
+  hbuf[lane] = fmaxf(a_lo, 0.f);
+  hbuf[64 + lane] = fmaxf(a_hi, 0.f);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const float* hh = hbuf + 64 * (lane & 1);
+  float acc = 0.f;
 #pragma unroll
-  for (int o = 0; o < 32; ++o) v[o] = fmaf(R.w2_hi[o], h_hi, R.w2_lo[o] * h_lo);
-#pragma unroll
-  for (int lvl = 0; lvl < 5; ++lvl) {
-    const int n = 16 >> lvl;
-    const int lb = 5 - lvl;
-    const bool up = (lane >> lb) & 1;
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-      const float keep = up ? v[n + i] : v[i];
-      const float send = up ? v[i] : v[n + i];
-      v[i] = keep + __shfl_xor(send, 1 << lb);
-    }
-  }
-  const float e = v[0] + __shfl_xor(v[0], 1);
+  for (int k = 0; k < H / 2; ++k) acc = fmaf(R.w2h[k], hh[k], acc);
+  const float e = acc + __shfl_xor(acc, 1);
   return e + R.bo;
 }
 
@@ -147,57 +170,126 @@ __device__ __forceinline__ float step_noise(const float* __restrict__ noise, int
 }
 
 struct HeadSmem {
+  float pg[POOL_GROUPS][C2];   // pool group sums
   float m[C2];
   float e[H];
   float c[H];
   float te[H];
-  float u[H];
-  float v[H];
+  float part[2][2][H];         // [branch][q][j] split-k partials
+  float w[H];                  // u + v
+  float hbuf[H];               // step body scratch (wave 0)
+  float w0x[PMAX][H];          // x columns of mlp.0 (k-major)
+  float w2f[H / 2][64];        // mlp.2 in step-lane order: [k][lane] = W2[lane>>1][64*(lane&1)+k]
 };
 
+constexpr int HEAD_THREADS = 512;
+
+// Phase stamps for the diagnostic build only (tools/diag_head.hip defines
+// ERTD_HEAD_STAMPS); the library build compiles them out.
+#ifdef ERTD_HEAD_STAMPS
+__device__ unsigned long long g_head_stamps[1024][2][8];
+#define HEAD_STAMP(i)                                                                   \
+  do {                                                                                  \
+    if ((threadIdx.x & 255) == 0)                                                       \
+      g_head_stamps[blockIdx.x][threadIdx.x >> 8][i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define HEAD_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
-// head_kernel: one workgroup per member; full head for timestep t.
+// head_kernel: one 512-thread workgroup per member; full head for timestep t.
 //   forward mode (eps_out != null): eps_out = model(x, t, cond)
 //   step mode    (x_out  != null): one faithful DDPM step
-// Threads 0..127 run the condition branch, 128..255 the time branch.
+// Threads 0..255: condition branch (j = tid&127, q = tid>>7), 256..511: time
+// branch.  Every weight a thread needs is requested at kernel start.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void head_kernel(ertd_weights w, const float* __restrict__ packed,
-                                                   HeadArgs a) {
+__global__ __launch_bounds__(HEAD_THREADS) void head_kernel(ertd_weights w,
+                                                            const float* __restrict__ packed,
+                                                            HeadArgs a) {
   __shared__ HeadSmem sm;
   const int P = w.param_dim;
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool cond_br = tid < 256;
+  const int j = tid & (H - 1), q = (tid >> 7) & 1;
   const DenseT d = dense_ptrs(packed);
   const int64_t t = a.t_vec ? a.t_vec[b] : (int64_t)a.t_scalar;
+  HEAD_STAMP(0);
 
-  if (tid < C2) sm.m[tid] = pool_mean(a.partial, b, a.S, a.L2, tid);
-  if (tid >= H) sm.e[tid - H] = sinusoid((float)t, a.freq, tid - H);
+  // ---- issue every load up front ------------------------------------------------
+  CondW cw;
+  TimeW tw;
+  if (cond_br) load_cond_w(cw, d, P, j, q);
+  else load_time_w(tw, d, P, j, q);
+  for (int i = tid; i < PMAX * H; i += HEAD_THREADS) {
+    const int k = i / H;
+    sm.w0x[0][i] = k < P ? d.W0T[i] : 0.f;
+    const int kk = i >> 6, ln = i & 63, o = ln >> 1;  // conflict-free lane-major image
+    sm.w2f[0][i] = o < P ? w.mlp2_w[o * H + 64 * (ln & 1) + kk] : 0.f;
+  }
+  {
+    const int c = tid & (C2 - 1), g = tid >> 6;
+    sm.pg[g][c] = pool_group(a.partial, b, a.S, c, g);
+  }
+  const float bias_c = (cond_br && q == 0) ? w.enc6_b[j] : 0.f;
+  const float bias_u = (cond_br && q == 0) ? w.mlp0_b[j] : 0.f;
+  const float bias_t = (!cond_br && q == 0) ? w.time_b[j] : 0.f;
+  if (!cond_br && q == 0) sm.e[j] = sinusoid((float)t, a.freq, j);
   __syncthreads();
+  HEAD_STAMP(1);
+
+  // ---- layer 1: cond_emb (64 -> 128), t_emb (128 -> 128) -------------------------
+  if (tid < C2) sm.m[tid] = pool_combine(sm.pg, tid, a.L2);
+  __syncthreads();
+  HEAD_STAMP(2);
+  if (cond_br) sm.part[0][q][j] = chain_half<C2>(cw.w3, sm.m, bias_c, q);
+  else sm.part[1][q][j] = chain_half<H>(tw.wt, sm.e, bias_t, q);
+  __syncthreads();
+  HEAD_STAMP(3);
   if (tid < H) {
-    const float c = cond_emb_j(d, w, sm.m, tid);
-    sm.c[tid] = c;
-    if (a.cond_emb_out) a.cond_emb_out[(size_t)b * H + tid] = c;
-  } else {
-    const int j = tid - H;
-    const float te = t_emb_j(d, w, sm.e, j);
+    const float c = fmaxf(sm.part[0][0][j] + sm.part[0][1][j], 0.f);
+    sm.c[j] = c;
+    if (a.cond_emb_out) a.cond_emb_out[(size_t)b * H + j] = c;
+  } else if (tid >= 256 && tid < 256 + H) {
+    const float te = fmaxf(sm.part[1][0][j] + sm.part[1][1][j], 0.f);
     sm.te[j] = te;
     if (a.t_emb_out) a.t_emb_out[(size_t)b * H + j] = te;
   }
   __syncthreads();
-  if (tid < H) sm.u[tid] = u_j(d, w, sm.c, tid);
-  else sm.v[tid - H] = v_j(d, w, sm.te, tid - H);
+
+  // ---- layer 2: u = b0 + W0c.c, v = W0t.te --------------------------------------
+  if (cond_br) sm.part[0][q][j] = chain_half<H>(cw.w0c, sm.c, bias_u, q);
+  else sm.part[1][q][j] = chain_half<H>(tw.w0t, sm.te, 0.f, q);
   __syncthreads();
+  if (tid < H) {
+    const float u = sm.part[0][0][j] + sm.part[0][1][j];
+    const float v = sm.part[1][0][j] + sm.part[1][1][j];
+    sm.w[j] = u + v;
+  }
+  __syncthreads();
+  HEAD_STAMP(4);
   if (wave != 0) return;
 
+  // ---- step body (one wave) --------------------------------------------------------
   StepRegs R;
-  load_step_regs(R, d.W0T, w.mlp2_w, w.mlp2_b, P, lane);
   const int o = lane >> 1;
+#pragma unroll
+  for (int k = 0; k < PMAX; ++k) {
+    R.w0x_lo[k] = sm.w0x[k][lane];
+    R.w0x_hi[k] = sm.w0x[k][64 + lane];
+  }
+#pragma unroll
+  for (int k = 0; k < H / 2; ++k) R.w2h[k] = sm.w2f[k][lane];
+  R.bo = o < P ? w.mlp2_b[o] : 0.f;
   float xv = o < P ? a.x_in[(size_t)b * P + o] : 0.f;
   float xs[PMAX];
   broadcast_x(xs, xv, P);
-  const float w_lo = sm.u[lane] + sm.v[lane];
-  const float w_hi = sm.u[lane + 64] + sm.v[lane + 64];
-  const float eps = step_eps(R, w_lo, w_hi, xs, P, lane);
+  HEAD_STAMP(5);
+  const float eps = step_eps(R, sm.w[lane], sm.w[lane + 64], xs, P, lane, sm.hbuf);
+  HEAD_STAMP(6);
   if (a.eps_out) {
     if (!(lane & 1) && o < P) a.eps_out[(size_t)b * P + o] = eps;
     return;
@@ -207,56 +299,84 @@ __global__ __launch_bounds__(256) void head_kernel(ertd_weights w, const float* 
                              a.member_offset + (uint32_t)b);
   xv = ddpm_update(xv, eps, a.c1[ts], a.c2[ts], a.sigma[ts], z, ts > 0);
   if (!(lane & 1) && o < P) a.x_out[(size_t)b * P + o] = xv;
+  HEAD_STAMP(7);
 }
 
 hipError_t launch_head(const ertd_weights& w, const float* packed, const HeadArgs& a, hipStream_t s) {
-  head_kernel<<<a.B, 256, 0, s>>>(w, packed, a);
+  head_kernel<<<a.B, HEAD_THREADS, 0, s>>>(w, packed, a);
   return hipGetLastError();
 }
 
 // ---- hoisted-mode precomputation ------------------------------------------------
-// U[b][j] = b0_j + W0c.relu(W3.mean + b3)   (one 128-thread block per member)
-__global__ __launch_bounds__(128) void hoist_prep_kernel(ertd_weights w, const float* __restrict__ packed,
+// U[b][j] = b0_j + W0c.relu(W3.mean + b3)   (one 256-thread block per member)
+__global__ __launch_bounds__(256) void hoist_prep_kernel(ertd_weights w, const float* __restrict__ packed,
                                                          const float* __restrict__ partial, int S,
                                                          int L2, float* __restrict__ U,
                                                          float* __restrict__ cond_emb_out) {
+  __shared__ float pg[POOL_GROUPS][C2];
   __shared__ float m[C2];
   __shared__ float c[H];
-  const int b = blockIdx.x, j = threadIdx.x;
+  __shared__ float part[2][H];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int j = tid & (H - 1), q = tid >> 7;
   const DenseT d = dense_ptrs(packed);
-  if (j < C2) m[j] = pool_mean(partial, b, S, L2, j);
+  CondW cw;
+  load_cond_w(cw, d, w.param_dim, j, q);
+  for (int i = tid; i < POOL_GROUPS * C2; i += 256) {
+    const int cc = i & (C2 - 1), g = i >> 6;
+    pg[g][cc] = pool_group(partial, b, S, cc, g);
+  }
+  const float bias_c = q == 0 ? w.enc6_b[j] : 0.f;
+  const float bias_u = q == 0 ? w.mlp0_b[j] : 0.f;
   __syncthreads();
-  const float cj = cond_emb_j(d, w, m, j);
-  c[j] = cj;
-  if (cond_emb_out) cond_emb_out[(size_t)b * H + j] = cj;
+  if (tid < C2) m[tid] = pool_combine(pg, tid, L2);
   __syncthreads();
-  U[(size_t)b * H + j] = u_j(d, w, c, j);
+  part[q][j] = chain_half<C2>(cw.w3, m, bias_c, q);
+  __syncthreads();
+  if (tid < H) {
+    const float cj = fmaxf(part[0][j] + part[1][j], 0.f);
+    c[j] = cj;
+    if (cond_emb_out) cond_emb_out[(size_t)b * H + j] = cj;
+  }
+  __syncthreads();
+  part[q][j] = chain_half<H>(cw.w0c, c, bias_u, q);
+  __syncthreads();
+  if (tid < H) U[(size_t)b * H + j] = part[0][j] + part[1][j];
 }
 
-// V[t][j] = W0t.relu(Wt.sinusoid(t) + bt)   (one 128-thread block per timestep)
-__global__ __launch_bounds__(128) void time_table_kernel(ertd_weights w, const float* __restrict__ packed,
+// V[t][j] = W0t.relu(Wt.sinusoid(t) + bt)   (one 256-thread block per timestep)
+__global__ __launch_bounds__(256) void time_table_kernel(ertd_weights w, const float* __restrict__ packed,
                                                          const float* __restrict__ freq, int t_lo,
                                                          float* __restrict__ V) {
   __shared__ float e[H];
   __shared__ float te[H];
-  const int t = t_lo + (int)blockIdx.x, j = threadIdx.x;
+  __shared__ float part[2][H];
+  const int t = t_lo + (int)blockIdx.x, tid = threadIdx.x;
+  const int j = tid & (H - 1), q = tid >> 7;
   const DenseT d = dense_ptrs(packed);
-  e[j] = sinusoid((float)t, freq, j);
+  TimeW tw;
+  load_time_w(tw, d, w.param_dim, j, q);
+  const float bias_t = q == 0 ? w.time_b[j] : 0.f;
+  if (q == 0) e[j] = sinusoid((float)t, freq, j);
   __syncthreads();
-  te[j] = t_emb_j(d, w, e, j);
+  part[q][j] = chain_half<H>(tw.wt, e, bias_t, q);
   __syncthreads();
-  V[(size_t)t * H + j] = v_j(d, w, te, j);
+  if (tid < H) te[j] = fmaxf(part[0][j] + part[1][j], 0.f);
+  __syncthreads();
+  part[q][j] = chain_half<H>(tw.w0t, te, 0.f, q);
+  __syncthreads();
+  if (tid < H) V[(size_t)t * H + j] = part[0][j] + part[1][j];
 }
 
 hipError_t launch_hoist_prep(const ertd_weights& w, const float* packed, const float* partial,
                              int S, int L2, int B, float* U, float* cond_emb_out, hipStream_t s) {
-  hoist_prep_kernel<<<B, 128, 0, s>>>(w, packed, partial, S, L2, U, cond_emb_out);
+  hoist_prep_kernel<<<B, 256, 0, s>>>(w, packed, partial, S, L2, U, cond_emb_out);
   return hipGetLastError();
 }
 
 hipError_t launch_time_table(const ertd_weights& w, const float* packed, const float* freq,
                              int t_lo, int n, float* V, hipStream_t s) {
-  time_table_kernel<<<n, 128, 0, s>>>(w, packed, freq, t_lo, V);
+  time_table_kernel<<<n, 256, 0, s>>>(w, packed, freq, t_lo, V);
   return hipGetLastError();
 }
 
@@ -269,9 +389,10 @@ __global__ __launch_bounds__(256) void hoisted_sampler_kernel(
     const float* __restrict__ V, const float* __restrict__ c1, const float* __restrict__ c2,
     const float* __restrict__ sigma, const float* __restrict__ noise, int num_steps, int t_first,
     int n_run, uint64_t seed, uint32_t member_offset, int B, float* __restrict__ x) {
+  __shared__ float hbuf[4][H];
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;  // whole wave exits together
+  if (b >= B) return;  // whole wave exits together (no block barriers below)
   const int P = w.param_dim;
   const DenseT d = dense_ptrs(packed);
   StepRegs R;
@@ -287,7 +408,7 @@ __global__ __launch_bounds__(256) void hoisted_sampler_kernel(
     const float w_lo = u_lo + V[(size_t)t * H + lane];
     const float w_hi = u_hi + V[(size_t)t * H + 64 + lane];
     const float z = step_noise(noise, num_steps, t, B, b, P, o, seed, member);
-    const float eps = step_eps(R, w_lo, w_hi, xs, P, lane);
+    const float eps = step_eps(R, w_lo, w_hi, xs, P, lane, hbuf[threadIdx.x >> 6]);
     xv = ddpm_update(xv, eps, c1[t], c2[t], sigma[t], z, t > 0);
   }
   if (!(lane & 1) && o < P) x[(size_t)b * P + o] = xv;

@@ -1,0 +1,84 @@
+"""Multi-process host logic of the sharded ensemble on CPU
+with the gloo backend, world_size 2 and 3.  The device sampler is replaced by
+a deterministic stand-in keyed by global member id (the property the HIP
+Philox stream has), so these tests check partitioning, the single condition
+broadcast and the gather -- not numerics (those are in test_gpu_parity)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ertdiff.ensemble import member_range, sample_ensemble
+
+
+def test_member_range_partition():
+    for n in (0, 1, 7, 64, 1024, 1025):
+        for world in (1, 2, 3, 4, 8):
+            spans = [member_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+class _Model:
+    param_dim = 5
+
+
+def fake_sampler(model, cond, T, betas, alphas, alpha_bar, P, device, *, num_steps, temperature,
+                 mode, noise, seed, member_offset, shared_condition, n_members):
+    assert shared_condition and noise == "philox" and cond.shape[0] == 1
+    ids = torch.arange(member_offset, member_offset + n_members, dtype=torch.float32)
+    # depends on the condition content, the seed and the GLOBAL member id only
+    return (cond.sum() + seed + ids[:, None] * 10 + torch.arange(P)[None, :]).float()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n_members, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = 37
+        cond = torch.arange(14 * L, dtype=torch.float32).reshape(14, L) / 100 if rank == 0 else None
+        out = sample_ensemble(_Model(), cond, n_members, 10, None, None, None, seed=3, L=L,
+                              device=torch.device("cpu"), _sampler=fake_sampler)
+        shard = sample_ensemble(_Model(), cond, n_members, 10, None, None, None, seed=3, L=L,
+                                device=torch.device("cpu"), gather=False, _sampler=fake_sampler)
+        q.put((rank, out.numpy(), shard.shape[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_members", [(2, 16), (2, 7), (3, 10)])
+def test_sharded_ensemble_gloo(world, n_members):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_members, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    L = 37
+    cond = torch.arange(14 * L, dtype=torch.float32).reshape(1, 14, L) / 100
+    expect = fake_sampler(_Model(), cond, 10, None, None, None, 5, None, num_steps=None,
+                          temperature=1.0, mode="hoisted", noise="philox", seed=3,
+                          member_offset=0, shared_condition=True, n_members=n_members).numpy()
+    for rank, out, nloc in sorted(res, key=lambda r: r[0]):
+        assert (out == expect).all(), f"rank {rank} gathered ensemble differs from the unsharded one"
+        lo, hi = member_range(n_members, world, rank)
+        assert nloc == hi - lo
