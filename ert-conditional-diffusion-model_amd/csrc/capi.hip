@@ -139,6 +139,10 @@ int ertd_device_ok(void) {
 size_t ertd_workspace_bytes(int B, int L, int P, int T, int op) {
   (void)P;
   if (B < 1 || L < 1) return 0;
+  if (op == ERTD_OP_TRAIN) {
+    int offs[5];
+    return train_ws_floats(B, L, offs) * sizeof(float);
+  }
   return ws_layout(B, L, T, op, nullptr, nullptr);
 }
 
@@ -280,6 +284,64 @@ int ertd_plan_destroy(ertd_plan* plan) {
   if (plan->stream) (void)hipStreamDestroy(plan->stream);
   delete plan;
   return ERTD_OK;
+}
+
+static bool grads_ok(float* const* g) {
+  if (!g) return false;
+  for (int k = 0; k < 12; ++k)
+    if (!g[k]) return false;
+  return true;
+}
+
+int ertd_train_forward(const ertd_weights* w, float* packed, const float* x, const float* x0,
+                       const float* noise, const float* alpha_bar, const int64_t* t,
+                       const float* cond, int B, int L, const float* freq, float* eps_out,
+                       void* ws, size_t ws_bytes, void* stream) {
+  if (!weights_ok(w) || !packed || !t || !cond || !freq || !ws || B < 1 || L < 1) return ERTD_EINVAL;
+  if (!x && (!x0 || !noise || !alpha_bar)) return ERTD_EINVAL;
+  int offs[5];
+  if (train_ws_floats(B, L, offs) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+  hipStream_t s = (hipStream_t)stream;
+  ERTD_TRY(launch_pack(*w, packed, s));
+  return rc(launch_train_forward(*w, packed, x, x0, noise, alpha_bar, t, cond, B, L, freq, eps_out,
+                                 (float*)ws, s));
+}
+
+int ertd_train_backward(const ertd_weights* w, const float* packed, const float* dout,
+                        const float* noise, const float* cond, int B, int L, float* const* grads,
+                        float* loss_out, float* dx_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!weights_ok(w) || !packed || !cond || !grads_ok(grads) || !ws || B < 1 || L < 1)
+    return ERTD_EINVAL;
+  if (!dout && (!noise || !loss_out)) return ERTD_EINVAL;
+  int offs[5];
+  if (train_ws_floats(B, L, offs) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+  return rc(launch_train_backward(*w, packed, dout, noise, cond, B, L, grads, loss_out, dx_out,
+                                  (float*)ws, (hipStream_t)stream));
+}
+
+int ertd_adam(const ertd_weights* w, float* const* grads, float* const* exp_avg,
+              float* const* exp_avg_sq, int step, float lr, float beta1, float beta2, float eps,
+              void* stream) {
+  if (!weights_ok(w) || !grads_ok(grads) || !grads_ok(exp_avg) || !grads_ok(exp_avg_sq) || step < 1)
+    return ERTD_EINVAL;
+  return rc(launch_adam(*w, grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps,
+                        (hipStream_t)stream));
+}
+
+int ertd_train_step(const ertd_weights* w, float* packed, const float* x0, const int64_t* t,
+                    const float* noise, const float* cond, const float* alpha_bar, int B, int L,
+                    const float* freq, float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
+                    float eps, float* loss_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!x0 || !noise || !alpha_bar || !loss_out) return ERTD_EINVAL;
+  if (!grads_ok(exp_avg) || !grads_ok(exp_avg_sq) || step < 1) return ERTD_EINVAL;
+  int r = ertd_train_forward(w, packed, nullptr, x0, noise, alpha_bar, t, cond, B, L, freq,
+                             nullptr, ws, ws_bytes, stream);
+  if (r != ERTD_OK) return r;
+  r = ertd_train_backward(w, packed, nullptr, noise, cond, B, L, grads, loss_out, nullptr, ws,
+                          ws_bytes, stream);
+  if (r != ERTD_OK) return r;
+  return ertd_adam(w, grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, stream);
 }
 
 }  // extern "C"

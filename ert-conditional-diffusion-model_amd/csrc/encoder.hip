@@ -85,10 +85,20 @@ __global__ __launch_bounds__(256) void pack_dense_kernel(ertd_weights w, float* 
   }
 }
 
+__global__ __launch_bounds__(256) void pack_w2b_kernel(ertd_weights w, float* __restrict__ packed) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= W2B_FLOATS) return;
+  const int kk = idx / (32 * 64), r = idx % (32 * 64);
+  const int st = r >> 6, l = r & 63;
+  const int o = 2 * st + (l >> 5), c = l & 31;
+  packed[PACK_W2B + idx] = w.enc2_w[(o * C1 + c) * 3 + kk];
+}
+
 hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s) {
   pack_kernel<<<(PACK_TOTAL + 255) / 256, 256, 0, s>>>(w, packed);
   const int n = C2 * H + H * H + (w.param_dim + 2 * H) * H;
   pack_dense_kernel<<<(n + 255) / 256, 256, 0, s>>>(w, packed);
+  pack_w2b_kernel<<<(W2B_FLOATS + 255) / 256, 256, 0, s>>>(w, packed);
   return hipGetLastError();
 }
 
@@ -108,28 +118,6 @@ struct EncSmem {
   float red[2][C2];       // q-tile partial pool sums
 };
 
-// Stage cond[b][:, pos0 : pos0+260] into X[u&3][c][u>>2] (zero outside [0,L)).
-// Thread tid owns u = tid for all 14 channels (+ u = 256..259 on threads 0..55):
-// every load is issued before the first LDS write.
-template <typename Tx, typename Cvt>
-__device__ __forceinline__ void stage_cond(Tx (*X)[CIN][XS], const float* __restrict__ cb, int L,
-                                           int pos0, int tid, Cvt cvt) {
-  float v[CIN];
-  const int pos = pos0 + tid;
-  const bool in = pos >= 0 && pos < L;
-#pragma unroll
-  for (int c = 0; c < CIN; ++c) v[c] = in ? cb[(size_t)c * L + pos] : 0.f;
-  float vt = 0.f;
-  const int tc = tid >> 2, tu = 256 + (tid & 3);
-  if (tid < CIN * 4) {
-    const int p2 = pos0 + tu;
-    vt = (p2 >= 0 && p2 < L) ? cb[(size_t)tc * L + p2] : 0.f;
-  }
-#pragma unroll
-  for (int c = 0; c < CIN; ++c) X[tid & 3][c][tid >> 2] = cvt(v[c]);
-  if (tid < CIN * 4) X[tu & 3][tc][tu >> 2] = cvt(vt);
-}
-
 template <int PAR>
 __device__ __forceinline__ void conv1_tile(f32x16& acc, const float (&a1)[STEPS1], const float* xb) {
 #pragma unroll
@@ -144,13 +132,18 @@ __device__ __forceinline__ void conv1_tile(f32x16& acc, const float (&a1)[STEPS1
   }
 }
 
+// TRAIN additionally stores what the backward needs (train.hip): the conv1
+// activations a1 (B,32,L1) at the conv1 positions this strip owns,
+// i in [2*j0, 2*j0 + 2J), and the conv2 ReLU mask m2 (B,64,L2) as bytes.
+template <bool TRAIN>
 __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__ packed,
                                                        const float* __restrict__ b1,
                                                        const float* __restrict__ b2,
                                                        const float* __restrict__ cond,
                                                        long long cstride, int L, int L1, int L2,
-                                                       int S,
-                                                       float* __restrict__ partial) {
+                                                       int S, float* __restrict__ partial,
+                                                       float* __restrict__ a1out,
+                                                       unsigned char* __restrict__ m2out) {
   __shared__ EncSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
@@ -187,6 +180,14 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
     }
   }
   __syncthreads();
+  if constexpr (TRAIN) {  // owned conv1 positions i = 2*j0 + r, r < 2J  (p = r + 1)
+    float* a1b = a1out + (size_t)b * C1 * L1;
+    for (int idx = tid; idx < C1 * 2 * J; idx += 256) {
+      const int c = idx / (2 * J), r = idx - c * (2 * J);
+      const int i = 2 * j0 + r;
+      if (i < L1) a1b[(size_t)c * L1 + i] = (r & 1) ? sm.E[c][(r + 1) >> 1] : sm.O[c][r >> 1];
+    }
+  }
 
   // ---- conv2 + bias + ReLU + masked column sum
   {
@@ -210,8 +211,12 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
     for (int r = 0; r < 16; ++r) {
       const int qq = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       const bool valid = (qq < J) && (j0 + qq < L2);
-      const float v = fmaxf(acc[r] + bias, 0.f);
+      const float z = acc[r] + bias;
+      const float v = fmaxf(z, 0.f);
       sum += valid ? v : 0.f;
+      if constexpr (TRAIN) {
+        if (valid) m2out[((size_t)b * C2 + o) * L2 + j0 + qq] = z > 0.f ? 1 : 0;
+      }
     }
     sum += __shfl_xor(sum, 32);
     if (h == 0) sm.red[qt][o] = sum;
@@ -337,7 +342,17 @@ hipError_t launch_encoder_strips(const float* packed, const float* b1, const flo
   if (precision == ERTD_PREC_BF16)
     enc_bf16_kernel<<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S, partial);
   else
-    enc_fp32_kernel<<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S, partial);
+    enc_fp32_kernel<false><<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S,
+                                                 partial, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_encoder_train(const float* packed, const float* b1, const float* b2,
+                                const float* cond, int B, int L, float* partial, float* a1,
+                                unsigned char* m2, hipStream_t s) {
+  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
+  enc_fp32_kernel<true><<<dim3((unsigned)(B * S)), 256, 0, s>>>(
+      packed, b1, b2, cond, (long long)CIN * L, L, L1, L2, S, partial, a1, m2);
   return hipGetLastError();
 }
 

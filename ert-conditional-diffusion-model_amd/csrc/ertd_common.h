@@ -79,12 +79,46 @@ __device__ inline float philox_normal(uint64_t seed, uint32_t member, uint32_t t
   return (o & 1) ? rad * s : rad * c;
 }
 
+// Stage cond[b][:, pos0 : pos0+260] into X[u&3][c][u>>2] (zero outside [0,L)).
+// Thread tid owns u = tid for all 14 channels (+ u = 256..259 on threads 0..55):
+// every load is issued before the first LDS write.
+template <typename Tx, typename Cvt>
+__device__ __forceinline__ void stage_cond(Tx (*X)[CIN][XS], const float* __restrict__ cb, int L,
+                                           int pos0, int tid, Cvt cvt) {
+  float v[CIN];
+  const int pos = pos0 + tid;
+  const bool in = pos >= 0 && pos < L;
+#pragma unroll
+  for (int c = 0; c < CIN; ++c) v[c] = in ? cb[(size_t)c * L + pos] : 0.f;
+  float vt = 0.f;
+  const int tc = tid >> 2, tu = 256 + (tid & 3);
+  if (tid < CIN * 4) {
+    const int p2 = pos0 + tu;
+    vt = (p2 >= 0 && p2 < L) ? cb[(size_t)tc * L + p2] : 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < CIN; ++c) X[tid & 3][c][tid >> 2] = cvt(v[c]);
+  if (tid < CIN * 4) X[tu & 3][tc][tu >> 2] = cvt(vt);
+}
+
+__device__ __forceinline__ void stage_cond_f32(float (*X)[CIN][XS], const float* __restrict__ cb,
+                                               int L, int pos0, int tid) {
+  stage_cond(X, cb, L, pos0, tid, [](float v) { return v; });
+}
+
 // ---- launch declarations (defined in encoder.hip / head.hip / train.hip) ------
 // `packed` is the ertd_pack_weights() buffer (conv fragments + k-major dense weights).
 constexpr int DENSE_FLOATS = C2 * H + H * H + (PMAX + 2 * H) * H;
-constexpr int PACKED_FLOATS_ALL = PACK_TOTAL + DENSE_FLOATS;
+// conv2 transposed-conv fragments for the backward (train.hip):
+// W2B[kk][s][lane] = W2[o = 2s + (lane>>5)][c = lane&31][kk]
+constexpr int PACK_W2B = PACK_TOTAL + DENSE_FLOATS;
+constexpr int W2B_FLOATS = 3 * 32 * 64;
+constexpr int PACKED_FLOATS_ALL = PACK_W2B + W2B_FLOATS;
 
 hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s);
+hipError_t launch_encoder_train(const float* packed, const float* b1, const float* b2,
+                                const float* cond, int B, int L, float* partial, float* a1,
+                                unsigned char* m2, hipStream_t s);
 hipError_t launch_encoder_strips(const float* packed, const float* b1, const float* b2,
                                  const float* cond, long long cstride, int B, int L,
                                  int precision, float* partial, hipStream_t s);
@@ -112,5 +146,18 @@ hipError_t launch_q_sample(const float* x0, const int64_t* t, const float* noise
                            const float* alpha_bar, int B, int P, float* out, hipStream_t s);
 hipError_t launch_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t,
                                 int tag, float* out, hipStream_t s);
+// train.hip
+size_t train_ws_floats(int B, int L, int* offs);
+hipError_t launch_train_forward(const ertd_weights& w, const float* packed, const float* x_in,
+                                const float* x0, const float* noise, const float* alpha_bar,
+                                const int64_t* t, const float* cond, int B, int L,
+                                const float* freq, float* eps_out, float* ws, hipStream_t s);
+hipError_t launch_train_backward(const ertd_weights& w, const float* packed, const float* dout,
+                                 const float* noise, const float* cond, int B, int L,
+                                 float* const* grads, float* loss_out, float* dx_out, float* ws,
+                                 hipStream_t s);
+hipError_t launch_adam(const ertd_weights& w, float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
+                       float eps, hipStream_t s);
 
 }  // namespace ertd

@@ -11,11 +11,14 @@ from .data import (DiffusionDataset, bounds_mask, check_param_bounds, inverse_tr
 from .model import STATE_KEYS, ConditionalDiffusionModel, get_timestep_embedding, q_sample
 from .sampler import SamplerPlan, as_ertdiff_model, draw_reference_noise, philox_normal, sample_model
 from .schedule import get_diffusion_schedule, step_tables, timestep_frequencies
+from .train import DiffusionForwardFn, train_step, validation_loss
+from .ensemble import member_range, sample_ensemble
 
 __all__ = [
     "ConditionalDiffusionModel", "get_timestep_embedding", "get_diffusion_schedule", "q_sample",
     "sample_model", "SamplerPlan", "philox_normal", "draw_reference_noise", "as_ertdiff_model",
     "step_tables", "timestep_frequencies", "transform_to_unconstrained", "inverse_transform",
     "DiffusionDataset", "check_param_bounds", "bounds_mask", "load_best_model",
-    "save_checkpoint", "STATE_KEYS",
+    "save_checkpoint", "STATE_KEYS", "train_step", "validation_loss", "DiffusionForwardFn",
+    "sample_ensemble", "member_range",
 ]

@@ -62,6 +62,12 @@ SIGNATURES = {
     "ertd_sample_plan_create": (_I, [_W, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I, _VP, _VP,
                                      _VP, _VP, _VP, _U64, _U32, _I, _I, _VP, _VP, _SZ,
                                      ctypes.POINTER(_VP)]),
+    "ertd_train_forward": (_I, [_W, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _SZ,
+                                _VP]),
+    "ertd_train_backward": (_I, [_W, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "ertd_adam": (_I, [_W, _VP, _VP, _VP, _I, _F, _F, _F, _F, _VP]),
+    "ertd_train_step": (_I, [_W, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _I, _F,
+                             _F, _F, _F, _VP, _VP, _SZ, _VP]),
     "ertd_plan_launch": (_I, [_VP, _VP]),
     "ertd_plan_destroy": (_I, [_VP]),
 }
@@ -132,6 +138,13 @@ def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 
 def stream_of(dev: torch.device) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
+
+
+def ptr_array(tensors) -> ctypes.c_void_p:
+    """float* const* argument: a C array of device pointers (kept alive by the caller)."""
+    arr = (ctypes.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+    ptr_array._keep = arr  # outlives the synchronous ctypes call
+    return ctypes.cast(arr, ctypes.c_void_p)
 
 
 def f32c(t: torch.Tensor, name: str) -> torch.Tensor:

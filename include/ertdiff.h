@@ -157,6 +157,41 @@ int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const fl
 int ertd_plan_launch(ertd_plan* plan, void* stream);
 int ertd_plan_destroy(ertd_plan* plan);
 
+/* ---- training (ERT_Conditional_Diffusion.py:305-320) ---------------------------
+ * Workspace: ertd_workspace_bytes(B, L, P, 0, ERTD_OP_TRAIN).  The forward
+ * stores the activations the backward reads there: keep it between the two.
+ * grads / exp_avg / exp_avg_sq: 12 device buffers in state_dict order with the
+ * parameters' shapes.  The parameters are the (mutable) pointers of `w`.    */
+
+/* Training forward: eps = model(x, t, cond) with activations saved in ws.
+ * x (B,P), or x == NULL and x0/noise/alpha_bar given: x = q_sample(x0, t, noise)
+ * (:314).  Re-packs the weights into `packed` first (they change every step). */
+int ertd_train_forward(const ertd_weights* w, float* packed, const float* x, const float* x0,
+                       const float* noise, const float* alpha_bar, const int64_t* t,
+                       const float* cond, int B, int L, const float* freq, float* eps_out,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* Backward of the last ertd_train_forward on `ws`.  dout (B,P) = dL/deps, or
+ * NULL with `noise`: L = MSELoss(mean)(eps, noise) (:295, :316), loss_out (1).
+ * dx_out (B,P) optional.  grads are overwritten (not accumulated).          */
+int ertd_train_backward(const ertd_weights* w, const float* packed, const float* dout,
+                        const float* noise, const float* cond, int B, int L, float* const* grads,
+                        float* loss_out, float* dx_out, void* ws, size_t ws_bytes, void* stream);
+
+/* torch.optim.Adam step (no weight decay / amsgrad) on the 12 parameters of w,
+ * in place.  step = the step count after this update (>= 1).               */
+int ertd_adam(const ertd_weights* w, float* const* grads, float* const* exp_avg,
+              float* const* exp_avg_sq, int step, float lr, float beta1, float beta2, float eps,
+              void* stream);
+
+/* The reference train step (:309-319) in one call: q_sample -> forward ->
+ * MSELoss -> backward -> Adam.  loss_out (1) float32 on device.            */
+int ertd_train_step(const ertd_weights* w, float* packed, const float* x0, const int64_t* t,
+                    const float* noise, const float* cond, const float* alpha_bar, int B, int L,
+                    const float* freq, float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
+                    float eps, float* loss_out, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

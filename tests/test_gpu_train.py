@@ -1,0 +1,139 @@
+"""GPU train step (ERT_Conditional_Diffusion.py:309-319) vs the golden vectors
+of the reference's own train step (fixed t / noise, seed-42 weights, 3 Adam
+steps) and vs the float64 hand-derived backward.  fp32 tolerances: loss 1e-5
+rel, gradients 1e-4 rel-L2 per tensor (the reference's own fp32 gradients sit
+up to 3.3e-5 from float64), Adam parameter deltas 1e-3 rel-L2 (tiny gradients
+make m/sqrt(v) sign-sensitive)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import ertdiff
+from oracle import ref_numpy as RN
+from synth import synth_normal, synth_timesteps, synth_uniform
+
+pytestmark = pytest.mark.gpu
+GRAD_TOL = 1e-4
+
+
+def _fresh_model(golden_weights, dev):
+    m = ertdiff.ConditionalDiffusionModel(29, 128)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_weights.items()})
+    return m.to(dev).train()
+
+
+def _rel(a, b):
+    return RN.rel_l2(a.detach().double().cpu().numpy(), np.asarray(b, np.float64))
+
+
+def test_train_step_vs_golden(golden_weights, train_kat, cuda_dev):
+    m = _fresh_model(golden_weights, cuda_dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    T = int(train_kat["T"])
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    x0 = torch.from_numpy(train_kat["x0"]).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((8, 14, 4693), int(train_kat["cs"]))).to(cuda_dev)
+    for step in range(3):
+        t = torch.from_numpy(train_kat[f"t{step}"]).to(cuda_dev)
+        noise = torch.from_numpy(train_kat[f"noise{step}"]).to(cuda_dev)
+        loss = ertdiff.train_step(m, opt, x0, cond, T, ab, t=t, noise=noise)
+        ref = float(train_kat[f"loss{step}"])
+        assert abs(loss - ref) <= 1e-5 * abs(ref), (step, loss, ref)
+        if step == 0:
+            for k, p in m.named_parameters():
+                assert _rel(p.grad, train_kat[f"grad0/{k}"]) < GRAD_TOL, k
+        if step in (0, 2):
+            for k, p in m.named_parameters():
+                d = p.detach().double().cpu().numpy() - golden_weights[k]
+                dref = train_kat[f"param{step}/{k}"].astype(np.float64) - golden_weights[k]
+                assert RN.rel_l2(d, dref) < 1e-3, (step, k)
+    # Adam state is torch's: step counters and buffers round-trip through state_dict
+    sd = opt.state_dict()
+    assert float(sd["state"][0]["step"]) == 3.0
+    opt2 = torch.optim.Adam(ertdiff.ConditionalDiffusionModel(29).parameters(), lr=1e-4)
+    opt2.load_state_dict(sd)
+
+
+def test_autograd_backward_vs_golden(golden_weights, train_kat, cuda_dev):
+    m = _fresh_model(golden_weights, cuda_dev)
+    x = torch.from_numpy(train_kat["x_noisy0"]).to(cuda_dev).requires_grad_(True)
+    t = torch.from_numpy(train_kat["t0"]).to(cuda_dev)
+    noise = torch.from_numpy(train_kat["noise0"]).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((8, 14, 4693), int(train_kat["cs"]))).to(cuda_dev)
+    pred = m(x, t, cond)
+    assert _rel(pred, train_kat["pred0"]) < 1e-5
+    loss = F.mse_loss(pred, noise)
+    assert abs(loss.item() - float(train_kat["loss0"])) <= 1e-5 * float(train_kat["loss0"])
+    loss.backward()
+    for k, p in m.named_parameters():
+        assert _rel(p.grad, train_kat[f"grad0/{k}"]) < GRAD_TOL, k
+    # dL/dx against the float64 backward
+    W = golden_weights
+    f = RN.forward_full(train_kat["x_noisy0"], train_kat["t0"],
+                        synth_uniform((8, 14, 4693), int(train_kat["cs"])), W)
+    dout = 2.0 * (f["out"] - train_kat["noise0"]) / f["out"].size
+    dz5 = (dout @ W["mlp.2.weight"].astype(np.float64)) * (f["z5"] > 0)
+    dx_ref = dz5 @ W["mlp.0.weight"].astype(np.float64)[:, :29]
+    assert _rel(x.grad, dx_ref) < GRAD_TOL
+
+
+def test_fused_step_equals_autograd_grads(golden_weights, cuda_dev):
+    """train_step's fused path and the autograd path run the same kernels."""
+    B, L, T = 6, 700, 500
+    x0 = torch.from_numpy(synth_normal((B, 29), 201)).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 202)).to(cuda_dev)
+    t = torch.from_numpy(synth_timesteps(B, T, 203)).to(cuda_dev)
+    noise = torch.from_numpy(synth_normal((B, 29), 204)).to(cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    m1 = _fresh_model(golden_weights, cuda_dev)
+    opt = torch.optim.Adam(m1.parameters(), lr=1e-4)
+    ertdiff.train_step(m1, opt, x0, cond, T, ab, t=t, noise=noise)
+    g1 = {k: p.grad.clone() for k, p in m1.named_parameters()}
+    m2 = _fresh_model(golden_weights, cuda_dev)
+    x = ertdiff.q_sample(x0, t, noise, ab)
+    F.mse_loss(m2(x, t, cond), noise).backward()
+    for k, p in m2.named_parameters():
+        assert torch.equal(p.grad, g1[k]), k
+
+
+@pytest.mark.parametrize("B,L", [(3, 37), (5, 250), (2, 1), (4, 4693), (32, 4693)])
+def test_grads_vs_fp64_backward(B, L, golden_weights, cuda_dev):
+    x = synth_normal((B, 29), 300 + L)
+    t = synth_timesteps(B, 500, 301 + L)
+    noise = synth_normal((B, 29), 302 + L)
+    cond = synth_uniform((B, 14, L), 303 + L)
+    m = _fresh_model(golden_weights, cuda_dev)
+    xd = torch.from_numpy(x).to(cuda_dev)
+    loss = F.mse_loss(m(xd, torch.from_numpy(t).to(cuda_dev), torch.from_numpy(cond).to(cuda_dev)),
+                      torch.from_numpy(noise).to(cuda_dev))
+    loss.backward()
+    f = RN.forward_full(x, t, cond, golden_weights)
+    ref_loss, g = RN.backward(f, noise, golden_weights)
+    assert abs(loss.item() - ref_loss) < 1e-5 * ref_loss
+    for k, p in m.named_parameters():
+        if np.linalg.norm(g[k]) == 0:
+            assert float(p.grad.abs().max()) == 0.0, k
+            continue
+        assert _rel(p.grad, g[k]) < GRAD_TOL, (k, _rel(p.grad, g[k]))
+
+
+def test_train_step_deterministic(golden_weights, cuda_dev):
+    B, L, T = 32, 4693, 500
+    x0 = torch.from_numpy(synth_normal((B, 29), 401)).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 402)).to(cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    outs = []
+    for _ in range(2):
+        m = _fresh_model(golden_weights, cuda_dev)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+        g = torch.Generator(device=cuda_dev).manual_seed(5)
+        losses = []
+        for s in range(5):
+            t = torch.randint(0, T, (B,), device=cuda_dev, generator=g)
+            n = torch.randn(B, 29, device=cuda_dev, generator=g)
+            losses.append(ertdiff.train_step(m, opt, x0, cond, T, ab, t=t, noise=n))
+        outs.append((losses, [p.detach().clone() for p in m.parameters()]))
+    assert outs[0][0] == outs[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(outs[0][1], outs[1][1]))
+    assert all(np.isfinite(outs[0][0]))
