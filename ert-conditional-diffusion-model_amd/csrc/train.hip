@@ -208,6 +208,7 @@ __global__ __launch_bounds__(256) void dense_grad_kernel(const float* __restrict
   else if ((i -= H) < P * H) { dz_off = TV_DOUT; in_off = TV_H; kdim = H; dst = g.w2; }
   else if ((i -= P * H) < P) { dz_off = TV_DOUT; bias = true; dst = g.b2; kdim = 1; in_off = 0; }
   else if (i - P == 0) {  // loss = sum of squared errors / (B*P)
+    if (!g.loss) return;      // autograd backward: the loss lives in torch
     float acc = 0.f;
     for (int b = 0; b < B; ++b) acc += vec[(size_t)b * TV + TV_SQ];
     *g.loss = acc * inv_n;
