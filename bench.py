@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hoisted", action="store_true", help="skip the secondary hoisted timing")
+    ap.add_argument("--no-train", action="store_true", help="skip the secondary train-step timing")
     ap.add_argument("--roofline-reps", type=int, default=200)
     return ap.parse_args()
 
@@ -135,14 +136,18 @@ def strip_kernel_roofline(model, cond, B, precision, reps, dev):
                                                   stream.cuda_stream), "encoder_strips")
     for _ in range(20):
         launch()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
-    for i in range(reps):
-        starts[i].record(stream)
-        launch()
-        ends[i].record(stream)
-    torch.cuda.synchronize(dev)
-    ms = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
+    # back-to-back launches between two events on the launching stream (the
+    # per-launch average then includes the ~1 us dispatch gap rocprof excludes)
+    rounds = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            launch()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        rounds.append(e0.elapsed_time(e1) / reps)
+    ms = sorted(rounds)
     avg_ms = sum(ms) / len(ms)
     flop = CONV_FLOP_PER_MEMBER * B
     achieved = flop / (avg_ms * 1e-3) / 1e12
@@ -159,9 +164,57 @@ def strip_kernel_roofline(model, cond, B, precision, reps, dev):
             "bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "avg_us": round(avg_ms * 1e3, 3), "median_us": round(ms[len(ms) // 2] * 1e3, 3),
+            "timing": f"HIP events around {reps} back-to-back launches x 5 rounds",
             "algorithmic_flop_per_launch": flop,
             "algorithmic_bytes_per_launch": COND_BYTES_PER_MEMBER * B,
             "hbm_gbs_algorithmic": round(COND_BYTES_PER_MEMBER * B / (avg_ms * 1e-3) / 1e9, 1)}
+
+
+def train_bench(dev, steps=200, B=32, T=500):
+    """Reference train step (:309-319) at the reference batch size, fused GPU path."""
+    torch.manual_seed(42)
+    model = ertdiff.ConditionalDiffusionModel(P, 128).to(dev).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    g = torch.Generator(device=dev).manual_seed(7)
+    x0 = torch.randn(B, P, device=dev, generator=g) * 2
+    cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=dev)
+    ts = torch.randint(0, T, (steps + 20, B), device=dev, generator=g)
+    ns = torch.randn(steps + 20, B, P, device=dev, generator=g)
+    for i in range(20):
+        ertdiff.train_step(model, opt, x0, cond, T, ab, t=ts[i], noise=ns[i], return_tensor=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = ertdiff.train_step(model, opt, x0, cond, T, ab, t=ts[20 + i], noise=ns[20 + i],
+                                  return_tensor=True)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    return {"train_steps_per_s": round(steps / el, 1), "train_batch": B,
+            "train_ms_per_step": round(el / steps * 1e3, 4), "train_final_loss": round(float(loss), 5)}
+
+
+def cpu_train_baseline(seconds, B=32, T=500):
+    from oracle import ref_torch as RT
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(42)
+    W = {k: v.detach() for k, v in ertdiff.ConditionalDiffusionModel(P, 128).state_dict().items()}
+    g = torch.Generator().manual_seed(7)
+    x0 = torch.randn(B, P, generator=g) * 2
+    cond = torch.rand(B, 14, L_MEAS, generator=g)
+    ts = [torch.randint(0, T, (B,), generator=g) for _ in range(3)]
+    ns = [torch.randn(B, P, generator=g) for _ in range(3)]
+    RT.train_steps(W, x0, cond, T, ts[:1], ns[:1])
+    t0 = time.perf_counter()
+    RT.train_steps(W, x0, cond, T, ts, ns)
+    per = (time.perf_counter() - t0) / 3
+    n = int(max(3, seconds / max(per, 1e-6)))
+    ts = [ts[i % 3] for i in range(n)]
+    ns = [ns[i % 3] for i in range(n)]
+    t0 = time.perf_counter()
+    RT.train_steps(W, x0, cond, T, ts, ns)
+    return round(n / (time.perf_counter() - t0), 2)
 
 
 def cpu_baseline(seconds, B, T, mode):
@@ -223,12 +276,16 @@ def main():
         hel = time_steps(hplan, T, T, x_T, world, dev)
         extra["hoisted_steps_per_s"] = round(world * T / hel, 1)
     roof = strip_kernel_roofline(model, cond, B, a.precision, a.roofline_reps, dev)
+    if not a.no_train:
+        extra.update(train_bench(dev))
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.cpu_seconds, B, T, "faithful")
         if "hoisted_steps_per_s" in extra:
             hc = cpu_baseline(max(3.0, a.cpu_seconds / 3), B, T, "hoisted")
             extra["cpu_hoisted_steps_per_s"] = hc["value"]
+        if not a.no_train:
+            extra["cpu_train_steps_per_s"] = cpu_train_baseline(max(3.0, a.cpu_seconds / 3))
     if rank == 0:
         step_s = el / a.steps
         extra.update({

@@ -18,7 +18,7 @@ rc=$?; tail -5 gpurun_out/bench.log; stop_if_fatal $rc bench
 if [ "${PROFILE:-1}" = "1" ]; then
   export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-    -- python3 bench.py --steps 1000 --warmup 100 --no-cpu-baseline --no-hoisted > gpurun_out/prof.log 2>&1
+    -- python3 bench.py --steps 1000 --warmup 100 --no-cpu-baseline --no-hoisted --no-train > gpurun_out/prof.log 2>&1
   rc=$?; tail -3 gpurun_out/prof.log; stop_if_fatal $rc rocprof
   find gpurun_out/prof -name "*stats*" | head
 fi
