@@ -1,7 +1,7 @@
 // extern "C" entry points of libertdiff_hip.so (declared in include/ertdiff.h).
 // Every shape is validated on the host before anything is enqueued.
+#include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <new>
 
 #include "ertd_common.h"
@@ -14,38 +14,12 @@ constexpr size_t ALIGN = 256;
 inline size_t align_up(size_t n) { return (n + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Ws {
-  float* partial;   // 2 buffers of (B, S, 64): the faithful pipeline alternates them
+  float* partial;   // (B, S, 64) per-strip pool sums
   float* U;
   float* V;
   float* cond_emb;
   size_t partial_floats;
 };
-
-// Per-device auxiliary stream + events for the faithful pipeline (created once,
-// reused by every call and captured into graphs as a fork/join).
-struct Aux {
-  hipStream_t stream = nullptr;
-  hipEvent_t ev_enc = nullptr, ev_head[2] = {nullptr, nullptr}, ev_join = nullptr;
-};
-std::mutex g_aux_mu;
-Aux g_aux[64];
-
-hipError_t get_aux(Aux** out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  Aux& a = g_aux[dev];
-  if (!a.stream) {
-    if ((e = hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&a.ev_enc, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&a.ev_head[0], hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&a.ev_head[1], hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&a.ev_join, hipEventDisableTiming)) != hipSuccess) return e;
-  }
-  *out = &a;
-  return hipSuccess;
-}
 
 size_t ws_layout(int B, int L, int T, int op, void* base, Ws* out) {
   const int L2 = conv_len(conv_len(L));
@@ -57,7 +31,6 @@ size_t ws_layout(int B, int L, int T, int op, void* base, Ws* out) {
   w.partial_floats = (size_t)B * S * C2;
   off += align_up((size_t)B * S * C2 * sizeof(float));
   if (op == ERTD_OP_SAMPLE) {
-    off += align_up((size_t)B * S * C2 * sizeof(float));  // second partial buffer
     w.U = (float*)(p + off);
     off += align_up((size_t)B * H * sizeof(float));
     w.V = (float*)(p + off);
@@ -110,14 +83,13 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
                                     n_run, seed, member_offset, B, x_inout, s));
     return ERTD_OK;
   }
-  // Faithful mode: every step re-runs the full condition encoder, as the
-  // reference does.  Encoder(t) does not depend on x, only head(t) does, so the
-  // chain is issued as a two-stream pipeline: encoders back to back on `s`,
-  // heads on an auxiliary stream; pool partials alternate between two buffers,
-  // so encoder(t-2) waits only for head(t), and head(t) for encoder(t) and
-  // head(t+1) (stream order).  Same kernels, same inputs, same results as the
-  // sequential order.
+  // Faithful mode: every step re-runs the full condition encoder and the
+  // member heads, as the reference does (encoder(t), head(t), encoder(t-1), ...
+  // on one stream).
+  // A pipeline over several streams was measured and rejected: cross-queue
+  // event hops inside a graph cost ~10 us each on ROCm 7.
   HeadArgs a{};
+  a.partial = W.partial;
   a.S = S;
   a.L2 = L2;
   a.freq = freq;
@@ -131,26 +103,16 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
   a.member_offset = member_offset;
   a.B = B;
   a.x_out = x_inout;
-  std::lock_guard<std::mutex> lock(g_aux_mu);
-  Aux* ax = nullptr;
-  ERTD_TRY(get_aux(&ax));
-  ERTD_TRY(hipEventRecord(ax->ev_join, s));  // fork: aux stream follows the caller's prior work
-  ERTD_TRY(hipStreamWaitEvent(ax->stream, ax->ev_join, 0));
+  // Each step's encoder launch also computes v(t) (the time branch, identical
+  // for every member of a step) in one extra block; head_step consumes it.
+  TimeRowArgs tr{*w, freq, 0, W.V};
   for (int t = t_first; t >= t_last; --t) {
-    const int k = (t_first - t) & 1;
-    float* part = W.partial + (k ? align_up(W.partial_floats * sizeof(float)) / sizeof(float) : 0);
-    if (t_first - t >= 2) ERTD_TRY(hipStreamWaitEvent(s, ax->ev_head[k], 0));  // head(t+2) done
-    ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, cstride, B, L, precision,
-                                   part, s));
-    ERTD_TRY(hipEventRecord(ax->ev_enc, s));
-    ERTD_TRY(hipStreamWaitEvent(ax->stream, ax->ev_enc, 0));
     a.t_scalar = t;
-    a.partial = part;
-    ERTD_TRY(launch_head(*w, packed, a, ax->stream));
-    ERTD_TRY(hipEventRecord(ax->ev_head[k], ax->stream));
+    tr.t = t;
+    ERTD_TRY(launch_encoder_strips_t(packed, w->enc0_b, w->enc2_b, cond, cstride, B, L, precision,
+                                     W.partial, tr, s));
+    ERTD_TRY(launch_head_step(*w, packed, a, W.V, s));
   }
-  ERTD_TRY(hipEventRecord(ax->ev_join, ax->stream));  // join back into the caller's stream
-  ERTD_TRY(hipStreamWaitEvent(s, ax->ev_join, 0));
   return ERTD_OK;
 }
 

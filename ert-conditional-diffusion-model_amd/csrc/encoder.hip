@@ -87,7 +87,22 @@ __global__ __launch_bounds__(256) void pack_dense_kernel(ertd_weights w, float* 
 
 __global__ __launch_bounds__(256) void pack_w2b_kernel(ertd_weights w, float* __restrict__ packed) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= W2B_FLOATS) return;
+  if (idx >= W2B_FLOATS) {
+    const int i = idx - W2B_FLOATS;
+    if (i < W2F_FLOATS) {
+      const int k = i >> 6, l = i & 63, o = l >> 1;
+      packed[PACK_W2F + i] = o < w.param_dim ? w.mlp2_w[o * H + 64 * (l & 1) + k] : 0.f;
+    } else if (i < W2F_FLOATS + W0XR_FLOATS) {
+      const int r = i - W2F_FLOATS, jj = r / W0XR_PITCH, k = r % W0XR_PITCH;
+      packed[PACK_W0XR + r] = k < w.param_dim ? w.mlp0_w[jj * (w.param_dim + 2 * H) + k] : 0.f;
+    } else if (i < W2F_FLOATS + W0XR_FLOATS + W2L_FLOATS) {
+      const int r = i - W2F_FLOATS - W0XR_FLOATS, l = r / W2L_PITCH, k = r % W2L_PITCH;
+      const int o = l >> 1;
+      packed[PACK_W2L + r] =
+          (o < w.param_dim && k < H / 2) ? w.mlp2_w[o * H + 64 * (l & 1) + k] : 0.f;
+    }
+    return;
+  }
   const int kk = idx / (32 * 64), r = idx % (32 * 64);
   const int st = r >> 6, l = r & 63;
   const int o = 2 * st + (l >> 5), c = l & 31;
@@ -98,7 +113,8 @@ hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s) {
   pack_kernel<<<(PACK_TOTAL + 255) / 256, 256, 0, s>>>(w, packed);
   const int n = C2 * H + H * H + (w.param_dim + 2 * H) * H;
   pack_dense_kernel<<<(n + 255) / 256, 256, 0, s>>>(w, packed);
-  pack_w2b_kernel<<<(W2B_FLOATS + 255) / 256, 256, 0, s>>>(w, packed);
+  pack_w2b_kernel<<<(W2B_FLOATS + W2F_FLOATS + W0XR_FLOATS + W2L_FLOATS + 255) / 256, 256, 0,
+                    s>>>(w, packed);
   return hipGetLastError();
 }
 
@@ -135,6 +151,8 @@ __device__ __forceinline__ void conv1_tile(f32x16& acc, const float (&a1)[STEPS1
 // TRAIN additionally stores what the backward needs (train.hip): the conv1
 // activations a1 (B,32,L1) at the conv1 positions this strip owns,
 // i in [2*j0, 2*j0 + 2J), and the conv2 ReLU mask m2 (B,64,L2) as bytes.
+// Optionally (tr.V != null) block number nstrip computes the time row v(tr.t)
+// for the faithful sampler's next head launch (time_row_lean: few registers).
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__ packed,
                                                        const float* __restrict__ b1,
@@ -143,9 +161,16 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
                                                        long long cstride, int L, int L1, int L2,
                                                        int S, float* __restrict__ partial,
                                                        float* __restrict__ a1out,
-                                                       unsigned char* __restrict__ m2out) {
+                                                       unsigned char* __restrict__ m2out,
+                                                       int nstrip, TimeRowArgs tr) {
   __shared__ EncSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!TRAIN && (int)blockIdx.x >= nstrip) {
+    float* f = &sm.X[0][0][0];  // e[128] | te[128] | part[2][128]
+    time_row_lean(tr.w, packed, tr.freq, tr.t, tr.V + (size_t)tr.t * H, f, f + H,
+                  reinterpret_cast<float(*)[H]>(f + 2 * H), tid);
+    return;
+  }
   const int h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.x / S, strip = blockIdx.x - b * S;
   const int j0 = strip * J;
@@ -223,6 +248,30 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
   }
   __syncthreads();
   if (tid < C2) partial[((size_t)b * S + strip) * C2 + tid] = sm.red[0][tid] + sm.red[1][tid];
+  if (!TRAIN && tr.V) {
+    // Warm this XCD's L2 with a slice of the weights the next head_step reads
+    // (W3T, the cond columns of W0T, the two step images: ~134 KB).  Blocks
+    // b, b+8, ... share an XCD under the observed round-robin placement (a
+    // speed hint only); together each XCD group touches every 64-B line.
+    constexpr int L_W3 = C2 * H / 16, L_W0C = H * H / 16;
+    constexpr int L_IMG = (W0XR_FLOATS + W2L_FLOATS) / 16;
+    const int total = L_W3 + L_W0C + L_IMG;
+    const int grp = blockIdx.x >> 3, ngrp = (nstrip + 7) >> 3;
+    const int per = (total + ngrp - 1) / ngrp;
+    if (tid < per) {
+      const int line = grp * per + tid;
+      if (line < total) {
+        const float* src;
+        if (line < L_W3) src = packed + PACK_TOTAL + line * 16;
+        else if (line < L_W3 + L_W0C)
+          src = packed + PACK_TOTAL + C2 * H + H * H + (size_t)(tr.w.param_dim + H) * H +
+                (line - L_W3) * 16;
+        else src = packed + PACK_W0XR + (line - L_W3 - L_W0C) * 16;  // W2L follows W0XR
+        const float v = *src;  // plain load: allocates the line in this XCD's L2
+        asm volatile("" ::"v"(v));
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -343,7 +392,22 @@ hipError_t launch_encoder_strips(const float* packed, const float* b1, const flo
     enc_bf16_kernel<<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S, partial);
   else
     enc_fp32_kernel<false><<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S,
-                                                 partial, nullptr, nullptr);
+                                                 partial, nullptr, nullptr, B * S, TimeRowArgs{});
+  return hipGetLastError();
+}
+
+hipError_t launch_encoder_strips_t(const float* packed, const float* b1, const float* b2,
+                                   const float* cond, long long cstride, int B, int L,
+                                   int precision, float* partial, const TimeRowArgs& tr,
+                                   hipStream_t s) {
+  if (precision == ERTD_PREC_BF16) {  // bf16 strips + the time row as its own launch
+    hipError_t e = launch_encoder_strips(packed, b1, b2, cond, cstride, B, L, precision, partial, s);
+    if (e != hipSuccess) return e;
+    return launch_time_table(tr.w, packed, tr.freq, tr.t, 1, tr.V, s);
+  }
+  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
+  enc_fp32_kernel<false><<<dim3((unsigned)(B * S + 1)), 256, 0, s>>>(
+      packed, b1, b2, cond, cstride, L, L1, L2, S, partial, nullptr, nullptr, B * S, tr);
   return hipGetLastError();
 }
 
@@ -352,7 +416,8 @@ hipError_t launch_encoder_train(const float* packed, const float* b1, const floa
                                 unsigned char* m2, hipStream_t s) {
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
   enc_fp32_kernel<true><<<dim3((unsigned)(B * S)), 256, 0, s>>>(
-      packed, b1, b2, cond, (long long)CIN * L, L, L1, L2, S, partial, a1, m2);
+      packed, b1, b2, cond, (long long)CIN * L, L, L1, L2, S, partial, a1, m2, B * S,
+      TimeRowArgs{});
   return hipGetLastError();
 }
 

@@ -101,6 +101,37 @@ __device__ __forceinline__ void stage_cond(Tx (*X)[CIN][XS], const float* __rest
   if (tid < CIN * 4) X[tu & 3][tc][tu >> 2] = cvt(vt);
 }
 
+// Time row with streamed weights (low register use; for blocks living inside a
+// high-occupancy kernel).  Arithmetic identical to the split-k chain_half code
+// of head.hip: thread (j = tid&127, q = tid>>7) runs acc = init; acc = fma(W, v,
+// acc) over k in [64q, 64q+64) in order; outputs p0 + p1.  256 threads.
+__device__ __forceinline__ void time_row_lean(const ertd_weights& w, const float* packed,
+                                              const float* freq, int t, float* vrow, float* e,
+                                              float* te, float (*part)[H], int tid) {
+  const float* WtT = packed + PACK_TOTAL + C2 * H;
+  const float* W0tT = WtT + H * H + (size_t)w.param_dim * H;
+  const int j = tid & (H - 1), q = tid >> 7;
+  if (q == 0) {
+    constexpr int half = H / 2;
+    const float a = (float)t * freq[j < half ? j : j - half];
+    e[j] = j < half ? sinf(a) : cosf(a);
+  }
+  __syncthreads();
+  float acc = q == 0 ? w.time_b[j] : 0.f;
+#pragma unroll 8
+  for (int k = 0; k < H / 2; ++k) acc = fmaf(WtT[(q * (H / 2) + k) * H + j], e[q * (H / 2) + k], acc);
+  part[q][j] = acc;
+  __syncthreads();
+  if (tid < H) te[j] = fmaxf(part[0][j] + part[1][j], 0.f);
+  __syncthreads();
+  acc = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < H / 2; ++k) acc = fmaf(W0tT[(q * (H / 2) + k) * H + j], te[q * (H / 2) + k], acc);
+  part[q][j] = acc;
+  __syncthreads();
+  if (tid < H) vrow[j] = part[0][j] + part[1][j];
+}
+
 __device__ __forceinline__ void stage_cond_f32(float (*X)[CIN][XS], const float* __restrict__ cb,
                                                int L, int pos0, int tid) {
   stage_cond(X, cb, L, pos0, tid, [](float v) { return v; });
@@ -113,7 +144,19 @@ constexpr int DENSE_FLOATS = C2 * H + H * H + (PMAX + 2 * H) * H;
 // W2B[kk][s][lane] = W2[o = 2s + (lane>>5)][c = lane&31][kk]
 constexpr int PACK_W2B = PACK_TOTAL + DENSE_FLOATS;
 constexpr int W2B_FLOATS = 3 * 32 * 64;
-constexpr int PACKED_FLOATS_ALL = PACK_W2B + W2B_FLOATS;
+// mlp.2 in step-lane order: W2F[k][lane] = W2[lane>>1][64*(lane&1) + k] (0 for o >= P)
+constexpr int PACK_W2F = PACK_W2B + W2B_FLOATS;
+constexpr int W2F_FLOATS = (H / 2) * 64;
+// Step-body LDS images (copied verbatim into LDS, read with ds_read_b128,
+// conflict-free): W0XR[j][k] = W0[j][k] (k < P, row pitch 36) and
+// W2L[lane][k] = W2[lane>>1][64*(lane&1) + k] (row pitch 68).
+constexpr int W0XR_PITCH = 36;
+constexpr int W2L_PITCH = 68;
+constexpr int PACK_W0XR = PACK_W2F + W2F_FLOATS;
+constexpr int W0XR_FLOATS = H * W0XR_PITCH;
+constexpr int PACK_W2L = PACK_W0XR + W0XR_FLOATS;
+constexpr int W2L_FLOATS = 64 * W2L_PITCH;
+constexpr int PACKED_FLOATS_ALL = PACK_W2L + W2L_FLOATS;
 
 hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s);
 hipError_t launch_encoder_train(const float* packed, const float* b1, const float* b2,
@@ -122,6 +165,18 @@ hipError_t launch_encoder_train(const float* packed, const float* b1, const floa
 hipError_t launch_encoder_strips(const float* packed, const float* b1, const float* b2,
                                  const float* cond, long long cstride, int B, int L,
                                  int precision, float* partial, hipStream_t s);
+// Same, plus one extra block computing the time row v(t) = W0t.relu(Wt.e(t)+bt)
+// into V[t] (faithful sampler: the row the next head_step launch consumes).
+struct TimeRowArgs {
+  ertd_weights w;
+  const float* freq;
+  int t;
+  float* V;
+};
+hipError_t launch_encoder_strips_t(const float* packed, const float* b1, const float* b2,
+                                   const float* cond, long long cstride, int B, int L,
+                                   int precision, float* partial, const TimeRowArgs& tr,
+                                   hipStream_t s);
 struct HeadArgs {
   const float* partial; int S; int L2;
   const float* freq;
@@ -131,6 +186,9 @@ struct HeadArgs {
   float* x_out; float* eps_out; float* cond_emb_out; float* t_emb_out;
 };
 hipError_t launch_head(const ertd_weights& w, const float* packed, const HeadArgs& a, hipStream_t s);
+// faithful step: per-member condition branch + step for a.t_scalar using V[t]
+hipError_t launch_head_step(const ertd_weights& w, const float* packed, const HeadArgs& a,
+                            const float* V, hipStream_t s);
 hipError_t launch_hoist_prep(const ertd_weights& w, const float* packed, const float* partial,
                              int S, int L2, int B, float* U, float* cond_emb_out, hipStream_t s);
 hipError_t launch_time_table(const ertd_weights& w, const float* packed, const float* freq,

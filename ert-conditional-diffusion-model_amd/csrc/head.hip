@@ -16,6 +16,21 @@
 
 namespace ertd {
 
+// Phase stamps for the diagnostic build only (tools/diag_head.hip defines
+// ERTD_HEAD_STAMPS); the library build compiles them out.
+#ifdef ERTD_HEAD_STAMPS
+__device__ unsigned long long g_head_stamps[1024][2][8];
+#define HEAD_STAMP(i)                                                                   \
+  do {                                                                                  \
+    if ((threadIdx.x & 255) == 0)                                                       \
+      g_head_stamps[blockIdx.x][threadIdx.x >> 8][i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define HEAD_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 // k-major dense weights behind the conv fragments (see pack_dense_kernel)
 struct DenseT {
   const float* W3T;  // [64][128]
@@ -59,8 +74,24 @@ __device__ __forceinline__ float chain_half(const HalfW<N>& r, const float* v, f
 constexpr int POOL_GROUPS = 8;
 __device__ __forceinline__ float pool_group(const float* __restrict__ partial, int b, int S, int c,
                                             int g) {
+  // loads of 4 strips issued together, then added in strip order
+  const float* p = partial + (size_t)b * S * C2 + c;
   float acc = 0.f;
-  for (int s = g; s < S; s += POOL_GROUPS) acc += partial[((size_t)b * S + s) * C2 + c];
+  int s = g;
+  for (; s + 3 * POOL_GROUPS < S; s += 4 * POOL_GROUPS) {
+    const float v0 = p[(size_t)s * C2], v1 = p[(size_t)(s + POOL_GROUPS) * C2];
+    const float v2 = p[(size_t)(s + 2 * POOL_GROUPS) * C2], v3 = p[(size_t)(s + 3 * POOL_GROUPS) * C2];
+    acc += v0;
+    acc += v1;
+    acc += v2;
+    acc += v3;
+  }
+  float v[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) v[i] = s + i * POOL_GROUPS < S ? p[(size_t)(s + i * POOL_GROUPS) * C2] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (s + i * POOL_GROUPS < S) acc += v[i];
   return acc;
 }
 __device__ __forceinline__ float pool_combine(const float (*pg)[C2], int c, int L2) {
@@ -106,51 +137,96 @@ struct StepRegs {
   float bo;                          // b2[lane>>1]
 };
 
-__device__ __forceinline__ void load_step_regs(StepRegs& R, const float* __restrict__ W0T,
-                                               const float* __restrict__ W2,
+// All loads coalesced: W0T rows (k-major) and the lane-major W2F copy.
+__device__ __forceinline__ void load_step_regs(StepRegs& R, const float* __restrict__ packed,
                                                const float* __restrict__ b2, int P, int lane) {
-  const int o = lane >> 1, half = lane & 1;
+  const float* W0T = packed + PACK_TOTAL + C2 * H + H * H;
+  const float* W2F = packed + PACK_W2F;
+  const int o = lane >> 1;
 #pragma unroll
   for (int k = 0; k < PMAX; ++k) {
     R.w0x_lo[k] = k < P ? W0T[k * H + lane] : 0.f;
     R.w0x_hi[k] = k < P ? W0T[k * H + 64 + lane] : 0.f;
   }
 #pragma unroll
-  for (int k = 0; k < H / 2; ++k) R.w2h[k] = o < P ? W2[o * H + 64 * half + k] : 0.f;
+  for (int k = 0; k < H / 2; ++k) R.w2h[k] = W2F[k * 64 + lane];
   R.bo = o < P ? b2[o] : 0.f;
 }
 
-// xs[k] = x[k], held by lanes 2k and 2k+1 (wave-uniform result).
-__device__ __forceinline__ void broadcast_x(float (&xs)[PMAX], float xv, int P) {
-#pragma unroll
-  for (int k = 0; k < PMAX; ++k)
-    xs[k] = k < P ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), 2 * k)) : 0.f;
-}
-
-// eps for o = lane>>1 given the pre-activations of hidden units lane, lane+64.
-// hbuf: this wave's 128-float LDS scratch.
-__device__ __forceinline__ float step_eps(const StepRegs& R, float w_lo, float w_hi,
-                                          const float (&xs)[PMAX], int P, int lane, float* hbuf) {
-  float a_lo = w_lo, a_hi = w_hi;
-#pragma unroll
-  for (int k = 0; k < PMAX; ++k) {
-    if (k < P) {
-      a_lo = fmaf(R.w0x_lo[k], xs[k], a_lo);
-      a_hi = fmaf(R.w0x_hi[k], xs[k], a_hi);
-    }
-  }
-  hbuf[lane] = fmaxf(a_lo, 0.f);
-  hbuf[64 + lane] = fmaxf(a_hi, 0.f);
+// xs[k] = x[k] for every lane: lanes 2k write x[k] to this wave's LDS slot,
+// then every lane reads the slot back (uniform-address broadcast reads).
+__device__ __forceinline__ void broadcast_x(float (&xs)[PMAX], float xv, int P, int lane,
+                                            float* xbuf) {
+  if (!(lane & 1) && (lane >> 1) < P) xbuf[lane >> 1] = xv;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const float* hh = hbuf + 64 * (lane & 1);
-  float acc = 0.f;
 #pragma unroll
-  for (int k = 0; k < H / 2; ++k) acc = fmaf(R.w2h[k], hh[k], acc);
-  const float e = acc + __shfl_xor(acc, 1);
-  return e + R.bo;
+  for (int k = 0; k < PMAX; ++k) xs[k] = k < P ? xbuf[k] : 0.f;
 }
+
+// eps for o = lane>>1 given the pre-activations of hidden units lane, lane+64.
+// hbuf: this wave's 128-float LDS scratch.  Src supplies the weights (registers
+// in the persistent sampler, LDS images in the per-step head): same fma order.
+template <class Src>
+__device__ __forceinline__ float step_eps(const Src& W, float w_lo, float w_hi,
+                                          const float (&xs)[PMAX], int P, int lane, float* hbuf) {
+  // mlp.0 x-part: two chains per hidden unit (k < 16, k >= 16), joined in order
+  float a_lo = w_lo, a_hi = w_hi, b_lo = 0.f, b_hi = 0.f;
+#pragma unroll
+  for (int k = 0; k < PMAX / 2; ++k) {
+    if (k < P) {
+      a_lo = fmaf(W.w0x_lo(k), xs[k], a_lo);
+      a_hi = fmaf(W.w0x_hi(k), xs[k], a_hi);
+    }
+    if (k + PMAX / 2 < P) {
+      b_lo = fmaf(W.w0x_lo(k + PMAX / 2), xs[k + PMAX / 2], b_lo);
+      b_hi = fmaf(W.w0x_hi(k + PMAX / 2), xs[k + PMAX / 2], b_hi);
+    }
+  }
+  hbuf[lane] = fmaxf(a_lo + b_lo, 0.f);
+  hbuf[64 + lane] = fmaxf(a_hi + b_hi, 0.f);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // mlp.2: four 16-term chains over this lane's k-half, joined (c0+c1)+(c2+c3)
+  const float4* hh4 = reinterpret_cast<const float4*>(hbuf + 64 * (lane & 1));
+  float hv[H / 2];  // all 16 LDS reads in flight before the chains start
+#pragma unroll
+  for (int i = 0; i < H / 8; ++i) {
+    const float4 q4 = hh4[i];
+    hv[4 * i] = q4.x;
+    hv[4 * i + 1] = q4.y;
+    hv[4 * i + 2] = q4.z;
+    hv[4 * i + 3] = q4.w;
+  }
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = fmaf(W.w2h(16 * i + k), hv[16 * i + k], c[i]);
+  }
+  const float acc = (c[0] + c[1]) + (c[2] + c[3]);
+  const float e = acc + __shfl_xor(acc, 1);
+  return e + W.bo;
+}
+
+struct RegSrc {  // StepRegs in registers
+  const StepRegs& R;
+  float bo;
+  __device__ float w0x_lo(int k) const { return R.w0x_lo[k]; }
+  __device__ float w0x_hi(int k) const { return R.w0x_hi[k]; }
+  __device__ float w2h(int k) const { return R.w2h[k]; }
+};
+struct LdsSrc {  // the packed W0XR / W2L images copied into LDS (16-B aligned rows)
+  const float* w0x_row_lo;  // &W0XR[lane][0]
+  const float* w0x_row_hi;  // &W0XR[lane + 64][0]
+  const float* w2_row;      // &W2L[lane][0]
+  float bo;
+  __device__ float w0x_lo(int k) const { return w0x_row_lo[k]; }
+  __device__ float w0x_hi(int k) const { return w0x_row_hi[k]; }
+  __device__ float w2h(int k) const { return w2_row[k]; }
+};
 
 // x <- c1*(x - c2*eps) [+ sig*z], one fp32 rounding per reference op (:113-118).
 __device__ __forceinline__ float ddpm_update(float xv, float eps, float c1, float c2, float sig,
@@ -178,26 +254,13 @@ struct HeadSmem {
   float part[2][2][H];         // [branch][q][j] split-k partials
   float w[H];                  // u + v
   float hbuf[H];               // step body scratch (wave 0)
-  float w0x[PMAX][H];          // x columns of mlp.0 (k-major)
-  float w2f[H / 2][64];        // mlp.2 in step-lane order: [k][lane] = W2[lane>>1][64*(lane&1)+k]
+  float xbuf[PMAX];
+  alignas(16) float w0xr[H * W0XR_PITCH];
+  alignas(16) float w2l[64 * W2L_PITCH];
 };
 
+// waves 0-3: condition branch, 4-7: time branch; wave 0 then runs the step.
 constexpr int HEAD_THREADS = 512;
-
-// Phase stamps for the diagnostic build only (tools/diag_head.hip defines
-// ERTD_HEAD_STAMPS); the library build compiles them out.
-#ifdef ERTD_HEAD_STAMPS
-__device__ unsigned long long g_head_stamps[1024][2][8];
-#define HEAD_STAMP(i)                                                                   \
-  do {                                                                                  \
-    if ((threadIdx.x & 255) == 0)                                                       \
-      g_head_stamps[blockIdx.x][threadIdx.x >> 8][i] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define HEAD_STAMP(i) \
-  do {                \
-  } while (0)
-#endif
 
 // ---------------------------------------------------------------------------
 // head_kernel: one 512-thread workgroup per member; full head for timestep t.
@@ -217,6 +280,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void head_kernel(ertd_weights w,
   const int j = tid & (H - 1), q = (tid >> 7) & 1;
   const DenseT d = dense_ptrs(packed);
   const int64_t t = a.t_vec ? a.t_vec[b] : (int64_t)a.t_scalar;
+  const int ts = (int)t;
+  const int o = lane >> 1;
   HEAD_STAMP(0);
 
   // ---- issue every load up front ------------------------------------------------
@@ -224,11 +289,24 @@ __global__ __launch_bounds__(HEAD_THREADS) void head_kernel(ertd_weights w,
   TimeW tw;
   if (cond_br) load_cond_w(cw, d, P, j, q);
   else load_time_w(tw, d, P, j, q);
-  for (int i = tid; i < PMAX * H; i += HEAD_THREADS) {
-    const int k = i / H;
-    sm.w0x[0][i] = k < P ? d.W0T[i] : 0.f;
-    const int kk = i >> 6, ln = i & 63, o = ln >> 1;  // conflict-free lane-major image
-    sm.w2f[0][i] = o < P ? w.mlp2_w[o * H + 64 * (ln & 1) + kk] : 0.f;
+  float xv = 0.f, z = 0.f, c1 = 0.f, c2 = 0.f, sig = 0.f, bo = 0.f;
+  if (wave == 0) {  // the step's own inputs, off the critical path
+    xv = o < P ? a.x_in[(size_t)b * P + o] : 0.f;
+    bo = o < P ? w.mlp2_b[o] : 0.f;
+    if (!a.eps_out) {
+      z = step_noise(a.noise, a.num_steps, ts, a.B, b, P, o, a.seed, a.member_offset + (uint32_t)b);
+      c1 = a.c1[ts];
+      c2 = a.c2[ts];
+      sig = a.sigma[ts];
+    }
+  }
+  {  // verbatim copies of the packed step images (float4, coalesced)
+    const float4* s0 = reinterpret_cast<const float4*>(packed + PACK_W0XR);
+    const float4* s1 = reinterpret_cast<const float4*>(packed + PACK_W2L);
+    float4* d0 = reinterpret_cast<float4*>(sm.w0xr);
+    float4* d1 = reinterpret_cast<float4*>(sm.w2l);
+    for (int i = tid; i < W0XR_FLOATS / 4; i += HEAD_THREADS) d0[i] = s0[i];
+    for (int i = tid; i < W2L_FLOATS / 4; i += HEAD_THREADS) d1[i] = s1[i];
   }
   {
     const int c = tid & (C2 - 1), g = tid >> 6;
@@ -273,31 +351,19 @@ __global__ __launch_bounds__(HEAD_THREADS) void head_kernel(ertd_weights w,
   HEAD_STAMP(4);
   if (wave != 0) return;
 
-  // ---- step body (one wave) --------------------------------------------------------
-  StepRegs R;
-  const int o = lane >> 1;
-#pragma unroll
-  for (int k = 0; k < PMAX; ++k) {
-    R.w0x_lo[k] = sm.w0x[k][lane];
-    R.w0x_hi[k] = sm.w0x[k][64 + lane];
-  }
-#pragma unroll
-  for (int k = 0; k < H / 2; ++k) R.w2h[k] = sm.w2f[k][lane];
-  R.bo = o < P ? w.mlp2_b[o] : 0.f;
-  float xv = o < P ? a.x_in[(size_t)b * P + o] : 0.f;
+  // ---- step body (wave 0), weights read from LDS inside the chains -----------------
   float xs[PMAX];
-  broadcast_x(xs, xv, P);
+  broadcast_x(xs, xv, P, lane, sm.xbuf);
   HEAD_STAMP(5);
-  const float eps = step_eps(R, sm.w[lane], sm.w[lane + 64], xs, P, lane, sm.hbuf);
+  const LdsSrc src{sm.w0xr + lane * W0XR_PITCH, sm.w0xr + (lane + 64) * W0XR_PITCH,
+                   sm.w2l + lane * W2L_PITCH, bo};
+  const float eps = step_eps(src, sm.w[lane], sm.w[lane + 64], xs, P, lane, sm.hbuf);
   HEAD_STAMP(6);
   if (a.eps_out) {
     if (!(lane & 1) && o < P) a.eps_out[(size_t)b * P + o] = eps;
     return;
   }
-  const int ts = (int)t;
-  const float z = step_noise(a.noise, a.num_steps, ts, a.B, b, P, o, a.seed,
-                             a.member_offset + (uint32_t)b);
-  xv = ddpm_update(xv, eps, a.c1[ts], a.c2[ts], a.sigma[ts], z, ts > 0);
+  xv = ddpm_update(xv, eps, c1, c2, sig, z, ts > 0);
   if (!(lane & 1) && o < P) a.x_out[(size_t)b * P + o] = xv;
   HEAD_STAMP(7);
 }
@@ -307,65 +373,101 @@ hipError_t launch_head(const ertd_weights& w, const float* packed, const HeadArg
   return hipGetLastError();
 }
 
+
+// ---- condition branch row and time row (shared by every mode) ---------------------
+// cond_row: U[j] = b0_j + W0c.relu(W3.mean + b3) for one member, 256 threads
+// (j = tid&127, q = tid>>7).  Weights must already be in `cw` (loaded early).
+struct CondScratch {
+  float pg[POOL_GROUPS][C2];
+  float m[C2];
+  float c[H];
+  float part[2][H];
+};
+__device__ __forceinline__ void cond_row_pool(CondScratch& sc, const float* partial, int b, int S,
+                                              int tid) {
+  for (int i = tid; i < POOL_GROUPS * C2; i += 256) {
+    const int cc = i & (C2 - 1), g = i >> 6;
+    sc.pg[g][cc] = pool_group(partial, b, S, cc, g);
+  }
+}
+// after cond_row_pool + __syncthreads(); returns u_j on threads < 128 (else 0).
+// Four block barriers; cond_row_idle() mirrors them for waves that sit it out.
+__device__ __forceinline__ float cond_row_finish_nb(CondScratch& sc, const CondW& cw, float bias_c,
+                                                    float bias_u, int L2, int tid, int j, int q,
+                                                    float* cond_emb_out = nullptr) {
+  if (tid < C2) sc.m[tid] = pool_combine(sc.pg, tid, L2);
+  __syncthreads();
+  sc.part[q][j] = chain_half<C2>(cw.w3, sc.m, bias_c, q);
+  __syncthreads();
+  if (tid < H) {
+    const float cj = fmaxf(sc.part[0][j] + sc.part[1][j], 0.f);
+    sc.c[j] = cj;
+    if (cond_emb_out) cond_emb_out[j] = cj;
+  }
+  __syncthreads();
+  sc.part[q][j] = chain_half<H>(cw.w0c, sc.c, bias_u, q);
+  __syncthreads();
+  return tid < H ? sc.part[0][j] + sc.part[1][j] : 0.f;
+}
+__device__ __forceinline__ void cond_row_idle() {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) __syncthreads();
+}
+__device__ __forceinline__ float cond_row_finish(CondScratch& sc, const CondW& cw, float bias_c,
+                                                 float bias_u, int L2, int tid, int j, int q,
+                                                 float* cond_emb_out) {
+  return cond_row_finish_nb(sc, cw, bias_c, bias_u, L2, tid, j, q, cond_emb_out);
+}
+
+// time_row: V[t][j] = W0t.relu(Wt.sinusoid(t) + bt), 256 threads.
+struct TimeScratch {
+  float e[H];
+  float te[H];
+  float part[2][H];
+};
+__device__ __forceinline__ void time_row(TimeScratch& sc, const ertd_weights& w, const DenseT& d,
+                                         const float* freq, int t, float* vrow, int tid) {
+  const int j = tid & (H - 1), q = tid >> 7;
+  TimeW tw;
+  load_time_w(tw, d, w.param_dim, j, q);
+  const float bias_t = q == 0 ? w.time_b[j] : 0.f;
+  if (q == 0) sc.e[j] = sinusoid((float)t, freq, j);
+  __syncthreads();
+  sc.part[q][j] = chain_half<H>(tw.wt, sc.e, bias_t, q);
+  __syncthreads();
+  if (tid < H) sc.te[j] = fmaxf(sc.part[0][j] + sc.part[1][j], 0.f);
+  __syncthreads();
+  sc.part[q][j] = chain_half<H>(tw.w0t, sc.te, 0.f, q);
+  __syncthreads();
+  if (tid < H) vrow[j] = sc.part[0][j] + sc.part[1][j];
+}
+
 // ---- hoisted-mode precomputation ------------------------------------------------
-// U[b][j] = b0_j + W0c.relu(W3.mean + b3)   (one 256-thread block per member)
 __global__ __launch_bounds__(256) void hoist_prep_kernel(ertd_weights w, const float* __restrict__ packed,
                                                          const float* __restrict__ partial, int S,
                                                          int L2, float* __restrict__ U,
                                                          float* __restrict__ cond_emb_out) {
-  __shared__ float pg[POOL_GROUPS][C2];
-  __shared__ float m[C2];
-  __shared__ float c[H];
-  __shared__ float part[2][H];
+  __shared__ CondScratch sc;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int j = tid & (H - 1), q = tid >> 7;
   const DenseT d = dense_ptrs(packed);
   CondW cw;
   load_cond_w(cw, d, w.param_dim, j, q);
-  for (int i = tid; i < POOL_GROUPS * C2; i += 256) {
-    const int cc = i & (C2 - 1), g = i >> 6;
-    pg[g][cc] = pool_group(partial, b, S, cc, g);
-  }
+  cond_row_pool(sc, partial, b, S, tid);
   const float bias_c = q == 0 ? w.enc6_b[j] : 0.f;
   const float bias_u = q == 0 ? w.mlp0_b[j] : 0.f;
   __syncthreads();
-  if (tid < C2) m[tid] = pool_combine(pg, tid, L2);
-  __syncthreads();
-  part[q][j] = chain_half<C2>(cw.w3, m, bias_c, q);
-  __syncthreads();
-  if (tid < H) {
-    const float cj = fmaxf(part[0][j] + part[1][j], 0.f);
-    c[j] = cj;
-    if (cond_emb_out) cond_emb_out[(size_t)b * H + j] = cj;
-  }
-  __syncthreads();
-  part[q][j] = chain_half<H>(cw.w0c, c, bias_u, q);
-  __syncthreads();
-  if (tid < H) U[(size_t)b * H + j] = part[0][j] + part[1][j];
+  const float u = cond_row_finish(sc, cw, bias_c, bias_u, L2, tid, j, q,
+                                  cond_emb_out ? cond_emb_out + (size_t)b * H : nullptr);
+  if (tid < H) U[(size_t)b * H + j] = u;
 }
 
-// V[t][j] = W0t.relu(Wt.sinusoid(t) + bt)   (one 256-thread block per timestep)
 __global__ __launch_bounds__(256) void time_table_kernel(ertd_weights w, const float* __restrict__ packed,
                                                          const float* __restrict__ freq, int t_lo,
                                                          float* __restrict__ V) {
-  __shared__ float e[H];
-  __shared__ float te[H];
-  __shared__ float part[2][H];
-  const int t = t_lo + (int)blockIdx.x, tid = threadIdx.x;
-  const int j = tid & (H - 1), q = tid >> 7;
-  const DenseT d = dense_ptrs(packed);
-  TimeW tw;
-  load_time_w(tw, d, w.param_dim, j, q);
-  const float bias_t = q == 0 ? w.time_b[j] : 0.f;
-  if (q == 0) e[j] = sinusoid((float)t, freq, j);
-  __syncthreads();
-  part[q][j] = chain_half<H>(tw.wt, e, bias_t, q);
-  __syncthreads();
-  if (tid < H) te[j] = fmaxf(part[0][j] + part[1][j], 0.f);
-  __syncthreads();
-  part[q][j] = chain_half<H>(tw.w0t, te, 0.f, q);
-  __syncthreads();
-  if (tid < H) V[(size_t)t * H + j] = part[0][j] + part[1][j];
+  __shared__ TimeScratch sc;
+  const int t = t_lo + (int)blockIdx.x;
+  time_row(sc, w, dense_ptrs(packed), freq, t, V + (size_t)t * H, threadIdx.x);
 }
 
 hipError_t launch_hoist_prep(const ertd_weights& w, const float* packed, const float* partial,
@@ -380,6 +482,74 @@ hipError_t launch_time_table(const ertd_weights& w, const float* packed, const f
   return hipGetLastError();
 }
 
+// ---- faithful per-step head -------------------------------------------------------
+// One block per member: the condition branch for this step's pool partials,
+// w = u + v(t), then wave 0 runs the step.  v(t) -- the time branch, identical
+// for every member of a step -- is computed once per step by an extra block of
+// the step's encoder launch (time_row_lean: the same fma chains as the
+// hoisted time table, so both modes stay bit-identical).
+struct HeadStepSmem {
+  CondScratch cond;
+  float w[H];
+  alignas(16) float hbuf[H];
+  alignas(16) float xbuf[PMAX];
+};
+constexpr int HEAD_STEP_THREADS = 320;  // waves 0-3: condition branch, wave 4: step
+
+__global__ __launch_bounds__(HEAD_STEP_THREADS) void head_step_kernel(
+    ertd_weights w, const float* __restrict__ packed, HeadArgs a, const float* __restrict__ V) {
+  __shared__ HeadStepSmem sm;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool step_wave = tid >= 256;
+  const DenseT d = dense_ptrs(packed);
+  const int P = w.param_dim, b = blockIdx.x, ts = a.t_scalar;
+  const int j = tid & (H - 1), q = (tid >> 7) & 1, o = lane >> 1;
+  HEAD_STAMP(0);
+  CondW cw;
+  StepRegs R;
+  float xv = 0.f, z = 0.f, c1 = 0.f, c2 = 0.f, sig = 0.f;
+  if (step_wave) {  // the step's weights and inputs, requested at kernel start
+    load_step_regs(R, packed, w.mlp2_b, P, lane);
+    xv = o < P ? a.x_in[(size_t)b * P + o] : 0.f;
+    z = step_noise(a.noise, a.num_steps, ts, a.B, b, P, o, a.seed, a.member_offset + (uint32_t)b);
+    c1 = a.c1[ts];
+    c2 = a.c2[ts];
+    sig = a.sigma[ts];
+  } else {
+    load_cond_w(cw, d, P, j, q);
+    cond_row_pool(sm.cond, a.partial, b, a.S, tid);
+  }
+  const float bias_c = q == 0 ? w.enc6_b[j] : 0.f;
+  const float bias_u = q == 0 ? w.mlp0_b[j] : 0.f;
+  const float vj = tid < H ? V[(size_t)ts * H + j] : 0.f;
+  __syncthreads();
+  HEAD_STAMP(1);
+  // cond_row_finish's barriers are block-wide: the step wave joins them idle
+  float u = 0.f;
+  if (!step_wave) u = cond_row_finish_nb(sm.cond, cw, bias_c, bias_u, a.L2, tid, j, q);
+  else cond_row_idle();
+  HEAD_STAMP(2);
+  if (tid < H) sm.w[j] = u + vj;
+  __syncthreads();
+  HEAD_STAMP(3);
+  if (!step_wave) return;
+  float xs[PMAX];
+  broadcast_x(xs, xv, P, lane, sm.xbuf);
+  HEAD_STAMP(4);
+  const RegSrc src{R, R.bo};
+  const float eps = step_eps(src, sm.w[lane], sm.w[lane + 64], xs, P, lane, sm.hbuf);
+  HEAD_STAMP(5);
+  xv = ddpm_update(xv, eps, c1, c2, sig, z, ts > 0);
+  if (!(lane & 1) && o < P) a.x_out[(size_t)b * P + o] = xv;
+  HEAD_STAMP(6);
+}
+
+hipError_t launch_head_step(const ertd_weights& w, const float* packed, const HeadArgs& a,
+                            const float* V, hipStream_t s) {
+  head_step_kernel<<<a.B, HEAD_STEP_THREADS, 0, s>>>(w, packed, a, V);
+  return hipGetLastError();
+}
+
 // ---- persistent hoisted sampler ---------------------------------------------------
 // One wave per member runs all num_steps steps; x lives in registers (lane 2o
 // and 2o+1 hold x[o]; a readlane broadcast feeds the next step's W0x.x as
@@ -390,13 +560,13 @@ __global__ __launch_bounds__(256) void hoisted_sampler_kernel(
     const float* __restrict__ sigma, const float* __restrict__ noise, int num_steps, int t_first,
     int n_run, uint64_t seed, uint32_t member_offset, int B, float* __restrict__ x) {
   __shared__ float hbuf[4][H];
+  __shared__ float xbuf[4][PMAX];
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;  // whole wave exits together (no block barriers below)
   const int P = w.param_dim;
-  const DenseT d = dense_ptrs(packed);
   StepRegs R;
-  load_step_regs(R, d.W0T, w.mlp2_w, w.mlp2_b, P, lane);
+  load_step_regs(R, packed, w.mlp2_b, P, lane);
   const float u_lo = U[(size_t)b * H + lane];
   const float u_hi = U[(size_t)b * H + 64 + lane];
   const int o = lane >> 1;
@@ -404,11 +574,12 @@ __global__ __launch_bounds__(256) void hoisted_sampler_kernel(
   float xv = o < P ? x[(size_t)b * P + o] : 0.f;
   float xs[PMAX];
   for (int t = t_first; t > t_first - n_run; --t) {
-    broadcast_x(xs, xv, P);
+    broadcast_x(xs, xv, P, lane, xbuf[threadIdx.x >> 6]);
     const float w_lo = u_lo + V[(size_t)t * H + lane];
     const float w_hi = u_hi + V[(size_t)t * H + 64 + lane];
     const float z = step_noise(noise, num_steps, t, B, b, P, o, seed, member);
-    const float eps = step_eps(R, w_lo, w_hi, xs, P, lane, hbuf[threadIdx.x >> 6]);
+    const RegSrc src{R, R.bo};
+    const float eps = step_eps(src, w_lo, w_hi, xs, P, lane, hbuf[threadIdx.x >> 6]);
     xv = ddpm_update(xv, eps, c1[t], c2[t], sigma[t], z, t > 0);
   }
   if (!(lane & 1) && o < P) x[(size_t)b * P + o] = xv;

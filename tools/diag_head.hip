@@ -21,7 +21,7 @@ int main() {
   CK(launch_pack(w, packed, 0));
   float* cond = dev((size_t)B * 14 * L);
   for (size_t i = 0; i < (size_t)B*14*L; i += 1) {}  // values in [-0.5,0.5)
-  float *partial = dev((size_t)B * S * 64), *x = dev(B * P), *tabs = dev(3 * T), *freq = dev(64);
+  float *partial = dev((size_t)B * S * 64), *x = dev(B * P), *tabs = dev(128 * T), *freq = dev(64);
   HeadArgs a{};
   a.partial = partial; a.S = S; a.L2 = L2; a.freq = freq; a.x_in = x; a.c1 = tabs; a.c2 = tabs + T;
   a.sigma = tabs + 2 * T; a.num_steps = T; a.seed = 1; a.B = B; a.x_out = x;
@@ -29,7 +29,7 @@ int main() {
   for (int it = 0; it < 30; ++it) {
     a.t_scalar = T - 1 - it;
     CK(launch_encoder_strips(packed, w.enc0_b, w.enc2_b, cond, 14LL * L, B, L, 0, partial, 0));
-    CK(launch_head(w, packed, a, 0));
+    CK(launch_head_step(w, packed, a, tabs, 0));
   }
   CK(hipDeviceSynchronize());
   // time each kernel alone, back to back
@@ -37,7 +37,7 @@ int main() {
     hipEventRecord(e0, 0);
     for (int it = 0; it < 100; ++it) {
       if (which == 0) launch_encoder_strips(packed, w.enc0_b, w.enc2_b, cond, 14LL * L, B, L, 0, partial, 0);
-      else launch_head(w, packed, a, 0);
+      else launch_head_step(w, packed, a, tabs, 0);
     }
     hipEventRecord(e1, 0); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
@@ -47,10 +47,11 @@ int main() {
   CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_head_stamps), sizeof(st)));
   unsigned long long t0 = ~0ull;
   for (int b = 0; b < B; ++b) t0 = std::min(t0, st[b][0][0]);
-  const char* names[8] = {"start", "loads+pool+sin barrier", "pool combine", "layer1", "layer2", "step regs+bcast", "eps", "update"};
-  for (int ph = 0; ph < 8; ++ph) {
+  const char* names[8] = {"start", "loads+pool barrier", "cond row done", "w barrier", "x bcast", "eps", "update", "-"};
+  for (int ph = 0; ph < 7; ++ph) {
     double mn = 1e30, mx = 0, avg = 0; int n = 0;
-    for (int b = 0; b < B; ++b) { if (ph >= 5 && false) continue; double v = (st[b][0][ph] - t0) / 100.0; mn = std::min(mn, v); mx = std::max(mx, v); avg += v; ++n; }
+    const int wv = 0;
+    for (int b = 0; b < B; ++b) { double v = (st[b][wv][ph] - t0) / 100.0; mn = std::min(mn, v); mx = std::max(mx, v); avg += v; ++n; }
     printf("phase %d %-26s wave0: min %.2f avg %.2f max %.2f us (from first block start)\n", ph, names[ph], mn, avg / n, mx);
   }
   return 0;
