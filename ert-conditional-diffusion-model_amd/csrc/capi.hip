@@ -19,7 +19,22 @@ struct Ws {
   float* V;
   float* cond_emb;
   size_t partial_floats;
+  // persistent faithful chain (OP_SAMPLE only)
+  float* ring;                  // CHAIN_RING x (B, S, 64)
+  unsigned* sync;               // zeroed per call (sync_words)
+  float* uring;                 // (R, B, 128) condition rows
+  float* Vc;                    // (T, 128) time rows of the chain
+  size_t zero_bytes;
 };
+
+// sync block (zeroed per call), one word per SYNC_PAD-word line:
+// cnt (R,B) | uflag (R,B) | progress (B) | claim (B) | vready | status
+inline size_t sync_words(int B) {
+  return ((size_t)2 * CHAIN_RING * B + 2 * (size_t)B + 2) * SYNC_PAD;
+}
+inline unsigned* status_word(unsigned* sync, int B) {
+  return sync + ((size_t)2 * CHAIN_RING * B + 2 * (size_t)B + 1) * SYNC_PAD;
+}
 
 size_t ws_layout(int B, int L, int T, int op, void* base, Ws* out) {
   const int L2 = conv_len(conv_len(L));
@@ -37,6 +52,15 @@ size_t ws_layout(int B, int L, int T, int op, void* base, Ws* out) {
     off += align_up((size_t)(T > 0 ? T : 1) * H * sizeof(float));
     w.cond_emb = (float*)(p + off);
     off += align_up((size_t)B * H * sizeof(float));
+    w.ring = (float*)(p + off);
+    off += align_up((size_t)CHAIN_RING * B * S * C2 * sizeof(float));
+    w.sync = (unsigned*)(p + off);
+    w.zero_bytes = sync_words(B) * sizeof(unsigned);
+    off += align_up(w.zero_bytes);
+    w.uring = (float*)(p + off);
+    off += align_up((size_t)CHAIN_RING * B * H * sizeof(float));
+    w.Vc = (float*)(p + off);
+    off += align_up((size_t)(T > 0 ? T : 1) * H * sizeof(float));
   }
   if (out) *out = w;
   return off;
@@ -65,7 +89,8 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
                    int precision, float* x_inout, void* ws, size_t ws_bytes, hipStream_t s) {
   if (!weights_ok(w) || !packed || !cond || !c1 || !c2 || !sigma || !freq || !x_inout || !ws)
     return ERTD_EINVAL;
-  if (B < 1 || L < 1 || num_steps < 1 || (mode != ERTD_MODE_HOISTED && mode != ERTD_MODE_FAITHFUL))
+  if (B < 1 || L < 1 || num_steps < 1 ||
+      (mode != ERTD_MODE_HOISTED && mode != ERTD_MODE_FAITHFUL && mode != ERTD_MODE_FAITHFUL_STEPS))
     return ERTD_EINVAL;
   if (precision != ERTD_PREC_FP32 && precision != ERTD_PREC_BF16) return ERTD_EINVAL;
   if (t_first < 0 || t_first >= num_steps || n_run < 1 || n_run > t_first + 1) return ERTD_EINVAL;
@@ -84,8 +109,47 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
     return ERTD_OK;
   }
   // Faithful mode: every step re-runs the full condition encoder and the
-  // member heads, as the reference does (encoder(t), head(t), encoder(t-1), ...
-  // on one stream).
+  // member heads, as the reference does.  Preferred schedule: one persistent
+  // launch for the whole chain (chain.hip); it needs every block resident, so
+  // it is used when the grid fits (and for fp32, the precision it implements).
+  if (mode == ERTD_MODE_FAITHFUL && precision == ERTD_PREC_FP32) {
+    const int grid = faithful_chain_grid(B, S);
+    if (grid > 0) {
+      ERTD_TRY(hipMemsetAsync(W.sync, 0, W.zero_bytes, s));
+      FaithfulChainArgs fa{};
+      fa.cond = cond;
+      fa.cstride = cstride;
+      fa.L = L;
+      fa.B = B;
+      fa.S = S;
+      fa.R = CHAIN_RING;
+      fa.n_run = n_run;
+      fa.t_first = t_first;
+      fa.num_steps = num_steps;
+      fa.c1 = c1;
+      fa.c2 = c2;
+      fa.sigma = sigma;
+      fa.freq = freq;
+      fa.noise = noise;
+      fa.seed = seed;
+      fa.member_offset = member_offset;
+      fa.x = x_inout;
+      fa.part = W.ring;
+      fa.cnt = W.sync;
+      fa.uflag = fa.cnt + (size_t)CHAIN_RING * B * SYNC_PAD;
+      fa.progress = fa.uflag + (size_t)CHAIN_RING * B * SYNC_PAD;
+      fa.claim = fa.progress + (size_t)B * SYNC_PAD;
+      fa.vready = fa.claim + (size_t)B * SYNC_PAD;
+      fa.status = status_word(W.sync, B);
+      fa.uring = W.uring;
+      fa.V = W.Vc;
+      return rc(launch_faithful_chain(*w, packed, fa, grid, s));
+    }
+  }
+  // Per-step schedule (ERTD_MODE_FAITHFUL_STEPS, bf16, or grids too large to
+  // be resident): encoder(t), head(t), encoder(t-1), ... on one stream.
+  // (The status word is cleared so ertd_sample_status reads ok.)
+  ERTD_TRY(hipMemsetAsync(status_word(W.sync, B), 0, sizeof(unsigned), s));
   // A pipeline over several streams was measured and rejected: cross-queue
   // event hops inside a graph cost ~10 us each on ROCm 7.
   HeadArgs a{};
@@ -239,6 +303,18 @@ int ertd_sample(const ertd_weights* w, const float* packed, const float* cond,
   return enqueue_sample(w, packed, cond, cond_stride, B, L, num_steps, t_first, n_run, c1, c2,
                         sigma, freq, noise, seed, member_offset, mode, precision, x_inout, ws,
                         ws_bytes, (hipStream_t)stream);
+}
+
+int ertd_sample_status(const void* ws, int B, int L, int num_steps, int* status, void* stream) {
+  if (!ws || !status || B < 1 || L < 1 || num_steps < 1) return ERTD_EINVAL;
+  Ws W;
+  ws_layout(B, L, num_steps, ERTD_OP_SAMPLE, const_cast<void*>(ws), &W);
+  const unsigned* dev = status_word(W.sync, B);
+  unsigned v = 0;
+  ERTD_TRY(hipMemcpyAsync(&v, dev, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  ERTD_TRY(hipStreamSynchronize((hipStream_t)stream));
+  *status = (int)v;
+  return v == 0 ? ERTD_OK : ERTD_ETIMEOUT;
 }
 
 int ertd_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t, int tag,

@@ -17,7 +17,7 @@
 // The k-order inside each MFMA splits channels between the two half-waves
 // (lanes 0-31: channels c, lanes 32-63: channels c+7 / c+16), which keeps the
 // per-step LDS offset an immediate.
-#include "ertd_common.h"
+#include "enc_strip.h"
 
 namespace ertd {
 
@@ -119,38 +119,8 @@ hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// fp32 strip kernel
+// fp32 strip kernel (body: enc_strip.h)
 // ---------------------------------------------------------------------------
-// The cond image is dead once conv1's MFMAs have run, so the conv1 output
-// images alias it: 17.9 KB per workgroup -> 8 workgroups (32 waves) per CU.
-struct EncSmem {
-  union {
-    float X[4][CIN][XS];  // 4-phase cond image (15,232 B)
-    struct {
-      float E[C1][HS];    // conv1 output, even p (8,704 B)
-      float O[C1][HS];    // conv1 output, odd p  (8,704 B) -- must follow E
-    };
-  };
-  float red[2][C2];       // q-tile partial pool sums
-};
-
-template <int PAR>
-__device__ __forceinline__ void conv1_tile(f32x16& acc, const float (&a1)[STEPS1], const float* xb) {
-#pragma unroll
-  for (int s = 0; s < STEPS1; ++s) {
-    const int cp = s / 3, kk = s % 3;
-    // even p=2m taps cond 4j0-3+4m+kk -> X[kk][c][m]
-    // odd  p=2m+1 taps 4j0-1+4m+kk   -> X[2][c][m], X[3][c][m], X[0][c][m+1]
-    const int arr = PAR == 0 ? kk : (kk == 2 ? 0 : kk + 2);
-    const int add = (PAR == 1 && kk == 2) ? 1 : 0;
-    const float bv = xb[(arr * CIN + cp) * XS + add];
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], bv, acc, 0, 0, 0);
-  }
-}
-
-// TRAIN additionally stores what the backward needs (train.hip): the conv1
-// activations a1 (B,32,L1) at the conv1 positions this strip owns,
-// i in [2*j0, 2*j0 + 2J), and the conv2 ReLU mask m2 (B,64,L2) as bytes.
 // Optionally (tr.V != null) block number nstrip computes the time row v(tr.t)
 // for the faithful sampler's next head launch (time_row_lean: few registers).
 template <bool TRAIN>
@@ -164,89 +134,15 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
                                                        unsigned char* __restrict__ m2out,
                                                        int nstrip, TimeRowArgs tr) {
   __shared__ EncSmem sm;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   if (!TRAIN && (int)blockIdx.x >= nstrip) {
     float* f = &sm.X[0][0][0];  // e[128] | te[128] | part[2][128]
     time_row_lean(tr.w, packed, tr.freq, tr.t, tr.V + (size_t)tr.t * H, f, f + H,
                   reinterpret_cast<float(*)[H]>(f + 2 * H), tid);
     return;
   }
-  const int h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.x / S, strip = blockIdx.x - b * S;
-  const int j0 = strip * J;
-
-  float a1[STEPS1];
-#pragma unroll
-  for (int s = 0; s < STEPS1; ++s) a1[s] = packed[PACK_W1 + s * 64 + lane];
-
-  // ---- stage cond[b][:, 4j0-3 : 4j0-3+260] into the 4-phase image (zero padded)
-  const float* cb = cond + (long long)b * cstride;
-  stage_cond(sm.X, cb, L, 4 * j0 - 3, tid, [](float v) { return v; });
-  __syncthreads();
-
-  // ---- conv1 + bias + ReLU -> E / O (never leaves LDS; aliases X)
-  {
-    const int par = wave >> 1, mt = wave & 1;
-    const int m = mt * 32 + l32;
-    f32x16 acc = {};
-    const float* xb = &sm.X[0][0][0] + 7 * h * XS + m;
-    if (par == 0) conv1_tile<0>(acc, a1, xb);
-    else conv1_tile<1>(acc, a1, xb);
-    __syncthreads();  // every wave has read X: the images may now overwrite it
-    if (tid < C1) sm.E[tid][64] = 0.f;  // read only by the pad row q=63
-    float* dst = par ? &sm.O[0][0] : &sm.E[0][0];
-    const int i = 2 * j0 - 1 + 2 * m + par;       // global conv1 position
-    const bool valid = (i >= 0) && (i < L1);      // outside -> conv2's zero padding
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float v = fmaxf(acc[r] + b1[o], 0.f);
-      dst[o * HS + m] = valid ? v : 0.f;
-    }
-  }
-  __syncthreads();
-  if constexpr (TRAIN) {  // owned conv1 positions i = 2*j0 + r, r < 2J  (p = r + 1)
-    float* a1b = a1out + (size_t)b * C1 * L1;
-    for (int idx = tid; idx < C1 * 2 * J; idx += 256) {
-      const int c = idx / (2 * J), r = idx - c * (2 * J);
-      const int i = 2 * j0 + r;
-      if (i < L1) a1b[(size_t)c * L1 + i] = (r & 1) ? sm.E[c][(r + 1) >> 1] : sm.O[c][r >> 1];
-    }
-  }
-
-  // ---- conv2 + bias + ReLU + masked column sum
-  {
-    const int qt = wave & 1, ot = wave >> 1;
-    const int q = qt * 32 + l32;
-    float w2r[STEPS2];
-#pragma unroll
-    for (int s = 0; s < STEPS2; ++s) w2r[s] = packed[PACK_W2 + (ot * STEPS2 + s) * 64 + lane];
-    const float* eb = &sm.E[0][0] + 16 * h * HS + q;
-    f32x16 acc = {};
-#pragma unroll
-    for (int s = 0; s < STEPS2; ++s) {
-      const int cp = s / 3, kk = s % 3;
-      const int off = (kk == 1 ? C1 * HS : 0) + cp * HS + (kk == 2 ? 1 : 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(eb[off], w2r[s], acc, 0, 0, 0);
-    }
-    const int o = ot * 32 + l32;
-    const float bias = b2[o];
-    float sum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qq = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const bool valid = (qq < J) && (j0 + qq < L2);
-      const float z = acc[r] + bias;
-      const float v = fmaxf(z, 0.f);
-      sum += valid ? v : 0.f;
-      if constexpr (TRAIN) {
-        if (valid) m2out[((size_t)b * C2 + o) * L2 + j0 + qq] = z > 0.f ? 1 : 0;
-      }
-    }
-    sum += __shfl_xor(sum, 32);
-    if (h == 0) sm.red[qt][o] = sum;
-  }
-  __syncthreads();
+  enc_strip_fp32<TRAIN>(sm, packed, b1, b2, cond, cstride, L, L1, L2, b, strip, a1out, m2out, tid);
   if (tid < C2) partial[((size_t)b * S + strip) * C2 + tid] = sm.red[0][tid] + sm.red[1][tid];
   if (!TRAIN && tr.V) {
     // Warm this XCD's L2 with a slice of the weights the next head_step reads

@@ -85,16 +85,23 @@ __device__ inline float philox_normal(uint64_t seed, uint32_t member, uint32_t t
 template <typename Tx, typename Cvt>
 __device__ __forceinline__ void stage_cond(Tx (*X)[CIN][XS], const float* __restrict__ cb, int L,
                                            int pos0, int tid, Cvt cvt) {
+  // addresses are clamped into the row and the value selected afterwards:
+  // unconditional loads, no branches (the loads may not be speculable)
   float v[CIN];
   const int pos = pos0 + tid;
   const bool in = pos >= 0 && pos < L;
+  const int pc = pos < 0 ? 0 : (pos >= L ? L - 1 : pos);
 #pragma unroll
-  for (int c = 0; c < CIN; ++c) v[c] = in ? cb[(size_t)c * L + pos] : 0.f;
+  for (int c = 0; c < CIN; ++c) v[c] = cb[(size_t)c * L + pc];
+#pragma unroll
+  for (int c = 0; c < CIN; ++c) v[c] = in ? v[c] : 0.f;
   float vt = 0.f;
   const int tc = tid >> 2, tu = 256 + (tid & 3);
   if (tid < CIN * 4) {
     const int p2 = pos0 + tu;
-    vt = (p2 >= 0 && p2 < L) ? cb[(size_t)tc * L + p2] : 0.f;
+    const int p2c = p2 < 0 ? 0 : (p2 >= L ? L - 1 : p2);
+    vt = cb[(size_t)tc * L + p2c];
+    vt = (p2 >= 0 && p2 < L) ? vt : 0.f;
   }
 #pragma unroll
   for (int c = 0; c < CIN; ++c) X[tid & 3][c][tid >> 2] = cvt(v[c]);
@@ -204,6 +211,33 @@ hipError_t launch_q_sample(const float* x0, const int64_t* t, const float* noise
                            const float* alpha_bar, int B, int P, float* out, hipStream_t s);
 hipError_t launch_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t,
                                 int tag, float* out, hipStream_t s);
+// chain.hip: persistent faithful sampler (one launch per chain)
+struct FaithfulChainArgs {
+  const float* cond; long long cstride; int L; int B; int S; int R;
+  int n_run; int t_first; int num_steps;
+  const float* c1; const float* c2; const float* sigma; const float* freq; const float* noise;
+  uint64_t seed; uint32_t member_offset;
+  float* x;                      // (B, P) in/out
+  float* part;                   // R ring slots of (B, S, 64) strip partials
+  // sync words, one per SYNC_PAD-word line:
+  unsigned* cnt;                 // (R, B) monotonic strip arrival counters
+  unsigned* progress;            // (B) steps consumed by each chain
+  unsigned* claim;               // (B) next strip item of each member (worker tickets)
+  unsigned* status;              // 0 = ok, else the code of the wait that timed out
+  unsigned* uflag;               // (R, B) step+1 of the u row in each ring slot
+  unsigned* vready;              // (1) time rows published so far
+  float* uring;                  // (R, B, 128) condition rows u_i[b]
+  float* V;                      // (n_run, 128) time rows v(t_first - i)
+};
+constexpr int CHAIN_RING = 8;
+// Every sync word of the chain sits alone in a 128-B line: words polled or
+// updated by hundreds of blocks serialize per line (measured: progress words
+// of 16 members sharing one line slowed every memory access on the chip 3-5x).
+constexpr int SYNC_PAD = 32;
+// grid for launch_faithful_chain (0: B too large for a resident grid)
+int faithful_chain_grid(int B, int S);
+hipError_t launch_faithful_chain(const ertd_weights& w, const float* packed,
+                                 const FaithfulChainArgs& a, int grid, hipStream_t s);
 // train.hip
 size_t train_ws_floats(int B, int L, int* offs);
 hipError_t launch_train_forward(const ertd_weights& w, const float* packed, const float* x_in,

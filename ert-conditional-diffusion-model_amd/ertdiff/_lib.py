@@ -23,8 +23,9 @@ ERTD_OK = 0
 ERTD_EINVAL = -1
 ERTD_ENOSPC = -2
 ERTD_ENOGPU = -3
+ERTD_ETIMEOUT = -4
 OP_FORWARD, OP_SAMPLE, OP_TRAIN = 0, 1, 2
-MODE_HOISTED, MODE_FAITHFUL = 0, 1
+MODE_HOISTED, MODE_FAITHFUL, MODE_FAITHFUL_STEPS = 0, 1, 2
 PREC_FP32, PREC_BF16 = 0, 1
 HIDDEN = 128
 PMAX = 32
@@ -59,6 +60,7 @@ SIGNATURES = {
     "ertd_sample": (_I, [_W, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I, _VP, _VP, _VP, _VP,
                          _VP, _U64, _U32, _I, _I, _VP, _VP, _SZ, _VP]),
     "ertd_philox_normal": (_I, [_U64, _U32, _I, _I, _I, _I, _VP, _VP]),
+    "ertd_sample_status": (_I, [_VP, _I, _I, _I, ctypes.POINTER(_I), _VP]),
     "ertd_sample_plan_create": (_I, [_W, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I, _VP, _VP,
                                      _VP, _VP, _VP, _U64, _U32, _I, _I, _VP, _VP, _SZ,
                                      ctypes.POINTER(_VP)]),

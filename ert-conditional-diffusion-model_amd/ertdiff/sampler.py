@@ -5,11 +5,15 @@ libertdiff_hip.so:
 
   mode="hoisted"  (default) condition encoder once per call, then one
                   persistent kernel runs all steps with x in registers.
-  mode="faithful" encoder re-evaluated every step exactly like the reference
-                  (two kernels per step).
+  mode="faithful" encoder re-evaluated every step exactly like the reference:
+                  one persistent launch per chain (encoder strips streamed
+                  ahead of per-member step chains), or the per-step schedule
+                  when the grid cannot be resident;
+  mode="faithful_steps"  faithful, forced per-step schedule (an encoder and a
+                  head launch per step).
 
-Both modes are bit-identical: the encoder is deterministic (fixed-order
-reductions) and both share the per-step device code.
+All modes are bit-identical: the encoder is deterministic (fixed-order
+reductions) and every schedule runs the same fma chains in the same order.
 
 Noise sources (keyword ``noise``):
   "torch"   (default) x_T and every z_t drawn with torch.randn on ``device``
@@ -31,7 +35,20 @@ from . import _lib
 from .model import _PREC, ConditionalDiffusionModel, STATE_KEYS
 from .schedule import step_tables, timestep_frequencies
 
-_MODES = {"hoisted": _lib.MODE_HOISTED, "faithful": _lib.MODE_FAITHFUL}
+_MODES = {"hoisted": _lib.MODE_HOISTED, "faithful": _lib.MODE_FAITHFUL,
+          "faithful_steps": _lib.MODE_FAITHFUL_STEPS}
+
+
+def sample_status(ws: torch.Tensor, B: int, L: int, num_steps: int) -> int:
+    """Status word of the last faithful run on ``ws`` (synchronizes): 0 = ok,
+    else the code of the persistent-chain wait that timed out."""
+    st = ctypes.c_int(0)
+    with torch.cuda.device(ws.device):
+        rc = _lib.lib().ertd_sample_status(ws.data_ptr(), B, L, num_steps, ctypes.byref(st),
+                                           _lib.stream_of(ws.device))
+    if rc not in (_lib.ERTD_OK, _lib.ERTD_ETIMEOUT):
+        _lib.check(rc, "sample_status")
+    return st.value
 
 
 def as_ertdiff_model(model, device) -> ConditionalDiffusionModel:
@@ -121,7 +138,7 @@ def sample_model(model, condition, T, betas, alphas, alpha_bar, param_dim, devic
     """Drop-in for sample_model (ERT_Conditional_Diffusion.py:102-119).
 
     Returns x_0 (B, param_dim) in the unconstrained space.  Extra keywords:
-    mode ("hoisted"|"faithful"), noise ("torch"|"philox"|tensor), seed and
+    mode ("hoisted"|"faithful"|"faithful_steps"), noise ("torch"|"philox"|tensor), seed and
     member_offset (philox), precision ("fp32"|"bf16", default: the model's),
     shared_condition + n_members: one (1,14,L) / (14,L) condition shared by
     n_members ensemble members (read in place, never replicated).
@@ -166,6 +183,9 @@ def sample_model(model, condition, T, betas, alphas, alpha_bar, param_dim, devic
     with torch.cuda.device(dev):
         _lib.check(_lib.lib().ertd_sample(*prep.args(B, x, inj, seed, member_offset, mode,
                                                      n - 1, n, ws), _lib.stream_of(dev)), "sample")
+    if mode != "hoisted" and sample_status(ws, B, prep.L, n) != 0:
+        raise RuntimeError("ertdiff: the persistent faithful sampler timed out (GPU shared with "
+                           "other work?); x is not valid")
     return x
 
 
@@ -216,6 +236,10 @@ class SamplerPlan:
                               self.mode, self.t_first, self.n_run, self.ws)
         with torch.cuda.device(self.dev):
             _lib.check(_lib.lib().ertd_sample(*args, s), "sample")
+
+    def status(self) -> int:
+        """0, or the timeout code of the last faithful replay (synchronizes)."""
+        return sample_status(self.ws, self.B, self.prep.L, self.prep.num_steps)
 
     def close(self):
         if self._plan:

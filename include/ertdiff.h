@@ -36,6 +36,7 @@ extern "C" {
 #define ERTD_EINVAL (-1)   /* bad shape / null pointer / unsupported dim */
 #define ERTD_ENOSPC (-2)   /* workspace too small */
 #define ERTD_ENOGPU (-3)   /* no gfx950 device / kernel image unavailable */
+#define ERTD_ETIMEOUT (-4) /* a persistent sampler wait timed out (see ertd_sample_status) */
 
 #define ERTD_CIN 14
 #define ERTD_HIDDEN 128
@@ -67,7 +68,11 @@ typedef struct ertd_weights {
 
 /* Sampler modes. */
 #define ERTD_MODE_HOISTED 0  /* condition encoder once, persistent T-loop   */
-#define ERTD_MODE_FAITHFUL 1 /* encoder re-evaluated every step (reference) */
+#define ERTD_MODE_FAITHFUL 1 /* encoder re-evaluated every step (reference):
+                                one persistent launch per chain when the grid
+                                fits, else the per-step schedule            */
+#define ERTD_MODE_FAITHFUL_STEPS 2 /* faithful, forced per-step schedule:
+                                      encoder + head launch per step        */
 
 /* Encoder operand precision. */
 #define ERTD_PREC_FP32 0
@@ -132,12 +137,19 @@ int ertd_forward(const ertd_weights* w, const float* packed, const float* x,
  *   noise: NULL -> counter-based Philox keyed by (seed, member_offset+b, t);
  *     else (num_steps, B, P) injected draws in reference order: noise[k] is
  *     the z used at t = num_steps-k (noise[0] = x_T is not read).
- *   mode: ERTD_MODE_HOISTED / ERTD_MODE_FAITHFUL (bit-identical outputs).  */
+ *   mode: ERTD_MODE_HOISTED / ERTD_MODE_FAITHFUL / ERTD_MODE_FAITHFUL_STEPS
+ *     (bit-identical outputs).                                            */
 int ertd_sample(const ertd_weights* w, const float* packed, const float* cond,
                 long long cond_stride, int B, int L, int num_steps, int t_first, int n_run,
                 const float* c1, const float* c2, const float* sigma, const float* freq,
                 const float* noise, uint64_t seed, uint32_t member_offset, int mode,
                 int precision, float* x_inout, void* ws, size_t ws_bytes, void* stream);
+
+/* Status word of the last persistent faithful chain run on `ws` (same B, L,
+ * num_steps as the ertd_sample call): synchronizes `stream`; *status = 0 and
+ * ERTD_OK, or the code of the wait that timed out and ERTD_ETIMEOUT (the
+ * launch then drained without finishing; x_inout is not valid).           */
+int ertd_sample_status(const void* ws, int B, int L, int num_steps, int* status, void* stream);
 
 /* Standard normals from the sampler's Philox stream: out (B,P) for members
  * member_offset..+B-1 at step `t`, stream tag `tag` (0 = step noise z_t,

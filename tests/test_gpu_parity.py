@@ -81,7 +81,7 @@ def _sched(T, dev):
     return ertdiff.get_diffusion_schedule(T, device=dev)
 
 
-@pytest.mark.parametrize("mode", ["hoisted", "faithful"])
+@pytest.mark.parametrize("mode", ["hoisted", "faithful", "faithful_steps"])
 def test_sampler_vs_golden(mode, gpu_model, sampler_kat, cuda_dev):
     cond = torch.from_numpy(synth_uniform((8, 14, 4693), int(sampler_kat["r1_cs"]))).to(cuda_dev)
     noise = torch.from_numpy(sampler_kat["r1_noise"]).to(cuda_dev)
@@ -103,9 +103,54 @@ def test_faithful_equals_hoisted_bitwise(gpu_model, cuda_dev):
     cond = torch.from_numpy(synth_uniform((16, 14, 4693), 91)).to(cuda_dev)
     sched = _sched(200, cuda_dev)
     xs = [ertdiff.sample_model(gpu_model, cond, 200, *sched, 29, cuda_dev, mode=m,
-                               noise="philox", seed=1234) for m in ("hoisted", "faithful")]
-    assert torch.equal(xs[0], xs[1])
+                               noise="philox", seed=1234)
+          for m in ("hoisted", "faithful", "faithful_steps")]
+    assert torch.equal(xs[0], xs[1]) and torch.equal(xs[0], xs[2])
     assert torch.isfinite(xs[0]).all()
+
+
+@pytest.mark.parametrize("B,L,T", [(1, 1, 3), (3, 37, 20), (5, 250, 17), (2, 4694, 9),
+                                   (7, 1003, 40), (40, 4693, 12)])
+def test_faithful_schedules_bitwise(B, L, T, gpu_model, cuda_dev):
+    """The persistent chain (ring of 8 slots: T > 8 wraps it), the per-step
+    schedule and the hoisted sampler agree bit for bit on ragged shapes, with
+    injected (reference-order) noise."""
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 500 + L)).to(cuda_dev)
+    noise = torch.from_numpy(synth_normal((T, B, 29), 600 + B)).to(cuda_dev)
+    sched = _sched(T, cuda_dev)
+    xs = {m: ertdiff.sample_model(gpu_model, cond, T, *sched, 29, cuda_dev, mode=m, noise=noise)
+          for m in ("faithful", "faithful_steps", "hoisted")}
+    assert torch.equal(xs["faithful"], xs["faithful_steps"])
+    assert torch.equal(xs["faithful"], xs["hoisted"])
+    assert torch.isfinite(xs["faithful"]).all()
+
+
+def test_faithful_chain_shared_condition(gpu_model, cuda_dev):
+    cond1 = torch.from_numpy(synth_uniform((1, 14, 4693), 97)).to(cuda_dev)
+    sched = _sched(30, cuda_dev)
+    a = ertdiff.sample_model(gpu_model, cond1, 30, *sched, 29, cuda_dev, noise="philox", seed=8,
+                             shared_condition=True, n_members=24, mode="faithful")
+    b = ertdiff.sample_model(gpu_model, cond1, 30, *sched, 29, cuda_dev, noise="philox", seed=8,
+                             shared_condition=True, n_members=24, mode="hoisted")
+    assert torch.equal(a, b)
+
+
+def test_faithful_chain_status_and_rerun(gpu_model, cuda_dev):
+    """Plan replays re-zero the chain's counters and granules every call."""
+    cond = torch.from_numpy(synth_uniform((8, 14, 4693), 98)).to(cuda_dev)
+    sched = _sched(40, cuda_dev)
+    x0 = ertdiff.philox_normal(8, 29, 40, 1, 4, 0, cuda_dev)
+    p = ertdiff.SamplerPlan(gpu_model, cond, 40, *sched, mode="faithful", seed=4)
+    outs = []
+    for _ in range(3):
+        p.x.copy_(x0)
+        p.launch()
+        assert p.status() == 0
+        outs.append(p.x.clone())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    ref = ertdiff.sample_model(gpu_model, cond, 40, *sched, 29, cuda_dev, mode="hoisted",
+                               noise="philox", seed=4)
+    assert torch.equal(outs[0], ref)
 
 
 def test_deterministic_rerun(gpu_model, cuda_dev):
@@ -149,7 +194,7 @@ def test_graph_plan_matches_direct(gpu_model, cuda_dev):
     cond = torch.from_numpy(synth_uniform((8, 14, 4693), 94)).to(cuda_dev)
     sched = _sched(60, cuda_dev)
     x0 = ertdiff.philox_normal(8, 29, 60, 1, 3, 0, cuda_dev)
-    for mode in ("faithful", "hoisted"):
+    for mode in ("faithful", "faithful_steps", "hoisted"):
         # the chain split into two graph segments == one direct call
         pa = ertdiff.SamplerPlan(gpu_model, cond, 60, *sched, t_first=59, n_run=25, mode=mode, seed=3)
         pb = ertdiff.SamplerPlan(gpu_model, cond, 60, *sched, t_first=34, n_run=35, mode=mode, seed=3)
