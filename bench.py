@@ -14,9 +14,17 @@ barrier + synchronize on each side, max over ranks.  One process per GPU
 noise keyed by global member id) and the only collective on the data path is
 one RCCL broadcast of the conditioning tensor from rank 0 before timing.
 
+The faithful chain runs as ONE persistent kernel per chain
+(faithful_chain_kernel: encoder strip workers streaming ahead of per-member
+step chains, chain.hip); mode "faithful_steps" times the per-step schedule
+(an encoder and a head launch per step) instead.
+
 Extra objects on the JSON line:
-  roofline      the strip kernel (conv1+conv2+pool partials), timed per launch
-                with HIP events on the launching stream; fp32 MFMA-bound.
+  roofline      the dominant kernel: faithful_chain_kernel (fp32 faithful) --
+                algorithmic FLOP of the reference model per member-step x B x
+                steps per launch / launch duration (HIP events on the launching
+                stream); fp32 MFMA-bound.  extra.roofline_strip: the per-step
+                schedule's strip kernel the same way.
   cpu_baseline  the reference algorithm on PyTorch-CPU (oracle/ref_torch.py,
                 bit-identical to the reference) on rank 0, bounded sample.
 """
@@ -55,15 +63,18 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=1000, help="untimed steps (a multiple of T keeps every chain launch T steps long)")
     ap.add_argument("--batch", type=int, default=64, help="members per GPU")
     ap.add_argument("--T", type=int, default=1000)
-    ap.add_argument("--mode", choices=["faithful", "hoisted"], default="faithful")
+    ap.add_argument("--mode", choices=["faithful", "faithful_steps", "hoisted"], default="faithful")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hoisted", action="store_true", help="skip the secondary hoisted timing")
     ap.add_argument("--no-train", action="store_true", help="skip the secondary train-step timing")
+    ap.add_argument("--no-strip-roofline", action="store_true")
+    ap.add_argument("--no-steps-schedule", action="store_true",
+                    help="skip the secondary per-step-schedule timing")
     ap.add_argument("--roofline-reps", type=int, default=200)
     return ap.parse_args()
 
@@ -92,6 +103,7 @@ def make_plans(model, cond, sched, T, B, mode, seed, member_offset):
             cache[n_run] = ertdiff.SamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=n_run,
                                                mode=mode, seed=seed, member_offset=member_offset, B=B)
         return cache[n_run]
+    plan.cache = cache
     return plan
 
 
@@ -131,6 +143,47 @@ def time_steps(plan_of, n_steps, T, x_T, world, dev):
     return el
 
 
+def _traffic(key):
+    pmc = os.path.join(ROOT, "profiles", "kernel_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        if key in rec:
+            return rec[key]["hbm_bytes_per_launch"]
+    return None
+
+
+def chain_kernel_roofline(plan, B, T, reps, dev):
+    """Average duration of one faithful_chain_kernel launch (a whole T-step
+    chain), HIP events on the launching stream around plan replays."""
+    stream = torch.cuda.current_stream(dev)
+    x0 = plan.x.clone()
+    ms = []
+    for _ in range(reps):
+        plan.x.copy_(x0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        plan.launch(stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms.append(e0.elapsed_time(e1))
+    st = plan.status()
+    if st != 0:
+        raise RuntimeError(f"faithful chain timed out (status {st}; launch ms {ms})")
+    avg_ms = sum(ms) / len(ms)
+    flop = STEP_FLOP_PER_MEMBER * B * T
+    achieved = flop / (avg_ms * 1e-3) / 1e12
+    return {"kernel": "faithful_chain_kernel", "bound": "mfma", "achieved": round(achieved, 3),
+            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "traffic": _traffic(f"chain_B{B}_T{T}"),
+            "avg_us": round(avg_ms * 1e3, 1), "min_us": round(min(ms) * 1e3, 1),
+            "timing": f"HIP events around {reps} launches of the {T}-step chain (sync-word zeroing kernel + chain kernel)",
+            "algorithmic_flop_per_launch": flop,
+            "flop_basis": f"{STEP_FLOP_PER_MEMBER} FLOP per member-step (reference model: conv "
+                          f"{CONV_FLOP_PER_MEMBER} + Linear layers) x {B} members x {T} steps",
+            "algorithmic_bytes_per_launch": COND_BYTES_PER_MEMBER * B * T}
+
+
 def strip_kernel_roofline(model, cond, B, precision, reps, dev):
     """Average duration of the encoder strip kernel, HIP events on its stream."""
     L = cond.shape[2]
@@ -162,14 +215,7 @@ def strip_kernel_roofline(model, cond, B, precision, reps, dev):
     flop = CONV_FLOP_PER_MEMBER * B
     achieved = flop / (avg_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if precision == "bf16" else PEAK_FP32_TFLOPS
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "strip_kernel_traffic.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            rec = json.load(f)
-        key = f"B{B}_{precision}"
-        if key in rec:
-            traffic = rec[key]["hbm_bytes_per_launch"]
+    traffic = _traffic(f"strip_B{B}_{precision}")
     return {"kernel": "enc_fp32_kernel" if precision == "fp32" else "enc_bf16_kernel",
             "bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -277,15 +323,30 @@ def main():
     torch.cuda.synchronize(dev)
     el = time_steps(plan_of, a.steps, T, x_T, world, dev)
     value = world * a.steps / el
+    if a.mode != "hoisted":
+        for n, p in plan_of.cache.items():
+            if p.status() != 0:
+                raise RuntimeError(f"faithful sampler plan n_run={n} timed out (status {p.status()})")
 
     extra = {}
+    if a.mode == "faithful" and not a.no_steps_schedule:
+        splan = make_plans(model, cond, sched, T, B, "faithful_steps", 2042, offset)
+        prepare(splan, T, T, x_T)
+        sel = time_steps(splan, T, T, x_T, world, dev)
+        extra["faithful_steps_schedule_steps_per_s"] = round(world * T / sel, 1)
     if not a.no_hoisted and a.mode == "faithful":
         hplan = make_plans(model, cond, sched, T, B, "hoisted", 2042, offset)
         prepare(hplan, T, T, x_T)
         run_steps(hplan, T, T, x_T)
         hel = time_steps(hplan, T, T, x_T, world, dev)
         extra["hoisted_steps_per_s"] = round(world * T / hel, 1)
-    roof = strip_kernel_roofline(model, cond, B, a.precision, a.roofline_reps, dev)
+    roof_strip = None if a.no_strip_roofline else strip_kernel_roofline(model, cond, B, a.precision,
+                                                                        a.roofline_reps, dev)
+    if a.mode == "faithful" and a.precision == "fp32":
+        roof = chain_kernel_roofline(plan_of(T), B, T, 5, dev)
+        extra["roofline_strip"] = roof_strip
+    else:
+        roof = roof_strip
     if not a.no_train:
         extra.update(train_bench(dev))
     cpu = None

@@ -115,7 +115,7 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
   if (mode == ERTD_MODE_FAITHFUL && precision == ERTD_PREC_FP32) {
     const int grid = faithful_chain_grid(B, S);
     if (grid > 0) {
-      ERTD_TRY(hipMemsetAsync(W.sync, 0, W.zero_bytes, s));
+      ERTD_TRY(launch_zero_words(W.sync, W.zero_bytes / sizeof(unsigned), s));
       FaithfulChainArgs fa{};
       fa.cond = cond;
       fa.cstride = cstride;
@@ -149,7 +149,7 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
   // Per-step schedule (ERTD_MODE_FAITHFUL_STEPS, bf16, or grids too large to
   // be resident): encoder(t), head(t), encoder(t-1), ... on one stream.
   // (The status word is cleared so ertd_sample_status reads ok.)
-  ERTD_TRY(hipMemsetAsync(status_word(W.sync, B), 0, sizeof(unsigned), s));
+  ERTD_TRY(launch_zero_words(status_word(W.sync, B), 1, s));
   // A pipeline over several streams was measured and rejected: cross-queue
   // event hops inside a graph cost ~10 us each on ROCm 7.
   HeadArgs a{};

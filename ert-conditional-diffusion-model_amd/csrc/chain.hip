@@ -496,6 +496,20 @@ int faithful_chain_grid(int B, int S) {
   return (int)(want < cached[dev] ? want : cached[dev]);
 }
 
+// Clears the chain's sync words before each launch.  Our own kernel rather
+// than hipMemsetAsync: a memset node replayed from a hipGraph was observed to
+// fill the block with a stale non-zero pattern (0xA5251C00 in every word)
+// after unrelated launches on the stream (ROCm 7.x runtime, MI355X).
+__global__ __launch_bounds__(256) void zero_words_kernel(unsigned* __restrict__ p, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) p[i] = 0u;
+}
+
+hipError_t launch_zero_words(unsigned* p, size_t n, hipStream_t s) {
+  const size_t blocks = (n + 255) / 256;
+  zero_words_kernel<<<(unsigned)(blocks < 1024 ? blocks : 1024), 256, 0, s>>>(p, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_faithful_chain(const ertd_weights& w, const float* packed,
                                  const FaithfulChainArgs& a, int grid, hipStream_t s) {
   faithful_chain_kernel<<<grid, 256, 0, s>>>(w, packed, a);

@@ -236,6 +236,7 @@ constexpr int CHAIN_RING = 8;
 constexpr int SYNC_PAD = 32;
 // grid for launch_faithful_chain (0: B too large for a resident grid)
 int faithful_chain_grid(int B, int S);
+hipError_t launch_zero_words(unsigned* p, size_t n, hipStream_t s);
 hipError_t launch_faithful_chain(const ertd_weights& w, const float* packed,
                                  const FaithfulChainArgs& a, int grid, hipStream_t s);
 // train.hip

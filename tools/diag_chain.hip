@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
   printf("B=%d T=%d S=%d R=%d grid=%d (workers %d)\n", B, T, S, R, grid, grid - B - 1);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   for (int rep = 0; rep < 3; ++rep) {
-    CK(hipMemsetAsync(zero, 0, zb, 0));
+    CK(launch_zero_words((unsigned*)zero, zb / 4, 0));
     hipEventRecord(e0, 0);
     CK(launch_faithful_chain(w, packed, fa, grid, 0));
     hipEventRecord(e1, 0);

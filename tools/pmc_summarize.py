@@ -1,34 +1,41 @@
-"""Per-launch HBM bytes of the encoder strip kernel from two rocprofv3 --pmc
-passes (tools/pmc_traffic.sh).  FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
+"""Per-launch HBM bytes of the hot kernels from two rocprofv3 --pmc passes
+(tools/pmc_traffic.sh).  FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of a coalesced stream, so reads are doubled
-(MI355X_MICROARCH.md, HBM section).  Infinity-Cache hits are counted too."""
+(MI355X_MICROARCH.md, HBM section).  Infinity-Cache hits are counted too.
+Writes profiles/kernel_traffic.json (read by bench.py's roofline objects)."""
 import csv, glob, json, os, statistics, sys
 
-KERNEL = "enc_fp32_kernel<false>"
+KERNELS = {  # json key -> kernel-name substring (bench.py R2 shape, fp32)
+    "chain_B64_T1000": "faithful_chain_kernel",
+    "strip_B64_fp32": "enc_fp32_kernel<false>",
+}
 
 
-def per_launch(d, counter):
+def per_launch(d, counter, name):
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if name in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     return vals
 
 
 fetch_dir, write_dir, out = sys.argv[1:4]
-fk, wk = per_launch(fetch_dir, "FETCH_SIZE"), per_launch(write_dir, "WRITE_SIZE")
-if not fk or not wk:
-    sys.exit(f"no {KERNEL} rows ({len(fk)} fetch, {len(wk)} write)")
-f_med, w_med = statistics.median(fk), statistics.median(wk)
 rec = json.load(open(out)) if os.path.exists(out) else {}
-rec["B64_fp32"] = {
-    "hbm_bytes_per_launch": int(2 * f_med * 1024 + w_med * 1024),
-    "fetch_size_kib_median": f_med, "write_size_kib_median": w_med,
-    "launches": [len(fk), len(wk)],
-    "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
-              "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
-    "workload": "bench.py R2 faithful, B=64, L=4693",
-}
+for key, name in KERNELS.items():
+    fk, wk = per_launch(fetch_dir, "FETCH_SIZE", name), per_launch(write_dir, "WRITE_SIZE", name)
+    if not fk or not wk:
+        print(f"no {name} rows ({len(fk)} fetch, {len(wk)} write)")
+        continue
+    f_med, w_med = statistics.median(fk), statistics.median(wk)
+    rec[key] = {
+        "kernel": name,
+        "hbm_bytes_per_launch": int(2 * f_med * 1024 + w_med * 1024),
+        "fetch_size_kib_median": f_med, "write_size_kib_median": w_med,
+        "launches": [len(fk), len(wk)],
+        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
+                  "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
+        "workload": "bench.py R2 faithful, B=64, L=4693, T=1000 (chain: one launch = 1000 steps)",
+    }
+    print(key, json.dumps(rec[key]))
 json.dump(rec, open(out, "w"), indent=1)
-print(json.dumps(rec["B64_fp32"]))
