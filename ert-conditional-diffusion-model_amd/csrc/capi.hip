@@ -323,6 +323,17 @@ int ertd_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int 
   return rc(launch_philox_normal(seed, member_offset, B, P, t, tag, out, (hipStream_t)stream));
 }
 
+int ertd_postprocess(const float* u, long long rows, int P, double a, double b,
+                     const double* min_, const double* scale_, const double* limits, float* out,
+                     uint8_t* valid, void* stream) {
+  if (!u || !min_ || !scale_ || !limits || !out || !valid || rows < 0 || P < 1 || P > PMAX)
+    return ERTD_EINVAL;
+  if (rows == 0) return ERTD_OK;
+  if (rows > (long long)8 * 0x7fffffff) return ERTD_EINVAL;
+  return rc(launch_postproc(u, rows, P, (float)a, (float)(b - a), min_, scale_, limits, out, valid,
+                            (hipStream_t)stream));
+}
+
 int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const float* cond,
                             long long cond_stride, int B, int L, int num_steps, int t_first,
                             int n_run, const float* c1, const float* c2, const float* sigma,

@@ -209,6 +209,9 @@ hipError_t launch_timestep_embedding(const int64_t* t, int B, int dim, const flo
                                      float* out, hipStream_t s);
 hipError_t launch_q_sample(const float* x0, const int64_t* t, const float* noise,
                            const float* alpha_bar, int B, int P, float* out, hipStream_t s);
+hipError_t launch_postproc(const float* u, long long rows, int P, float a, float bma,
+                           const double* min_, const double* scale_, const double* limits,
+                           float* out, uint8_t* valid, hipStream_t s);
 hipError_t launch_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t,
                                 int tag, float* out, hipStream_t s);
 // chain.hip: persistent faithful sampler (one launch per chain)

@@ -13,6 +13,7 @@ from .sampler import SamplerPlan, as_ertdiff_model, draw_reference_noise, philox
 from .schedule import get_diffusion_schedule, step_tables, timestep_frequencies
 from .train import DiffusionForwardFn, train_step, validation_loss
 from .ensemble import member_range, sample_ensemble
+from .postproc import compact, postprocess, sample_realisations
 
 __all__ = [
     "ConditionalDiffusionModel", "get_timestep_embedding", "get_diffusion_schedule", "q_sample",
@@ -20,5 +21,5 @@ __all__ = [
     "step_tables", "timestep_frequencies", "transform_to_unconstrained", "inverse_transform",
     "DiffusionDataset", "check_param_bounds", "bounds_mask", "load_best_model",
     "save_checkpoint", "STATE_KEYS", "train_step", "validation_loss", "DiffusionForwardFn",
-    "sample_ensemble", "member_range",
+    "sample_ensemble", "member_range", "postprocess", "sample_realisations", "compact",
 ]

@@ -70,6 +70,8 @@ SIGNATURES = {
     "ertd_adam": (_I, [_W, _VP, _VP, _VP, _I, _F, _F, _F, _F, _VP]),
     "ertd_train_step": (_I, [_W, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _I, _F,
                              _F, _F, _F, _VP, _VP, _SZ, _VP]),
+    "ertd_postprocess": (_I, [_VP, ctypes.c_longlong, _I, ctypes.c_double, ctypes.c_double, _VP,
+                              _VP, _VP, _VP, _VP, _VP]),
     "ertd_plan_launch": (_I, [_VP, _VP]),
     "ertd_plan_destroy": (_I, [_VP]),
 }

@@ -59,9 +59,10 @@ class DiffusionDataset(Dataset):
 
 
 def bounds_mask(param: np.ndarray, limits: np.ndarray) -> np.ndarray:
-    """Row validity of (n, P) parameter sets against (P, 2) [min, max] limits."""
+    """Row validity of (n, P) parameter sets against (P, 2) [min, max] limits:
+    rejected when some value is < min or > max (:205-207; a NaN passes)."""
     lo, hi = limits[:, 0], limits[:, 1]
-    return np.all((param >= lo) & (param <= hi), axis=1)
+    return ~np.any((param < lo) | (param > hi), axis=1)
 
 
 def check_param_bounds(param: np.ndarray, limits: np.ndarray, verbose: bool = True) -> Optional[np.ndarray]:

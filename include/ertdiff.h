@@ -157,6 +157,19 @@ int ertd_sample_status(const void* ws, int B, int L, int num_steps, int* status,
 int ertd_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t,
                        int tag, float* out, void* stream);
 
+/* Ensemble post-processing (ERT_Conditional_Diffusion.py:400-406, :1054-1060):
+ * u (rows, P) unconstrained samples (sample_model output) ->
+ *   out (rows, P) = param_scaler.inverse_transform(inverse_transform(u, a, b))
+ *     (sigmoid in float32; then MinMaxScaler's float64 min_/scale_ applied as
+ *      x -= min_; x /= scale_ on the float32 array, each op rounded to float32)
+ *   valid (rows) uint8 = 1 unless check_param_bounds (:183-218) rejects the row
+ *     (any value < limits[p][0] or > limits[p][1], compared in float64).
+ * min_, scale_: (P) float64 (a fitted MinMaxScaler's min_ and scale_);
+ * limits: (P, 2) float64 [min, max] (Generate_ERT_utils.ParameterLimits.plims). */
+int ertd_postprocess(const float* u, long long rows, int P, double a, double b,
+                     const double* min_, const double* scale_, const double* limits, float* out,
+                     uint8_t* valid, void* stream);
+
 /* hipGraph plans: capture one full ertd_sample call (all kernels of all
  * steps) once, replay with ertd_plan_launch.  Buffers are bound at creation. */
 typedef struct ertd_plan ertd_plan;

@@ -238,10 +238,27 @@ def inverse_transform(u, a, b):
 
 
 def bounds_mask(params, limits) -> np.ndarray:
-    """check_param_bounds :183-218 as a per-row validity mask."""
+    """check_param_bounds :183-218 as a per-row validity mask: a row is rejected
+    when some value is < min or > max (so a NaN passes, as in the reference)."""
     lo = limits[:, 0]
     hi = limits[:, 1]
-    return np.all((params >= lo) & (params <= hi), axis=1)
+    return ~np.any((params < lo) | (params > hi), axis=1)
+
+
+def postprocess_chain(u, min_, scale_, limits, a=0.0, b=1.0):
+    """The post-sampling chain of :400-406 / :1054-1060 on a float32 (rows, P)
+    array: sigmoid inverse_transform in float32 (torch op on a float32 tensor:
+    (b-a) and a enter as float32 scalars), then sklearn MinMaxScaler's
+    in-place ``x -= min_; x /= scale_`` (float64 operands, result stored back
+    into the float32 array), then check_param_bounds as a mask."""
+    u = np.asarray(u, np.float32)
+    # torch.sigmoid on float32 = 1/(1+exp(-u)) with float32 rounding per op
+    e = np.exp(-u.astype(np.float64)).astype(np.float32)
+    s = (np.float32(1.0) / (np.float32(1.0) + e)).astype(np.float32)
+    x = (np.float32(a) + np.float32(b - a) * s).astype(np.float32)
+    x = (x.astype(np.float64) - min_).astype(np.float32)
+    x = (x.astype(np.float64) / scale_).astype(np.float32)
+    return x, bounds_mask(x, limits)
 
 
 def rel_l2(a, b) -> float:

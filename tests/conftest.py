@@ -51,6 +51,11 @@ def postproc_kat():
 
 
 @pytest.fixture(scope="session")
+def postproc_chain_kat():
+    return load_golden("postproc_chain_kat.npz")
+
+
+@pytest.fixture(scope="session")
 def cuda_dev():
     import torch
     if not torch.cuda.is_available():

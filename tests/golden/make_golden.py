@@ -230,18 +230,69 @@ def gen_postproc(ref, ref_dir, out_dir):
                         valid=np.zeros((0, P)) if valid is None else valid, mask=mask)
 
 
+def gen_postproc_chain(ref, ref_dir, out_dir):
+    """The reference's whole post-sampling chain (:398-410, :1054-1064):
+    inverse_transform on a float32 tensor (torch.sigmoid), .numpy(),
+    MinMaxScaler.inverse_transform (float64 min_/scale_ applied in place to the
+    float32 array), check_param_bounds.  The scaler is fitted, as at :232-234,
+    on a synthetic (N, 29) physical-unit table that overshoots the
+    ParameterLimits by 1 % on each side so the bounds check rejects some rows."""
+    sys.path.insert(0, ref_dir)
+    import Generate_ERT_utils as ert_utils
+    from sklearn.preprocessing import MinMaxScaler
+    limits = np.asarray(ert_utils.ParameterLimits().plims, dtype=np.float64)
+    lo, hi = limits[:, 0], limits[:, 1]
+    table = lo + (hi - lo) * (synth_uniform((400, P), 71).astype(np.float64) * 1.02 - 0.01)
+    scaler = MinMaxScaler(feature_range=(0.0, 1.0))
+    scaler.fit(table)
+    R, B = 3, 16
+    u = synth_normal((R, B, P), 72) * np.float32(2.5)
+    u[0, 0, :3] = [30.0, -30.0, 0.0]        # saturated sigmoid -> data_max / data_min
+    out = np.zeros((R, B, P), np.float32)
+    mask = np.zeros((R, B), bool)
+    n_valid = np.zeros(R, np.int64)
+    import contextlib, io
+    for r in range(R):
+        x = ref["inverse_transform"](torch.from_numpy(u[r]), 0.0, 1.0).numpy()
+        x = scaler.inverse_transform(x)
+        assert x.dtype == np.float32
+        out[r] = x
+        mask[r] = [not any((v < mn) or (v > mx) for v, (mn, mx) in zip(row, limits)) for row in x]
+        with contextlib.redirect_stdout(io.StringIO()):
+            valid = ref["check_param_bounds"](x, limits)
+        n_valid[r] = 0 if valid is None else len(valid)
+        assert n_valid[r] == mask[r].sum()
+        if valid is not None:
+            assert np.array_equal(valid, x[mask[r]])
+    np.savez_compressed(os.path.join(out_dir, "postproc_chain_kat.npz"), limits=limits,
+                        data_min=scaler.data_min_, data_max=scaler.data_max_,
+                        min_=scaler.min_, scale_=scaler.scale_, u=u, out=out, mask=mask,
+                        n_valid=n_valid)
+
+
+GENERATORS = ("forward", "schedule", "sampler", "train", "postproc", "postproc_chain")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", nargs="*", choices=GENERATORS, default=list(GENERATORS))
     args = ap.parse_args()
     torch.set_num_threads(8)
     ref = load_reference(args.ref)
-    gen_forward(ref, args.out)
-    gen_schedule(ref, args.out)
-    gen_sampler(ref, args.out)
-    gen_train(ref, args.out)
-    gen_postproc(ref, args.ref, args.out)
+    if "forward" in args.only:
+        gen_forward(ref, args.out)
+    if "schedule" in args.only:
+        gen_schedule(ref, args.out)
+    if "sampler" in args.only:
+        gen_sampler(ref, args.out)
+    if "train" in args.only:
+        gen_train(ref, args.out)
+    if "postproc" in args.only:
+        gen_postproc(ref, args.ref, args.out)
+    if "postproc_chain" in args.only:
+        gen_postproc_chain(ref, args.ref, args.out)
     for f in sorted(os.listdir(args.out)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(args.out, f)))

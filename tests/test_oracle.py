@@ -124,3 +124,18 @@ def test_philox_known_answers():
     out = [int(v) for v in philox4x32_10(0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344,
                                          0xA4093822, 0x299F31D0)]
     assert out == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_postproc_chain_oracle(postproc_chain_kat):
+    """The numpy restatement of the post-sampling chain reproduces the
+    reference chain (torch sigmoid -> sklearn MinMaxScaler -> check_param_bounds)."""
+    k = postproc_chain_kat
+    R = k["u"].shape[0]
+    for r in range(R):
+        out, mask = RN.postprocess_chain(k["u"][r], k["min_"], k["scale_"], k["limits"])
+        # error in units of each feature's data range (x - min_ cancels near
+        # the range ends, so a 1-ulp sigmoid difference is not 1 ulp of out)
+        err = np.abs(out.astype(np.float64) - k["out"][r]) * k["scale_"]
+        assert err.max() <= 2.0 ** -22, err.max()
+        assert np.array_equal(mask, k["mask"][r])
+        assert mask.sum() == k["n_valid"][r]
