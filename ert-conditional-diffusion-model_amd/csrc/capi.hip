@@ -319,7 +319,7 @@ int ertd_sample_status(const void* ws, int B, int L, int num_steps, int* status,
 
 int ertd_philox_normal(uint64_t seed, uint32_t member_offset, int B, int P, int t, int tag,
                        float* out, void* stream) {
-  if (!out || B < 1 || P < 1 || P > PMAX || t < 0) return ERTD_EINVAL;
+  if (!out || B < 1 || P < 1 || (long long)B * P > (1LL << 31) || t < 0) return ERTD_EINVAL;
   return rc(launch_philox_normal(seed, member_offset, B, P, t, tag, out, (hipStream_t)stream));
 }
 

@@ -1,0 +1,97 @@
+// Build-defined conditional U-Net denoiser (SURVEY.md 8a', BASELINE north_star):
+// shared declarations of its kernels (unet_conv.hip, unet_ops.hip) and the
+// layer plan (unet_capi.hip).  PARITY UNPINNED vs the reference, which has
+// no U-Net; the specification is oracle/unet_torch.py.
+//
+// Layout in HBM: every activation is NCHW fp32, one buffer per layer output
+// (B, C, H, W), contiguous.  The sampled variable x stays (B, H*W) = (B, P),
+// the reference's (B, param_dim) contract.
+#pragma once
+#include "ertd_common.h"
+
+namespace ertd {
+namespace unet {
+
+constexpr int CK = 8;       // input channels per K-chunk of the implicit GEMM
+constexpr int NTHR = 256;   // conv workgroup: 4 waves, each a 64 (cout) x 64 (pixel) tile
+constexpr double GN_EPS = 1e-5;   // GroupNorm eps (oracle/unet_torch.py)
+
+// Activation applied to the conv input while it is staged into LDS.
+enum Act { ACT_NONE = 0, ACT_GN_SILU = 1, ACT_GN = 2 };
+// Spatial mode of a 3x3 conv: stride 1, stride 2 (Downsample), nearest x2
+// upsample of the source followed by the stride-1 conv (Upsample).
+enum Mode { MODE_S1 = 0, MODE_S2 = 1, MODE_UP = 2 };
+
+struct ConvArgs {
+  const float* srcA;     // (B, Ca, Hs, Ws)  channels [0, Ca)
+  const float* srcB;     // (B, Cb, Hs, Ws)  channels [Ca, Ca+Cb) (skip concat) or null
+  int Ca, Cb;
+  const float2* gn;      // (B, Cin) {scale, shift}: GroupNorm(x) = x*scale + shift (ACT_GN*)
+  const float* wpk;      // packed weights: [co_tile32][chunk][group][64 lanes][4]
+  const float* bias;     // (Cout)
+  const float* ebias;    // (B, eb_stride) per-sample per-channel add (offset applied) or null
+  int eb_stride;
+  const float* res;      // (B, Cout, Ho, Wo) residual add, or null
+  float* out;            // (B, Cout, Ho, Wo)
+  int Cin, Cout;
+  int Hs, Ws;            // source spatial size
+  int Ho, Wo;            // output spatial size
+  int IR, IP;            // staged LDS image rows / pitch (floats) per channel
+  int ir_magic;          // ceil(2^19 / IR): row / IR == (row * ir_magic) >> 19 for row < 4096
+  int nchunk;            // ceil(Cin / CK)
+};
+
+// groups of 4 k-steps per chunk in the packed weight stream
+__host__ __device__ constexpr int conv_groups(int ks) { return ks == 3 ? 9 : 1; }
+
+hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
+// packed floats of one conv's weights
+size_t conv_packed_floats(int cin, int cout, int ks);
+hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s);
+
+struct GnArgs {
+  const float* srcA; const float* srcB; int Ca, Cb;
+  int HW, groups;
+  const float* gamma; const float* beta;
+  float2* out;           // (B, Ca+Cb) {gamma*rstd, beta - mean*gamma*rstd}
+};
+hipError_t launch_gn_stats(const GnArgs& a, int B, hipStream_t s);
+
+// y[b][o] = bias[o] (+ add[b][o]) + sum_k Wt[k][o] * in(b, k)
+enum DenseIn { DIN_PLAIN = 0, DIN_SILU = 1, DIN_SINUSOID = 2 };
+struct DenseArgs {
+  const float* x; int x_stride;     // (B, K) input (DIN_PLAIN / DIN_SILU)
+  const int64_t* t;                 // DIN_SINUSOID: per-sample t (B), or null -> *t_dev
+  const int* t_dev;
+  const float* freq;                // DIN_SINUSOID: (K/2) frequencies
+  const float* wt;                  // (K, O) k-major
+  const float* bias;                // (O)
+  const float* add; int add_stride; // optional (B, O) add (row stride), or null
+  int add_bcast;                    // add row 0 for every b
+  float* y; int y_stride;
+  int K, O;
+};
+hipError_t launch_dense(int din, const DenseArgs& a, int B, hipStream_t s);
+hipError_t launch_transpose(const float* w, int O, int K, float* dst, int dst_ld, hipStream_t s);
+
+// single-head self-attention core: o[b][c][i] = sum_j softmax_j(q_i . k_j / sqrt(C)) v[c][j]
+// qkv (B, 3C, N) -> o (B, C, N)
+hipError_t launch_attention(const float* qkv, int C, int N, float* o, float* scratch, int B,
+                            hipStream_t s);
+
+struct UpdateArgs {
+  float* x;             // (B, P) in/out
+  const float* eps;     // (B, P)
+  const float* c1; const float* c2; const float* sigma;   // per-step tables (index t)
+  const float* noise;   // injected (num_steps, B, P) or null -> Philox
+  int num_steps;
+  const int* t_dev;
+  uint64_t seed; uint32_t member_offset;
+  int P;
+};
+hipError_t launch_unet_update(const UpdateArgs& a, int B, hipStream_t s);
+hipError_t launch_set_word(int* w, int v, hipStream_t s);
+hipError_t launch_dec_word(int* w, hipStream_t s);
+
+}  // namespace unet
+}  // namespace ertd

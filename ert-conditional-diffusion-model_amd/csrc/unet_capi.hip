@@ -1,0 +1,681 @@
+// C ABI of the build-defined conditional U-Net (include/ertdiff.h, "U-Net"
+// section): parameter enumeration, weight packing, forward and the T-step
+// sampler.  The layer walk below restates oracle/unet_torch.py (the
+// specification; PARITY UNPINNED vs the reference, which has no U-Net).
+//
+// Everything is enqueued on the caller's stream; the library allocates
+// nothing.  Workspace = one NCHW buffer per layer output (bump allocator over
+// the caller's ws), so a whole step can be captured into a hipGraph.
+#include <cstring>
+#include <new>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "unet.h"
+
+using namespace ertd;
+using namespace ertd::unet;
+
+namespace {
+
+struct Param {
+  std::string name;
+  std::vector<int> shape;
+  size_t numel() const {
+    size_t n = 1;
+    for (int d : shape) n *= (size_t)d;
+    return n;
+  }
+};
+
+bool cfg_ok(const ertd_unet_config* c) {
+  if (!c) return false;
+  if (c->image < 16 || c->image > 128 || (c->image & (c->image - 1))) return false;
+  if (c->n_levels < 1 || c->n_levels > 4 || c->num_res < 1 || c->num_res > 4) return false;
+  if (c->groups < 1 || c->ch < 8) return false;
+  if ((c->image >> (c->n_levels - 1)) < 16) return false;  // every level >= 16x16
+  for (int i = 0; i < c->n_levels; ++i) {
+    const int C = c->ch * c->ch_mult[i];
+    if (c->ch_mult[i] < 1 || C % c->groups) return false;
+  }
+  if (c->ch % c->groups) return false;
+  if (c->attn) {
+    const int Cm = c->ch * c->ch_mult[c->n_levels - 1];
+    const int r = c->image >> (c->n_levels - 1);
+    if (r * r != 256 || Cm % 256) return false;  // attention kernel: N = 256, C multiple of 256
+  }
+  return true;
+}
+
+int temb(const ertd_unet_config* c) { return 4 * c->ch; }
+
+std::vector<Param> enumerate(const ertd_unet_config* c) {
+  std::vector<Param> P;
+  auto lin = [&](const std::string& n, int i, int o) {
+    P.push_back({n + ".weight", {o, i}});
+    P.push_back({n + ".bias", {o}});
+  };
+  auto conv = [&](const std::string& n, int i, int o, int k) {
+    P.push_back({n + ".weight", {o, i, k, k}});
+    P.push_back({n + ".bias", {o}});
+  };
+  auto gn = [&](const std::string& n, int ch) {
+    P.push_back({n + ".weight", {ch}});
+    P.push_back({n + ".bias", {ch}});
+  };
+  auto res = [&](const std::string& n, int i, int o) {
+    gn(n + ".norm1", i);
+    conv(n + ".conv1", i, o, 3);
+    lin(n + ".emb", temb(c), o);
+    gn(n + ".norm2", o);
+    conv(n + ".conv2", o, o, 3);
+    if (i != o) conv(n + ".skip", i, o, 1);
+  };
+  P.push_back({"condition_encoder.0.weight", {C1, CIN, 3}});
+  P.push_back({"condition_encoder.0.bias", {C1}});
+  P.push_back({"condition_encoder.2.weight", {C2, C1, 3}});
+  P.push_back({"condition_encoder.2.bias", {C2}});
+  P.push_back({"condition_encoder.6.weight", {H, C2}});
+  P.push_back({"condition_encoder.6.bias", {H}});
+  lin("time_embed.0", c->ch, temb(c));
+  lin("time_embed.2", temb(c), temb(c));
+  lin("cond_proj", H, temb(c));
+  conv("conv_in", 1, c->ch, 3);
+  std::vector<int> chans{c->ch};
+  int ch = c->ch;
+  const int nl = c->n_levels;
+  for (int i = 0; i < nl; ++i) {
+    for (int r = 0; r < c->num_res; ++r) {
+      const int o = c->ch * c->ch_mult[i];
+      res("down." + std::to_string(i) + ".res." + std::to_string(r), ch, o);
+      ch = o;
+      chans.push_back(ch);
+    }
+    if (i != nl - 1) {
+      conv("down." + std::to_string(i) + ".downsample", ch, ch, 3);
+      chans.push_back(ch);
+    }
+  }
+  res("mid.res1", ch, ch);
+  if (c->attn) {
+    gn("mid.attn.norm", ch);
+    conv("mid.attn.qkv", ch, 3 * ch, 1);
+    conv("mid.attn.proj", ch, ch, 1);
+  }
+  res("mid.res2", ch, ch);
+  for (int i = nl - 1; i >= 0; --i) {
+    for (int r = 0; r <= c->num_res; ++r) {
+      const int o = c->ch * c->ch_mult[i];
+      const int skip = chans.back();
+      chans.pop_back();
+      res("up." + std::to_string(i) + ".res." + std::to_string(r), ch + skip, o);
+      ch = o;
+    }
+    if (i != 0) conv("up." + std::to_string(i) + ".upsample", ch, ch, 3);
+  }
+  gn("norm_out", ch);
+  conv("conv_out", ch, 1, 3);
+  return P;
+}
+
+bool ends_with(const std::string& s, const char* suf) {
+  const size_t n = strlen(suf);
+  return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
+}
+
+// ---- packed layout ------------------------------------------------------------
+// [encoder pack (ertd_pack_weights layout)] [zero head dummy] then, per
+// parameter in enumeration order: conv weights in conv fragment order, the
+// three embedding-path linears transposed (K, O), every ResBlock's emb linear
+// into one concatenated transposed matrix Wall^T (temb, sum C) + bias vector,
+// everything else verbatim.
+constexpr size_t DUMMY_FLOATS = (size_t)H * H + H + (size_t)H * (1 + 2 * H) + H + H + 1;
+
+struct Layout {
+  std::vector<Param> params;
+  std::map<std::string, size_t> off;  // packed offset per parameter name
+  std::map<std::string, int> eboff;   // ResBlock name -> column offset in Wall
+  size_t enc = 0, dummy = 0, wall = 0, ball = 0, total = 0;
+  int ebtotal = 0;
+};
+
+size_t a64(size_t n) { return (n + 63) / 64 * 64; }
+
+Layout layout(const ertd_unet_config* c) {
+  Layout L;
+  L.params = enumerate(c);
+  size_t o = 0;
+  L.enc = o;
+  o += a64(PACKED_FLOATS_ALL);
+  L.dummy = o;
+  o += a64(DUMMY_FLOATS);
+  for (const Param& p : L.params)
+    if (ends_with(p.name, ".emb.weight")) {
+      L.eboff[p.name.substr(0, p.name.size() - 11)] = L.ebtotal;
+      L.ebtotal += p.shape[0];
+    }
+  L.wall = o;
+  o += a64((size_t)temb(c) * L.ebtotal);
+  L.ball = o;
+  o += a64((size_t)L.ebtotal);
+  for (const Param& p : L.params) {
+    if (p.name.rfind("condition_encoder.", 0) == 0) continue;
+    if (ends_with(p.name, ".emb.weight") || ends_with(p.name, ".emb.bias")) continue;
+    L.off[p.name] = o;
+    if (p.shape.size() == 4) o += a64(conv_packed_floats(p.shape[1], p.shape[0], p.shape[2]));
+    else o += a64(p.numel());
+  }
+  L.total = o;
+  return L;
+}
+
+// ---- forward walk -----------------------------------------------------------------
+struct Walk {
+  const ertd_unet_config* c;
+  const Layout* L;
+  const float* pk;       // packed
+  char* ws;              // workspace base (null: size only)
+  size_t used = 0;
+  int B;
+  hipStream_t s;
+  bool dry;
+  hipError_t err = hipSuccess;
+
+  float* alloc(size_t floats) {
+    float* p = dry ? nullptr : (float*)(ws + used);
+    used += (floats * sizeof(float) + 255) / 256 * 256;
+    return p;
+  }
+  const float* P(const std::string& n) const { return pk + L->off.at(n); }
+  void chk(hipError_t e) {
+    if (err == hipSuccess && e != hipSuccess) err = e;
+  }
+
+  float2* gnbuf = nullptr;
+
+  void gn_stats(const float* A, int Ca, const float* Bs, int Cb, int HW, const std::string& n) {
+    if (dry) return;
+    GnArgs g{A, Bs, Ca, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"), gnbuf};
+    chk(launch_gn_stats(g, B, s));
+  }
+
+  // conv over input (A: Ca ch, Bs: Cb ch) at source size Hs x Ws
+  float* conv(const std::string& n, int ks, int mode, int act, const float* A, int Ca,
+              const float* Bs, int Cb, int Hs, int Ws, const float* ebias, const float* res,
+              float* out = nullptr) {
+    const Param* wp = nullptr;
+    for (const Param& p : L->params)
+      if (p.name == n + ".weight") { wp = &p; break; }
+    const int Cout = wp->shape[0], Cin = wp->shape[1];
+    int Ho = Hs, Wo = Ws;
+    if (mode == MODE_S2) { Ho = Hs / 2; Wo = Ws / 2; }
+    if (mode == MODE_UP) { Ho = Hs * 2; Wo = Ws * 2; }
+    if (!out) out = alloc((size_t)B * Cout * Ho * Wo);
+    if (dry) return out;
+    const int wco = Cout >= 128 ? 2 : 1;
+    const int bm = 64 * (4 / wco);
+    const int R = bm / Wo;
+    int IR;
+    if (ks == 1) IR = R;
+    else if (mode == MODE_S2) IR = 2 * R + 1;
+    else IR = R + 2;
+    const int Wst = mode == MODE_UP ? 2 * Ws : Ws;
+    const int IP = Wst + 2;
+    const int rstep = NTHR / Wst;
+    const int nit = (CK * IR + rstep - 1) / rstep;
+    if (bm % Wo || (Ho * Wo) % bm || Wst > NTHR || nit > (mode == MODE_S2 ? 36 : 20) ||
+        CK * IR >= 4096 || Cin != Ca + Cb) {
+      chk(hipErrorInvalidValue);
+      return out;
+    }
+    ConvArgs a{};
+    a.srcA = A; a.srcB = Bs; a.Ca = Ca; a.Cb = Cb;
+    a.gn = act != ACT_NONE ? gnbuf : nullptr;
+    a.wpk = P(n + ".weight");
+    a.bias = P(n + ".bias");
+    a.ebias = ebias; a.eb_stride = L->ebtotal;
+    a.res = res; a.out = out;
+    a.Cin = Cin; a.Cout = Cout;
+    a.Hs = Hs; a.Ws = Ws; a.Ho = Ho; a.Wo = Wo;
+    a.IR = IR; a.IP = IP;
+    a.ir_magic = (int)(((1u << 19) + IR - 1) / IR);
+    a.nchunk = (Cin + CK - 1) / CK;
+    chk(launch_conv(ks, mode, act, a, B, s));
+    return out;
+  }
+
+  float* resblock(const std::string& n, const float* A, int Ca, const float* Bs, int Cb, int Hh,
+                  int Ww, int cout, const float* ebias_all) {
+    const int HW = Hh * Ww;
+    const float* eb = ebias_all ? ebias_all + L->eboff.at(n) : nullptr;
+    gn_stats(A, Ca, Bs, Cb, HW, n + ".norm1");
+    float* h1 = conv(n + ".conv1", 3, MODE_S1, ACT_GN_SILU, A, Ca, Bs, Cb, Hh, Ww, eb, nullptr);
+    const float* resid = A;
+    if (Ca + Cb != cout) resid = conv(n + ".skip", 1, MODE_S1, ACT_NONE, A, Ca, Bs, Cb, Hh, Ww,
+                                      nullptr, nullptr);
+    gn_stats(h1, cout, nullptr, 0, HW, n + ".norm2");
+    return conv(n + ".conv2", 3, MODE_S1, ACT_GN_SILU, h1, cout, nullptr, 0, Hh, Ww, nullptr, resid);
+  }
+
+  // x (B, image^2) -> eps (B, image^2); emb_act source = ebias_all (B, ebtotal)
+  void unet(const float* x, const float* ebias_all, float* eps) {
+    const int nl = c->n_levels;
+    int Hh = c->image;
+    std::vector<std::pair<const float*, int>> hs;
+    const float* h = conv("conv_in", 3, MODE_S1, ACT_NONE, x, 1, nullptr, 0, Hh, Hh, nullptr,
+                          nullptr);
+    int ch = c->ch;
+    hs.push_back({h, ch});
+    for (int i = 0; i < nl; ++i) {
+      for (int r = 0; r < c->num_res; ++r) {
+        const int o = c->ch * c->ch_mult[i];
+        h = resblock("down." + std::to_string(i) + ".res." + std::to_string(r), h, ch, nullptr, 0,
+                     Hh, Hh, o, ebias_all);
+        ch = o;
+        hs.push_back({h, ch});
+      }
+      if (i != nl - 1) {
+        h = conv("down." + std::to_string(i) + ".downsample", 3, MODE_S2, ACT_NONE, h, ch, nullptr,
+                 0, Hh, Hh, nullptr, nullptr);
+        Hh /= 2;
+        hs.push_back({h, ch});
+      }
+    }
+    h = resblock("mid.res1", h, ch, nullptr, 0, Hh, Hh, ch, ebias_all);
+    if (c->attn) {
+      gn_stats(h, ch, nullptr, 0, Hh * Hh, "mid.attn.norm");
+      float* qkv = conv("mid.attn.qkv", 1, MODE_S1, ACT_GN, h, ch, nullptr, 0, Hh, Hh, nullptr,
+                        nullptr);
+      float* o = alloc((size_t)B * ch * Hh * Hh);
+      if (!dry) chk(launch_attention(qkv, ch, Hh * Hh, o, nullptr, B, s));
+      h = conv("mid.attn.proj", 1, MODE_S1, ACT_NONE, o, ch, nullptr, 0, Hh, Hh, nullptr, h);
+    }
+    h = resblock("mid.res2", h, ch, nullptr, 0, Hh, Hh, ch, ebias_all);
+    for (int i = nl - 1; i >= 0; --i) {
+      for (int r = 0; r <= c->num_res; ++r) {
+        const int o = c->ch * c->ch_mult[i];
+        const auto sk = hs.back();
+        hs.pop_back();
+        h = resblock("up." + std::to_string(i) + ".res." + std::to_string(r), h, ch, sk.first,
+                     sk.second, Hh, Hh, o, ebias_all);
+        ch = o;
+      }
+      if (i != 0) {
+        h = conv("up." + std::to_string(i) + ".upsample", 3, MODE_UP, ACT_NONE, h, ch, nullptr, 0,
+                 Hh, Hh, nullptr, nullptr);
+        Hh *= 2;
+      }
+    }
+    gn_stats(h, ch, nullptr, 0, Hh * Hh, "norm_out");
+    conv("conv_out", 3, MODE_S1, ACT_GN_SILU, h, ch, nullptr, 0, Hh, Hh, nullptr, nullptr, eps);
+  }
+
+  int max_cin() const {
+    int m = 1;
+    for (const Param& p : L->params)
+      if (p.shape.size() == 4 && p.shape[1] > m) m = p.shape[1];
+    return m;
+  }
+
+  void dense(int din, const float* xin, int xs, const int64_t* t, const int* tdev,
+             const float* freq, const std::string& n, int K, int O, const float* add, int adds,
+             float* y, int ys, const float* wt = nullptr, const float* bias = nullptr) {
+    if (dry) return;
+    DenseArgs d{};
+    d.x = xin; d.x_stride = xs; d.t = t; d.t_dev = tdev; d.freq = freq;
+    d.wt = wt ? wt : P(n + ".weight");
+    d.bias = bias ? bias : P(n + ".bias");
+    d.add = add; d.add_stride = adds; d.add_bcast = 0;
+    d.y = y; d.y_stride = ys; d.K = K; d.O = O;
+    chk(launch_dense(din, d, B, s));
+  }
+};
+
+// Persistent per-call buffers at the head of the workspace.
+struct Fixed {
+  float* cond_emb;   // (B, 128)
+  float* cproj;      // (B, temb)
+  float* e1;         // (B, temb)
+  float* emb;        // (B, temb)
+  float* ebias;      // (B, ebtotal)
+  float* eps;        // (B, P)
+  float* freq;       // (ch/2)
+  float* partial;    // encoder strips (B, S, 64)
+  float* Uscr;       // (B, 128)
+  int* tdev;         // step counter word
+};
+
+Fixed fixed(Walk& w, int L) {
+  Fixed f{};
+  const int B = w.B, tb = temb(w.c);
+  const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
+  f.cond_emb = w.alloc((size_t)B * H);
+  f.cproj = w.alloc((size_t)B * tb);
+  f.e1 = w.alloc((size_t)B * tb);
+  f.emb = w.alloc((size_t)B * tb);
+  f.ebias = w.alloc((size_t)B * w.L->ebtotal);
+  f.eps = w.alloc((size_t)B * w.c->image * w.c->image);
+  f.freq = w.alloc((size_t)w.c->ch / 2);
+  f.partial = w.alloc((size_t)B * S * C2);
+  f.Uscr = w.alloc((size_t)B * H);
+  f.tdev = (int*)w.alloc(64);
+  w.gnbuf = (float2*)w.alloc((size_t)B * w.max_cin() * 2);
+  return f;
+}
+
+ertd_weights enc_weights(const Layout& L, const float* pk, const float* const* params) {
+  ertd_weights e{};
+  e.enc0_w = params[0]; e.enc0_b = params[1];
+  e.enc2_w = params[2]; e.enc2_b = params[3];
+  e.enc6_w = params[4]; e.enc6_b = params[5];
+  const float* d = pk + L.dummy;
+  e.time_w = d; d += H * H;
+  e.time_b = d; d += H;
+  e.mlp0_w = d; d += (size_t)H * (1 + 2 * H);
+  e.mlp0_b = d; d += H;
+  e.mlp2_w = d; d += H;
+  e.mlp2_b = d;
+  e.param_dim = 1;
+  e.hidden_dim = H;
+  return e;
+}
+
+// encoder weights as seen by the strip/pool kernels after packing: the biases
+// and enc6 are read from the packed copies (no params pointer needed at run time)
+ertd_weights enc_weights_packed(const Layout& L, const float* pk) {
+  const float* const* none = nullptr;
+  (void)none;
+  ertd_weights e{};
+  const float* d = pk + L.dummy;
+  e.time_w = d; d += H * H;
+  e.time_b = d; d += H;
+  e.mlp0_w = d; d += (size_t)H * (1 + 2 * H);
+  e.mlp0_b = d; d += H;
+  e.mlp2_w = d; d += H;
+  e.mlp2_b = d;
+  e.enc0_w = pk + L.off.at("enc.0.weight");
+  e.enc0_b = pk + L.off.at("enc.0.bias");
+  e.enc2_w = pk + L.off.at("enc.2.weight");
+  e.enc2_b = pk + L.off.at("enc.2.bias");
+  e.enc6_w = pk + L.off.at("enc.6.weight");
+  e.enc6_b = pk + L.off.at("enc.6.bias");
+  e.param_dim = 1;
+  e.hidden_dim = H;
+  return e;
+}
+
+Layout layout_full(const ertd_unet_config* c) {
+  Layout L = layout(c);
+  // verbatim copies of the encoder parameters (the encoder kernels read its
+  // biases and enc6 directly), appended at the end
+  const char* names[6] = {"enc.0.weight", "enc.0.bias", "enc.2.weight",
+                          "enc.2.bias", "enc.6.weight", "enc.6.bias"};
+  for (int i = 0; i < 6; ++i) {
+    L.off[names[i]] = L.total;
+    L.total += a64(L.params[i].numel());
+  }
+  return L;
+}
+
+// cond (B,14,Lc) -> cond_emb -> cproj; once per forward / sampler call
+int prologue(Walk& w, const Fixed& f, const float* cond, long long cstride, int Lc) {
+  const float* pk = w.pk;
+  const ertd_weights e = enc_weights_packed(*w.L, pk);
+  const int L2 = conv_len(conv_len(Lc)), S = n_strips(L2);
+  w.chk(launch_encoder_strips(pk + w.L->enc, e.enc0_b, e.enc2_b, cond, cstride, w.B, Lc,
+                              ERTD_PREC_FP32, f.partial, w.s));
+  w.chk(launch_hoist_prep(e, pk + w.L->enc, f.partial, S, L2, w.B, f.Uscr, f.cond_emb, w.s));
+  w.dense(DIN_PLAIN, f.cond_emb, H, nullptr, nullptr, nullptr, "cond_proj", H, temb(w.c), nullptr,
+          0, f.cproj, temb(w.c));
+  // sinusoid frequencies exp(-i*ln(1e4)/(half-1)) (float32, as the reference's
+  // get_timestep_embedding) are packed on the host side into "freq"
+  return w.err == hipSuccess ? ERTD_OK : (int)w.err;
+}
+
+// t (per-sample) or *tdev -> emb -> all ResBlock emb biases
+void embed(Walk& w, const Fixed& f, const int64_t* t) {
+  const int tb = temb(w.c);
+  w.dense(DIN_SINUSOID, nullptr, 0, t, f.tdev, w.pk + w.L->off.at("freq"), "time_embed.0", w.c->ch,
+          tb, nullptr, 0, f.e1, tb);
+  w.dense(DIN_SILU, f.e1, tb, nullptr, nullptr, nullptr, "time_embed.2", tb, tb, f.cproj, tb, f.emb,
+          tb);
+  w.dense(DIN_SILU, f.emb, tb, nullptr, nullptr, nullptr, "", tb, w.L->ebtotal, nullptr, 0, f.ebias,
+          w.L->ebtotal, w.pk + w.L->wall, w.pk + w.L->ball);
+}
+
+Layout layout_with_freq(const ertd_unet_config* c) {
+  Layout L = layout_full(c);
+  L.off["freq"] = L.total;
+  L.total += a64((size_t)c->ch / 2);
+  return L;
+}
+
+size_t ws_bytes_for(const ertd_unet_config* c, const Layout& L, int B, int Lc) {
+  Walk w{c, &L, nullptr, nullptr, 0, B, nullptr, true};
+  fixed(w, Lc);
+  w.unet(nullptr, nullptr, nullptr);
+  return w.used;
+}
+
+inline int rcode(hipError_t e) { return e == hipSuccess ? ERTD_OK : (int)e; }
+
+// One sampler call: head = encoder + cond_proj + t := t_first; step = one
+// reverse step (embedding, U-Net, update, t := t - 1) reading t from the
+// workspace word, so the same step can be replayed as a graph.
+struct SampleCall {
+  const ertd_unet_config* c;
+  const float* packed; const float* cond; long long cond_stride; int L; int B;
+  int num_steps; int t_first; int n_run;
+  const float* c1; const float* c2; const float* sigma; const float* noise;
+  uint64_t seed; uint32_t member_offset; float* x; void* ws; size_t ws_bytes;
+
+  int check() const {
+    if (!cfg_ok(c) || !packed || !cond || !c1 || !c2 || !sigma || !x || !ws || B < 1 || L < 1 ||
+        num_steps < 1 || t_first < 0 || t_first >= num_steps || n_run < 0 || n_run > t_first + 1)
+      return ERTD_EINVAL;
+    const Layout Lo = layout_with_freq(c);
+    if (ws_bytes_for(c, Lo, B, L) > ws_bytes) return ERTD_ENOSPC;
+    return ERTD_OK;
+  }
+  int head(hipStream_t s) const {
+    const Layout Lo = layout_with_freq(c);
+    Walk w{c, &Lo, packed, (char*)ws, 0, B, s, false};
+    const Fixed f = fixed(w, L);
+    const int r = prologue(w, f, cond, cond_stride, L);
+    if (r != ERTD_OK) return r;
+    w.chk(launch_set_word(f.tdev, t_first, s));
+    return rcode(w.err);
+  }
+  int step(hipStream_t s) const {
+    const Layout Lo = layout_with_freq(c);
+    Walk w{c, &Lo, packed, (char*)ws, 0, B, s, false};
+    const Fixed f = fixed(w, L);
+    const int P = c->image * c->image;
+    embed(w, f, nullptr);
+    w.unet(x, f.ebias, f.eps);
+    UpdateArgs u{x, f.eps, c1, c2, sigma, noise, num_steps, f.tdev, seed, member_offset, P};
+    w.chk(launch_unet_update(u, B, s));
+    w.chk(launch_dec_word(f.tdev, s));
+    return rcode(w.err);
+  }
+};
+
+}  // namespace
+
+struct ertd_unet_plan {
+  ertd_unet_config cfg{};
+  SampleCall call{};
+  hipStream_t stream = nullptr;
+  hipGraph_t g_head = nullptr, g_step = nullptr;
+  hipGraphExec_t x_head = nullptr, x_step = nullptr;
+};
+
+extern "C" {
+
+int ertd_unet_n_params(const ertd_unet_config* c) {
+  if (!cfg_ok(c)) return ERTD_EINVAL;
+  return (int)enumerate(c).size();
+}
+
+int ertd_unet_param_info(const ertd_unet_config* c, int idx, char* name, int name_len,
+                         int64_t* shape, int* ndim) {
+  if (!cfg_ok(c) || !name || name_len < 2 || !shape || !ndim) return ERTD_EINVAL;
+  const std::vector<Param> P = enumerate(c);
+  if (idx < 0 || idx >= (int)P.size()) return ERTD_EINVAL;
+  const Param& p = P[idx];
+  strncpy(name, p.name.c_str(), (size_t)name_len - 1);
+  name[name_len - 1] = 0;
+  *ndim = (int)p.shape.size();
+  for (int i = 0; i < *ndim; ++i) shape[i] = p.shape[i];
+  return ERTD_OK;
+}
+
+size_t ertd_unet_packed_floats(const ertd_unet_config* c) {
+  if (!cfg_ok(c)) return 0;
+  return layout_with_freq(c).total;
+}
+
+size_t ertd_unet_workspace_bytes(const ertd_unet_config* c, int B, int L) {
+  if (!cfg_ok(c) || B < 1 || L < 1) return 0;
+  const Layout Lo = layout_with_freq(c);
+  return ws_bytes_for(c, Lo, B, L);
+}
+
+int ertd_unet_pack(const ertd_unet_config* c, const float* const* params, const float* freq,
+                   float* packed, void* stream) {
+  if (!cfg_ok(c) || !params || !freq || !packed) return ERTD_EINVAL;
+  const Layout L = layout_with_freq(c);
+  for (size_t i = 0; i < L.params.size(); ++i)
+    if (!params[i]) return ERTD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(packed + L.dummy, 0, DUMMY_FLOATS * sizeof(float), s);
+  if (e != hipSuccess) return (int)e;
+  const ertd_weights ew = enc_weights(L, packed, params);
+  if ((e = launch_pack(ew, packed + L.enc, s)) != hipSuccess) return (int)e;
+  const int tb = temb(c);
+  for (size_t i = 0; i < L.params.size(); ++i) {
+    const Param& p = L.params[i];
+    const float* src = params[i];
+    if (p.name.rfind("condition_encoder.", 0) == 0) {
+      static const char* map[6] = {"enc.0.weight", "enc.0.bias", "enc.2.weight",
+                                   "enc.2.bias", "enc.6.weight", "enc.6.bias"};
+      e = hipMemcpyAsync(packed + L.off.at(map[i]), src, p.numel() * sizeof(float),
+                         hipMemcpyDeviceToDevice, s);
+    } else if (ends_with(p.name, ".emb.weight")) {
+      const int col = L.eboff.at(p.name.substr(0, p.name.size() - 11));
+      e = launch_transpose(src, p.shape[0], p.shape[1], packed + L.wall + col, L.ebtotal, s);
+    } else if (ends_with(p.name, ".emb.bias")) {
+      const int col = L.eboff.at(p.name.substr(0, p.name.size() - 9));
+      e = hipMemcpyAsync(packed + L.ball + col, src, p.numel() * sizeof(float),
+                         hipMemcpyDeviceToDevice, s);
+    } else if (p.shape.size() == 4) {
+      e = launch_pack_conv(src, p.shape[1], p.shape[0], p.shape[2], packed + L.off.at(p.name), s);
+    } else if (p.shape.size() == 2) {
+      e = launch_transpose(src, p.shape[0], p.shape[1], packed + L.off.at(p.name), p.shape[0], s);
+    } else {
+      e = hipMemcpyAsync(packed + L.off.at(p.name), src, p.numel() * sizeof(float),
+                         hipMemcpyDeviceToDevice, s);
+    }
+    if (e != hipSuccess) return (int)e;
+  }
+  (void)tb;
+  e = hipMemcpyAsync(packed + L.off.at("freq"), freq, (size_t)c->ch / 2 * sizeof(float),
+                     hipMemcpyDeviceToDevice, s);
+  return rcode(e);
+}
+
+int ertd_unet_forward(const ertd_unet_config* c, const float* packed, const float* x,
+                      const int64_t* t, const float* cond, long long cond_stride, int L, int B,
+                      float* out, float* cond_emb_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!cfg_ok(c) || !packed || !x || !t || !cond || !out || !ws || B < 1 || L < 1)
+    return ERTD_EINVAL;
+  const Layout Lo = layout_with_freq(c);
+  if (ws_bytes_for(c, Lo, B, L) > ws_bytes) return ERTD_ENOSPC;
+  Walk w{c, &Lo, packed, (char*)ws, 0, B, (hipStream_t)stream, false};
+  const Fixed f = fixed(w, L);
+  int r = prologue(w, f, cond, cond_stride, L);
+  if (r != ERTD_OK) return r;
+  embed(w, f, t);
+  w.unet(x, f.ebias, out);
+  if (cond_emb_out && w.err == hipSuccess)
+    w.chk(hipMemcpyAsync(cond_emb_out, f.cond_emb, (size_t)B * H * sizeof(float),
+                         hipMemcpyDeviceToDevice, w.s));
+  return rcode(w.err);
+}
+
+int ertd_unet_sample(const ertd_unet_config* c, const float* packed, const float* cond,
+                     long long cond_stride, int L, int B, int num_steps, int t_first, int n_run,
+                     const float* c1, const float* c2, const float* sigma, const float* noise,
+                     uint64_t seed, uint32_t member_offset, float* x_inout, void* ws,
+                     size_t ws_bytes, void* stream) {
+  SampleCall sc{c, packed, cond, cond_stride, L, B, num_steps, t_first, n_run, c1, c2, sigma,
+                noise, seed, member_offset, x_inout, ws, ws_bytes};
+  int r = sc.check();
+  if (r != ERTD_OK) return r;
+  hipStream_t s = (hipStream_t)stream;
+  if ((r = sc.head(s)) != ERTD_OK) return r;
+  for (int i = 0; i < n_run; ++i)
+    if ((r = sc.step(s)) != ERTD_OK) return r;
+  return ERTD_OK;
+}
+
+int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed, const float* cond,
+                                 long long cond_stride, int L, int B, int num_steps, int t_first,
+                                 int n_run, const float* c1, const float* c2, const float* sigma,
+                                 const float* noise, uint64_t seed, uint32_t member_offset,
+                                 float* x_inout, void* ws, size_t ws_bytes,
+                                 ertd_unet_plan** plan) {
+  if (!plan) return ERTD_EINVAL;
+  *plan = nullptr;
+  ertd_unet_plan* p = new (std::nothrow) ertd_unet_plan();
+  if (!p) return ERTD_EINVAL;
+  p->call = SampleCall{c, packed, cond, cond_stride, L, B, num_steps, t_first, n_run, c1, c2,
+                       sigma, noise, seed, member_offset, x_inout, ws, ws_bytes};
+  p->cfg = *c;
+  p->call.c = &p->cfg;
+  int r = p->call.check();
+  if (r != ERTD_OK) {
+    delete p;
+    return r;
+  }
+  hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+  for (int k = 0; e == hipSuccess && k < 2; ++k) {
+    e = hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) break;
+    r = k == 0 ? p->call.head(p->stream) : p->call.step(p->stream);
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(p->stream, &g);
+    (k == 0 ? p->g_head : p->g_step) = g;
+    if (r != ERTD_OK) break;
+    if (e == hipSuccess)
+      e = hipGraphInstantiate(k == 0 ? &p->x_head : &p->x_step, g, nullptr, nullptr, 0);
+  }
+  if (r != ERTD_OK || e != hipSuccess) {
+    ertd_unet_plan_destroy(p);
+    return r != ERTD_OK ? r : (int)e;
+  }
+  *plan = p;
+  return ERTD_OK;
+}
+
+int ertd_unet_plan_launch(ertd_unet_plan* p, void* stream) {
+  if (!p || !p->x_head || !p->x_step) return ERTD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipGraphLaunch(p->x_head, s);
+  for (int i = 0; e == hipSuccess && i < p->call.n_run; ++i) e = hipGraphLaunch(p->x_step, s);
+  return rcode(e);
+}
+
+int ertd_unet_plan_destroy(ertd_unet_plan* p) {
+  if (!p) return ERTD_OK;
+  if (p->x_head) (void)hipGraphExecDestroy(p->x_head);
+  if (p->x_step) (void)hipGraphExecDestroy(p->x_step);
+  if (p->g_head) (void)hipGraphDestroy(p->g_head);
+  if (p->g_step) (void)hipGraphDestroy(p->g_step);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+  return ERTD_OK;
+}
+
+}  // extern "C"

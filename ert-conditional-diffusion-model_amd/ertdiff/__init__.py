@@ -14,6 +14,7 @@ from .schedule import get_diffusion_schedule, step_tables, timestep_frequencies
 from .train import DiffusionForwardFn, train_step, validation_loss
 from .ensemble import member_range, sample_ensemble
 from .postproc import compact, postprocess, sample_realisations
+from .unet import ConditionalUNet, UNetSamplerPlan, sample_unet
 
 __all__ = [
     "ConditionalDiffusionModel", "get_timestep_embedding", "get_diffusion_schedule", "q_sample",
@@ -22,4 +23,5 @@ __all__ = [
     "DiffusionDataset", "check_param_bounds", "bounds_mask", "load_best_model",
     "save_checkpoint", "STATE_KEYS", "train_step", "validation_loss", "DiffusionForwardFn",
     "sample_ensemble", "member_range", "postprocess", "sample_realisations", "compact",
+    "ConditionalUNet", "UNetSamplerPlan", "sample_unet",
 ]

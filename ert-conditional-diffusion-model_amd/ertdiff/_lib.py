@@ -72,6 +72,20 @@ SIGNATURES = {
                              _F, _F, _F, _VP, _VP, _SZ, _VP]),
     "ertd_postprocess": (_I, [_VP, ctypes.c_longlong, _I, ctypes.c_double, ctypes.c_double, _VP,
                               _VP, _VP, _VP, _VP, _VP]),
+    "ertd_unet_n_params": (_I, [_VP]),
+    "ertd_unet_param_info": (_I, [_VP, _I, ctypes.c_char_p, _I, _VP, ctypes.POINTER(_I)]),
+    "ertd_unet_packed_floats": (_SZ, [_VP]),
+    "ertd_unet_pack": (_I, [_VP, _VP, _VP, _VP, _VP]),
+    "ertd_unet_workspace_bytes": (_SZ, [_VP, _I, _I]),
+    "ertd_unet_forward": (_I, [_VP, _VP, _VP, _VP, _VP, ctypes.c_longlong, _I, _I, _VP, _VP, _VP,
+                               _SZ, _VP]),
+    "ertd_unet_sample": (_I, [_VP, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I, _VP, _VP, _VP,
+                              _VP, _U64, _U32, _VP, _VP, _SZ, _VP]),
+    "ertd_unet_sample_plan_create": (_I, [_VP, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I,
+                                          _VP, _VP, _VP, _VP, _U64, _U32, _VP, _VP, _SZ,
+                                          ctypes.POINTER(_VP)]),
+    "ertd_unet_plan_launch": (_I, [_VP, _VP]),
+    "ertd_unet_plan_destroy": (_I, [_VP]),
     "ertd_plan_launch": (_I, [_VP, _VP]),
     "ertd_plan_destroy": (_I, [_VP]),
 }

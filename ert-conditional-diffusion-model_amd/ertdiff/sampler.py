@@ -143,6 +143,12 @@ def sample_model(model, condition, T, betas, alphas, alpha_bar, param_dim, devic
     shared_condition + n_members: one (1,14,L) / (14,L) condition shared by
     n_members ensemble members (read in place, never replicated).
     """
+    from .unet import ConditionalUNet, sample_unet
+    if isinstance(model, ConditionalUNet):
+        return sample_unet(model, condition, T, betas, alphas, alpha_bar, param_dim, device,
+                           num_steps, temperature, noise=noise, seed=seed,
+                           member_offset=member_offset, shared_condition=shared_condition,
+                           n_members=n_members)
     if mode not in _MODES:
         raise ValueError(f"mode must be one of {list(_MODES)}")
     dev = _lib.require_device(condition)

@@ -1,0 +1,285 @@
+"""Build-defined conditional U-Net denoiser (SURVEY.md 8a', BASELINE north_star).
+
+PARITY UNPINNED vs the reference: ERT_Conditional_Diffusion.py has no U-Net
+(SURVEY.md 0.3).  The specification is oracle/unet_torch.py; the kernels are
+in csrc/unet_conv.hip (3x3 / 1x1 convs as implicit GEMMs on fp32 MFMA, with
+GroupNorm+SiLU fused into the input staging and bias / embedding / residual
+adds fused into the epilogue), csrc/unet_ops.hip (GroupNorm statistics,
+embedding-path dense layers, mid-block attention, DDPM update) and
+csrc/unet_capi.hip (the layer walk and the sampler step graph).
+
+The call surface is the reference's: ``ConditionalUNet`` is an ``nn.Module``
+whose forward is ``model(x (B, image^2), t (B,), condition (B,14,L))`` like
+ConditionalDiffusionModel.forward (:155-164), so ``x`` keeps the (B,
+param_dim) contract of sample_model (:107); ``sample_model`` dispatches to
+``sample_unet`` when handed a ConditionalUNet.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .schedule import step_tables, timestep_frequencies
+
+
+class ErtdUnetConfig(ctypes.Structure):
+    _fields_ = [("image", ctypes.c_int), ("ch", ctypes.c_int), ("n_levels", ctypes.c_int),
+                ("ch_mult", ctypes.c_int * 4), ("num_res", ctypes.c_int), ("attn", ctypes.c_int),
+                ("groups", ctypes.c_int)]
+
+
+# SURVEY.md 8a' table (U4 = U2's network on the 1024-member ensemble)
+CONFIGS: Dict[str, dict] = {
+    "U1": dict(image=32, ch=32, ch_mult=(1, 2), num_res=2, attn=False),
+    "U2": dict(image=64, ch=64, ch_mult=(1, 2, 4), num_res=2, attn=False),
+    "U3": dict(image=64, ch=64, ch_mult=(1, 2, 4), num_res=2, attn=True),
+    "U5": dict(image=128, ch=128, ch_mult=(1, 1, 2, 2), num_res=2, attn=True),
+}
+
+
+def make_config(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, attn=False,
+                groups=32) -> ErtdUnetConfig:
+    m = list(ch_mult) + [0] * (4 - len(ch_mult))
+    return ErtdUnetConfig(int(image), int(ch), len(ch_mult), (ctypes.c_int * 4)(*m), int(num_res),
+                          int(bool(attn)), int(groups))
+
+
+def param_layout(cfg: ErtdUnetConfig) -> List[Tuple[str, Tuple[int, ...]]]:
+    """(name, shape) of every parameter, in state_dict order, from the library."""
+    lib = _lib.lib()
+    n = lib.ertd_unet_n_params(ctypes.byref(cfg))
+    if n < 0:
+        raise RuntimeError("ertdiff: unsupported U-Net configuration")
+    out = []
+    name = ctypes.create_string_buffer(128)
+    shape = (ctypes.c_int64 * 4)()
+    nd = ctypes.c_int()
+    for i in range(n):
+        _lib.check(lib.ertd_unet_param_info(ctypes.byref(cfg), i, name, 128, shape,
+                                            ctypes.byref(nd)), "unet_param_info")
+        out.append((name.value.decode(), tuple(int(shape[j]) for j in range(nd.value))))
+    return out
+
+
+class ConditionalUNet(nn.Module):
+    """eps(x, t, condition) with a 2-D U-Net over x viewed as (B,1,image,image).
+
+    Parameters are registered as nested modules so the state_dict keys and
+    order are those of oracle/unet_torch.layer_shapes (and of the library's
+    enumeration).  Init: uniform(+-1/sqrt(fan_in)) for conv/linear weights and
+    biases (PyTorch's default bound), GroupNorm weight 1 / bias 0.
+    """
+
+    def __init__(self, image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, attn=False,
+                 groups=32, seed: Optional[int] = None):
+        super().__init__()
+        self.spec = dict(image=image, ch=ch, ch_mult=tuple(ch_mult), num_res=num_res, attn=attn,
+                         groups=groups)
+        self.cfg = make_config(image, ch, ch_mult, num_res, attn, groups)
+        self.image = image
+        self.param_dim = image * image
+        self.layout = param_layout(self.cfg)
+        g = torch.Generator().manual_seed(seed) if seed is not None else None
+        shapes = dict(self.layout)
+        for name, shape in self.layout:
+            parts = name.split(".")
+            mod = self
+            for p in parts[:-1]:
+                if not hasattr(mod, p) or not isinstance(getattr(mod, p), nn.Module):
+                    mod.add_module(p, nn.Module())
+                mod = getattr(mod, p)
+            if ".norm" in name or name.startswith("norm_out"):
+                val = torch.ones(shape) if parts[-1] == "weight" else torch.zeros(shape)
+            else:
+                wshape = shape if parts[-1] == "weight" else shapes[name[:-4] + "weight"]
+                fan_in = int(math.prod(wshape[1:]))
+                bound = 1.0 / math.sqrt(fan_in)
+                val = (torch.rand(shape, generator=g) * 2 - 1) * bound
+            mod.register_parameter(parts[-1], nn.Parameter(val))
+        keys = list(self.state_dict().keys())
+        if keys != [n for n, _ in self.layout]:
+            raise RuntimeError("ertdiff: U-Net state_dict order differs from the library's")
+        self._packed: Optional[torch.Tensor] = None
+        self._packed_key = None
+        self._ws: Dict = {}
+
+    @classmethod
+    def from_config(cls, name: str, seed: Optional[int] = None) -> "ConditionalUNet":
+        return cls(**CONFIGS[name], seed=seed)
+
+    def _params(self) -> List[torch.Tensor]:
+        sd = dict(self.named_parameters())
+        return [sd[n] for n, _ in self.layout]
+
+    def packed_weights(self, dev: torch.device) -> torch.Tensor:
+        ps = self._params()
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        if self._packed is None or self._packed_key != key or self._packed.device != dev:
+            for (n, _), p in zip(self.layout, ps):
+                if p.dtype != torch.float32 or not p.is_contiguous() or p.device != dev:
+                    raise RuntimeError(f"ertdiff: parameter {n} must be contiguous float32 on {dev}")
+            lib = _lib.lib()
+            nf = lib.ertd_unet_packed_floats(ctypes.byref(self.cfg))
+            if self._packed is None or self._packed.device != dev:
+                self._packed = torch.empty(nf, dtype=torch.float32, device=dev)
+            arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
+            freq = timestep_frequencies(self.spec["ch"], dev)
+            with torch.cuda.device(dev):
+                _lib.check(lib.ertd_unet_pack(ctypes.byref(self.cfg), arr, freq.data_ptr(),
+                                              self._packed.data_ptr(), _lib.stream_of(dev)),
+                           "unet_pack")
+            self._packed_key = key
+        return self._packed
+
+    def workspace(self, dev: torch.device, B: int, L: int) -> torch.Tensor:
+        n = _lib.lib().ertd_unet_workspace_bytes(ctypes.byref(self.cfg), B, L)
+        if n == 0:
+            raise RuntimeError("ertdiff: unsupported U-Net configuration")
+        ws = self._ws.get(dev)
+        if ws is None or ws.numel() < n:
+            self._ws.pop(dev, None)
+            ws = torch.empty(n, dtype=torch.uint8, device=dev)
+            self._ws[dev] = ws
+        return ws
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, t: torch.Tensor, condition: torch.Tensor,
+                return_cond_emb: bool = False):
+        dev = _lib.require_device(x, t, condition, self.conv_in.weight)
+        x = _lib.f32c(x, "x")
+        cond = _lib.f32c(condition, "condition")
+        B = x.shape[0]
+        if x.dim() != 2 or x.shape[1] != self.param_dim:
+            raise RuntimeError(f"ertdiff: x must be (B, {self.param_dim}), got {tuple(x.shape)}")
+        if cond.dim() != 3 or cond.shape[0] != B or cond.shape[1] != _lib.CIN:
+            raise RuntimeError(f"ertdiff: condition must be (B, 14, L), got {tuple(cond.shape)}")
+        tt = t.to(torch.int64).contiguous()
+        if tt.shape != (B,):
+            raise RuntimeError(f"ertdiff: t must be (B,), got {tuple(t.shape)}")
+        L = cond.shape[2]
+        out = torch.empty(B, self.param_dim, dtype=torch.float32, device=dev)
+        cemb = torch.empty(B, _lib.HIDDEN, dtype=torch.float32, device=dev) if return_cond_emb else None
+        packed = self.packed_weights(dev)
+        ws = self.workspace(dev, B, L)
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().ertd_unet_forward(
+                ctypes.byref(self.cfg), packed.data_ptr(), x.data_ptr(), tt.data_ptr(),
+                cond.data_ptr(), _lib.CIN * L, L, B, out.data_ptr(), _lib.ptr(cemb), ws.data_ptr(),
+                ws.numel(), _lib.stream_of(dev)), "unet_forward")
+        return (out, cemb) if return_cond_emb else out
+
+
+class _UPrepared:
+    def __init__(self, model: ConditionalUNet, condition, T, betas, alphas, alpha_bar, num_steps,
+                 temperature, shared_condition):
+        dev = _lib.require_device(condition, model.conv_in.weight)
+        self.dev = dev
+        cond = _lib.f32c(condition, "condition")
+        if cond.dim() == 2:
+            cond = cond.unsqueeze(0)
+        if cond.dim() != 3 or cond.shape[1] != _lib.CIN:
+            raise RuntimeError(f"ertdiff: condition must be (B, 14, L), got {tuple(condition.shape)}")
+        self.cond = cond
+        self.L = cond.shape[2]
+        self.stride = 0 if shared_condition else _lib.CIN * self.L
+        self.num_steps = T if num_steps is None else int(num_steps)
+        if not 1 <= self.num_steps <= T:
+            raise RuntimeError(f"ertdiff: num_steps={self.num_steps} must be in [1, T={T}]")
+        self.tables = step_tables(betas, alphas, alpha_bar, self.num_steps, temperature).to(dev)
+        self.model = model
+        self.packed = model.packed_weights(dev)
+
+    def args(self, B, x, noise, seed, member_offset, t_first, n_run, ws):
+        tb = self.tables
+        return (ctypes.byref(self.model.cfg), self.packed.data_ptr(), self.cond.data_ptr(),
+                self.stride, self.L, B, self.num_steps, t_first, n_run, tb[0].data_ptr(),
+                tb[1].data_ptr(), tb[2].data_ptr(), _lib.ptr(noise), int(seed) & (2**64 - 1),
+                int(member_offset) & 0xFFFFFFFF, x.data_ptr(), ws.data_ptr(), ws.numel())
+
+
+@torch.no_grad()
+def sample_unet(model: ConditionalUNet, condition, T, betas, alphas, alpha_bar, param_dim, device,
+                num_steps=None, temperature=1.0, *, noise: Union[str, torch.Tensor] = "torch",
+                seed: int = 0, member_offset: int = 0, shared_condition: bool = False,
+                n_members: Optional[int] = None, **_ignored):
+    """sample_model (ERT_Conditional_Diffusion.py:102-119) with the U-Net
+    denoiser: same signature, same noise options as ertdiff.sample_model."""
+    from .sampler import draw_reference_noise, philox_normal
+    if model.param_dim != param_dim:
+        raise RuntimeError(f"ertdiff: param_dim={param_dim} but the U-Net predicts {model.param_dim}")
+    prep = _UPrepared(model, condition, T, betas, alphas, alpha_bar, num_steps, temperature,
+                      shared_condition)
+    n = prep.num_steps
+    dev = prep.dev
+    B = n_members if shared_condition else prep.cond.shape[0]
+    inj = None
+    if isinstance(noise, torch.Tensor):
+        inj = _lib.f32c(noise, "noise")
+        if inj.dim() != 3 or inj.shape[0] != n or inj.shape[2] != param_dim:
+            raise RuntimeError(f"ertdiff: noise must be (num_steps={n}, B, {param_dim})")
+        B = inj.shape[1]
+        x = inj[0].clone()
+    elif noise == "torch":
+        if B is None:
+            raise RuntimeError("ertdiff: shared_condition needs n_members")
+        inj = draw_reference_noise(B, param_dim, n, device).to(dev)
+        x = inj[0].clone()
+    elif noise == "philox":
+        x = philox_normal(B, param_dim, n, 1, seed, member_offset, dev)
+    else:
+        raise ValueError("noise must be 'torch', 'philox' or a tensor")
+    if not shared_condition and prep.cond.shape[0] != B:
+        raise RuntimeError(f"ertdiff: condition batch {prep.cond.shape[0]} != noise batch {B}")
+    ws = model.workspace(dev, B, prep.L)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().ertd_unet_sample(*prep.args(B, x, inj, seed, member_offset, n - 1, n,
+                                                          ws), _lib.stream_of(dev)), "unet_sample")
+    return x
+
+
+class UNetSamplerPlan:
+    """hipGraph plan of one U-Net sampler call (head graph + one step graph
+    replayed n_run times); ``x`` holds the state, set it to x_T before launch."""
+
+    def __init__(self, model: ConditionalUNet, condition, T, betas, alphas, alpha_bar, *,
+                 num_steps=None, t_first=None, n_run=None, temperature=1.0, seed=0,
+                 member_offset=0, B=None, shared_condition=False,
+                 noise: Optional[torch.Tensor] = None):
+        self.prep = _UPrepared(model, condition, T, betas, alphas, alpha_bar, num_steps,
+                               temperature, shared_condition)
+        n = self.prep.num_steps
+        dev = self.prep.dev
+        self.dev = dev
+        self.t_first = n - 1 if t_first is None else int(t_first)
+        self.n_run = self.t_first + 1 if n_run is None else int(n_run)
+        self.B = B if B is not None else self.prep.cond.shape[0]
+        self.noise = None if noise is None else _lib.f32c(noise, "noise")
+        self.x = torch.zeros(self.B, model.param_dim, dtype=torch.float32, device=dev)
+        self.ws = model.workspace(dev, self.B, self.prep.L)
+        self._plan = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().ertd_unet_sample_plan_create(
+                *self.prep.args(self.B, self.x, self.noise, seed, member_offset, self.t_first,
+                                self.n_run, self.ws), ctypes.byref(self._plan)),
+                "unet_sample_plan_create")
+
+    def launch(self, stream: Optional[torch.cuda.Stream] = None):
+        s = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
+        with torch.cuda.device(self.dev):
+            _lib.check(_lib.lib().ertd_unet_plan_launch(self._plan, s), "unet_plan_launch")
+
+    def close(self):
+        if self._plan:
+            _lib.lib().ertd_unet_plan_destroy(self._plan)
+            self._plan = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -217,6 +217,63 @@ int ertd_train_step(const ertd_weights* w, float* packed, const float* x0, const
                     float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
                     float eps, float* loss_out, void* ws, size_t ws_bytes, void* stream);
 
+/* ---- build-defined conditional U-Net (SURVEY.md 8a'; north_star) -----------------
+ * PARITY UNPINNED vs the reference: ERT_Conditional_Diffusion.py has no U-Net
+ * (SURVEY.md 0.3).  The specification is oracle/unet_torch.py: x (B, image^2)
+ * viewed as (B,1,image,image); emb = time MLP(sinusoid(t, ch)) + Linear(128->4ch)
+ * of the reference's condition encoder (:133-142); ResBlocks of GroupNorm ->
+ * SiLU -> 3x3 conv (+emb) -> GroupNorm -> SiLU -> 3x3 conv (+1x1 skip);
+ * stride-2 Downsample, nearest-x2 Upsample + 3x3 conv, optional single-head
+ * mid-block attention; GroupNorm -> SiLU -> 3x3 conv out.  fp32 throughout
+ * (convs on fp32 MFMA).  Activations NCHW in the caller's workspace.         */
+typedef struct ertd_unet_config {
+  int image;       /* H = W: 16..128, power of two                          */
+  int ch;          /* base channels                                         */
+  int n_levels;    /* 1..4; every level >= 16x16                           */
+  int ch_mult[4];  /* channel multiplier per level                          */
+  int num_res;     /* ResBlocks per level on the way down (num_res+1 up)    */
+  int attn;        /* 1: mid-block attention (needs 16x16 and C % 256 == 0) */
+  int groups;      /* GroupNorm groups (32)                                 */
+} ertd_unet_config;
+
+/* Parameter tensors in state_dict order: count, and (name, shape) of one.  */
+int ertd_unet_n_params(const ertd_unet_config* cfg);
+int ertd_unet_param_info(const ertd_unet_config* cfg, int idx, char* name, int name_len,
+                         int64_t* shape, int* ndim);
+/* Packed device weights (floats) and their packing from the params array
+ * (ertd_unet_n_params device pointers, state_dict order).  freq: (ch/2)
+ * float32 sinusoid frequencies computed on the host with the reference's
+ * get_timestep_embedding expression (:80-88) at dim = ch.                 */
+size_t ertd_unet_packed_floats(const ertd_unet_config* cfg);
+int ertd_unet_pack(const ertd_unet_config* cfg, const float* const* params, const float* freq,
+                   float* packed, void* stream);
+/* Workspace bytes for batch B and condition length L (forward and sampler). */
+size_t ertd_unet_workspace_bytes(const ertd_unet_config* cfg, int B, int L);
+/* eps = unet(x (B, image^2), t (B,) int64, cond (B,14,L) with member stride
+ * cond_stride floats (0: one shared condition)); cond_emb_out (B,128) optional. */
+int ertd_unet_forward(const ertd_unet_config* cfg, const float* packed, const float* x,
+                      const int64_t* t, const float* cond, long long cond_stride, int L, int B,
+                      float* out, float* cond_emb_out, void* ws, size_t ws_bytes, void* stream);
+/* sample_model (:102-119) around the U-Net: steps t = t_first .. t_first-n_run+1 on
+ * x_inout (B, image^2); c1/c2/sigma/noise/seed/member_offset as in ertd_sample.
+ * The condition embedding is computed once per call (it does not depend on x
+ * or t; recomputing it per step would give identical bits).               */
+int ertd_unet_sample(const ertd_unet_config* cfg, const float* packed, const float* cond,
+                     long long cond_stride, int L, int B, int num_steps, int t_first, int n_run,
+                     const float* c1, const float* c2, const float* sigma, const float* noise,
+                     uint64_t seed, uint32_t member_offset, float* x_inout, void* ws,
+                     size_t ws_bytes, void* stream);
+/* The same call as a plan: the head and one step are captured as hipGraphs
+ * once; a launch replays head + n_run x step on `stream`.                 */
+typedef struct ertd_unet_plan ertd_unet_plan;
+int ertd_unet_sample_plan_create(const ertd_unet_config* cfg, const float* packed, const float* cond,
+                                 long long cond_stride, int L, int B, int num_steps, int t_first,
+                                 int n_run, const float* c1, const float* c2, const float* sigma,
+                                 const float* noise, uint64_t seed, uint32_t member_offset,
+                                 float* x_inout, void* ws, size_t ws_bytes, ertd_unet_plan** plan);
+int ertd_unet_plan_launch(ertd_unet_plan* plan, void* stream);
+int ertd_unet_plan_destroy(ertd_unet_plan* plan);
+
 #ifdef __cplusplus
 }
 #endif

@@ -146,3 +146,39 @@ def test_checkpoint_roundtrip(tmp_path):
                        "train_history", "val_history", "param_dim"}
     for k, v in m.state_dict().items():
         assert torch.equal(v, m2.state_dict()[k])
+
+
+@pytest.mark.parametrize("name", ["U1", "U2", "U3", "U5"])
+def test_unet_layout_matches_spec(name):
+    """The library's U-Net parameter enumeration (state_dict order and
+    shapes) and the module's init equal the specification
+    (oracle/unet_torch.py, build-defined: parity unpinned vs the reference)."""
+    from oracle import unet_torch as U
+    m = ertdiff.ConditionalUNet.from_config(name, seed=0)
+    spec = [(n, tuple(s)) for n, s in U.layer_shapes(U.CONFIGS[name])]
+    assert [(k, tuple(v.shape)) for k, v in m.state_dict().items()] == spec
+    W = U.init_weights(U.CONFIGS[name], 0)
+    assert all(torch.equal(W[k], v) for k, v in m.state_dict().items())
+
+
+def test_unet_host_queries_and_errors():
+    import ctypes
+    from ertdiff.unet import make_config
+    lib = _lib.load()
+    good = make_config(64, 64, (1, 2, 4), 2, False)
+    assert lib.ertd_unet_packed_floats(ctypes.byref(good)) > 14_000_000
+    assert lib.ertd_unet_workspace_bytes(ctypes.byref(good), 2, 4693) > 0
+    for bad in (make_config(48, 64, (1, 2, 4)),            # not a power of two
+                make_config(64, 64, (1, 2, 4, 8, 8)[:4]),  # 8x8 level
+                make_config(64, 64, (1, 2), attn=True),    # attention needs 16x16
+                make_config(64, 48, (1, 2, 4))):           # channels % groups
+        assert lib.ertd_unet_n_params(ctypes.byref(bad)) == _lib.ERTD_EINVAL
+        assert lib.ertd_unet_packed_floats(ctypes.byref(bad)) == 0
+    assert lib.ertd_unet_forward(ctypes.byref(good), None, None, None, None, 0, 1, 1, None, None,
+                                 None, 0, None) == _lib.ERTD_EINVAL
+
+
+def test_unet_forward_raises_off_gpu():
+    m = ertdiff.ConditionalUNet.from_config("U1", seed=0)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 1024), torch.zeros(1, dtype=torch.long), torch.zeros(1, 14, 9))
