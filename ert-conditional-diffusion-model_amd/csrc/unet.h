@@ -12,7 +12,7 @@
 namespace ertd {
 namespace unet {
 
-constexpr int CK = 8;       // input channels per K-chunk of the implicit GEMM
+constexpr int CK = 4;       // input channels per K-chunk of the implicit GEMM
 constexpr int NTHR = 256;   // conv workgroup: 4 waves, each a 64 (cout) x 64 (pixel) tile
 constexpr double GN_EPS = 1e-5;   // GroupNorm eps (oracle/unet_torch.py)
 
@@ -27,7 +27,7 @@ struct ConvArgs {
   const float* srcB;     // (B, Cb, Hs, Ws)  channels [Ca, Ca+Cb) (skip concat) or null
   int Ca, Cb;
   const float2* gn;      // (B, Cin) {scale, shift}: GroupNorm(x) = x*scale + shift (ACT_GN*)
-  const float* wpk;      // packed weights: [co_tile32][chunk][group][64 lanes][4]
+  const float* wpk;      // packed weights: [co_tile32][chunk][step pair][64 lanes][2]
   const float* bias;     // (Cout)
   const float* ebias;    // (B, eb_stride) per-sample per-channel add (offset applied) or null
   int eb_stride;
@@ -36,13 +36,7 @@ struct ConvArgs {
   int Cin, Cout;
   int Hs, Ws;            // source spatial size
   int Ho, Wo;            // output spatial size
-  int IR, IP;            // staged LDS image rows / pitch (floats) per channel
-  int ir_magic;          // ceil(2^19 / IR): row / IR == (row * ir_magic) >> 19 for row < 4096
-  int nchunk;            // ceil(Cin / CK)
 };
-
-// groups of 4 k-steps per chunk in the packed weight stream
-__host__ __device__ constexpr int conv_groups(int ks) { return ks == 3 ? 9 : 1; }
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
 // packed floats of one conv's weights

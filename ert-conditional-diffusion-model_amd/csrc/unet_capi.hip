@@ -213,19 +213,7 @@ struct Walk {
     if (mode == MODE_UP) { Ho = Hs * 2; Wo = Ws * 2; }
     if (!out) out = alloc((size_t)B * Cout * Ho * Wo);
     if (dry) return out;
-    const int wco = Cout >= 128 ? 2 : 1;
-    const int bm = 64 * (4 / wco);
-    const int R = bm / Wo;
-    int IR;
-    if (ks == 1) IR = R;
-    else if (mode == MODE_S2) IR = 2 * R + 1;
-    else IR = R + 2;
-    const int Wst = mode == MODE_UP ? 2 * Ws : Ws;
-    const int IP = Wst + 2;
-    const int rstep = NTHR / Wst;
-    const int nit = (CK * IR + rstep - 1) / rstep;
-    if (bm % Wo || (Ho * Wo) % bm || Wst > NTHR || nit > (mode == MODE_S2 ? 36 : 20) ||
-        CK * IR >= 4096 || Cin != Ca + Cb) {
+    if (Cin != Ca + Cb) {
       chk(hipErrorInvalidValue);
       return out;
     }
@@ -238,9 +226,6 @@ struct Walk {
     a.res = res; a.out = out;
     a.Cin = Cin; a.Cout = Cout;
     a.Hs = Hs; a.Ws = Ws; a.Ho = Ho; a.Wo = Wo;
-    a.IR = IR; a.IP = IP;
-    a.ir_magic = (int)(((1u << 19) + IR - 1) / IR);
-    a.nchunk = (Cin + CK - 1) / CK;
     chk(launch_conv(ks, mode, act, a, B, s));
     return out;
   }

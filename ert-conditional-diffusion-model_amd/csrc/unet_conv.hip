@@ -7,22 +7,27 @@
 // GEMM view per sample: rows = output channels (A = packed weights), columns =
 // output pixels (B = im2col of the staged input), K = Cin * ks * ks.
 // Workgroup = 4 waves, each a 64 (cout) x 64 (pixel) tile = 2 x 2 MFMA tiles;
-// WCO waves along cout, 4/WCO along pixels, so a workgroup covers BN = 64*WCO
+// WCO waves along cout, 4/WCO along pixels: a workgroup covers BN = 64*WCO
 // output channels x BM = 64*(4/WCO) consecutive output pixels of one sample.
+// The output width WO is a template parameter, so every LDS offset of the
+// inner loop is an immediate.
 //
-// K is walked in chunks of CK = 8 input channels.  Per chunk the input rows the
-// tile needs (with the 3x3 halo) are staged in LDS as an image [c][row][col]
-// with a zero column on each side, AFTER the input transform (GroupNorm
-// apply + SiLU for a ResBlock's convs, nothing for Downsample/Upsample/skip):
-// zero padding therefore pads the activated tensor, as in the oracle.  The
-// stage of chunk k+1 is loaded into registers while chunk k's MFMAs run
-// (double-buffered LDS, one barrier per chunk).
+// K is walked in chunks of CK = 4 input channels.  Per chunk:
+//   * the weight slice (BN couts x 4 channels x 9 taps, pre-packed in MFMA
+//     fragment order) is copied global -> LDS by LDS-DMA (global_load_lds,
+//     16 B per lane) one chunk ahead, so the MFMA loop issues no global loads;
+//   * the input rows the tile needs (with the 3x3 halo) are loaded into
+//     registers one chunk ahead, transformed (GroupNorm apply + SiLU for a
+//     ResBlock's convs, GroupNorm only for the attention qkv, nothing for
+//     Downsample/Upsample/skip) and written as an LDS image [c][row][col]
+//     with a zero column on each side; zero padding therefore pads the
+//     activated tensor, as in the oracle.
+// Both LDS images are double-buffered; one barrier per chunk.
 //
-// K order inside a chunk: lane half h takes channels 4h..4h+3, k-step s takes
-// channel s/9 of that half and tap s%9, so a lane's LDS operand address is a
-// per-lane base plus a per-step constant.  The host packs W in exactly this
-// order ([co_tile32][chunk][group of 4 steps][lane][4]) so each lane streams
-// its A operands as one coalesced float4 per 4 k-steps.
+// K order inside a chunk: lane half h takes channels 2h, 2h+1; k-step s takes
+// channel s/9 of that pair and tap s%9, so a lane's LDS operand address is a
+// per-lane base plus a per-step immediate.  The host packs W in exactly this
+// order: [co_tile32][chunk][step pair][lane][2] (ds_read_b64 per 2 steps).
 //
 // Skip concatenations (the up path) are read from two source tensors in place
 // (channels [0,Ca) from srcA, [Ca,Ca+Cb) from srcB); the nearest x2 Upsample is
@@ -32,112 +37,157 @@
 namespace ertd {
 namespace unet {
 
-template <int MODE, int KS>
-__device__ __forceinline__ int first_row(int oy0) {
-  if constexpr (KS == 1) return oy0;
-  else if constexpr (MODE == MODE_S2) return 2 * oy0 - 1;
-  else return oy0 - 1;
+// LDS byte address of a pointer into dynamic shared memory (the M0 base of an
+// LDS-DMA instruction)
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <int KS, int MODE, int ACT, int WCO>
+template <int KS, int MODE, int WCO, int WO>
+struct ConvGeom {
+  static constexpr int WPX = 4 / WCO;
+  static constexpr int BM = 64 * WPX;                 // output pixels per workgroup
+  static constexpr int BN = 64 * WCO;                 // output channels per workgroup
+  static constexpr int WST = MODE == MODE_S2 ? 2 * WO : WO;   // staged image width
+  static constexpr int R = BM / WO;                   // output rows per workgroup
+  static constexpr int IR = KS == 1 ? R : (MODE == MODE_S2 ? 2 * R + 1 : R + 2);
+  static constexpr int IP = WST + 2;                  // LDS row pitch (zero column each side)
+  static constexpr int CP = IR * IP;                  // channel pitch
+  static constexpr int HP = 2 * CP + (MODE == MODE_S2 ? 1 : 0);  // lane-half (channel pair) pitch
+  static constexpr int XB = (2 * HP + 3) / 4 * 4;     // input image floats per buffer
+  static constexpr int SPC = KS == 3 ? 18 : 2;        // k-steps per chunk
+  static constexpr int TW = SPC * 64;                 // weight floats per 32-cout tile and chunk
+  static constexpr int WB = (BN / 32) * TW;           // weight floats per buffer
+  static constexpr int RSTEP = NTHR / WST;            // staged rows per thread pass
+  static constexpr int NROWS = CK * IR;
+  static constexpr int NIT = (NROWS + RSTEP - 1) / RSTEP;
+  static constexpr int NGL = WB / 256;                // 16-B-per-lane DMA instructions per chunk
+  static constexpr size_t LDS = (size_t)(2 * XB + 2 * WB) * sizeof(float);
+  static_assert(BM % WO == 0, "tile must hold whole output rows");
+  static_assert(WST <= NTHR, "staged row wider than the workgroup");
+  static_assert(WB % 256 == 0, "weight slice must be whole DMA instructions");
+};
+
+template <int KS, int MODE, int ACT, int WCO, int WO>
 __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
-  constexpr int WPX = 4 / WCO;
-  constexpr int BM = 64 * WPX;           // output pixels per workgroup
-  constexpr int BN = 64 * WCO;           // output channels per workgroup
-  constexpr int NG = conv_groups(KS);    // weight groups (4 k-steps) per chunk
-  constexpr int NIT = MODE == MODE_S2 ? 36 : 20;  // max staged rows per thread
+  using G = ConvGeom<KS, MODE, WCO, WO>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* wim = smem;                  // [2][WB] weight slices (DMA targets, 16-B aligned)
+  float* xim = smem + 2 * G::WB;      // [2][XB] input images
+  float2* gtab = reinterpret_cast<float2*>(smem + 2 * G::WB + 2 * G::XB);  // [Cin] GN scale/shift
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, l32 = lane & 31;
   const int wco = wave % WCO, wpx = wave / WCO;
   const int b = blockIdx.z;
-  const int p0 = blockIdx.x * BM;
-  const int Wo = a.Wo;
-  const int oy0 = p0 / Wo;
-  const int IR = a.IR, IP = a.IP, ICH = IR * IP;
-  const int CHB = CK * ICH;              // floats per LDS buffer
-  const int Wst = MODE == MODE_UP ? 2 * a.Ws : a.Ws;   // staged image width
-  const int Hst = MODE == MODE_UP ? 2 * a.Hs : a.Hs;
+  const int p0 = blockIdx.x * G::BM;
+  const int oy0 = p0 / WO;
   const int Cin = a.Cin, Ca = a.Ca;
+  constexpr int HS = MODE == MODE_UP ? WO / 2 : G::WST;   // source height = width (square)
+  constexpr int HST = MODE == MODE_UP ? WO : G::WST;      // staged image height
+  const int nchunk = (Cin + CK - 1) / CK;
 
-  // ---- zero the halo columns of both buffers (never written by staging)
-  for (int r = tid; r < 2 * CK * IR; r += NTHR) {
-    smem[r * IP] = 0.f;
-    smem[r * IP + IP - 1] = 0.f;
+  // ---- GroupNorm table of this sample, zero halo columns of both images
+  if constexpr (ACT != ACT_NONE) {
+    for (int c = tid; c < Cin; c += NTHR) gtab[c] = a.gn[(size_t)b * Cin + c];
+  }
+  for (int r = tid; r < 2 * CK * G::IR; r += NTHR) {  // rows of [buf][c][row]
+    const int buf = r / (CK * G::IR), rem = r - buf * (CK * G::IR);
+    const int c = rem / G::IR, rr = rem - c * G::IR;
+    float* row = xim + buf * G::XB + (c >> 1) * G::HP + (c & 1) * G::CP + rr * G::IP;
+    row[0] = 0.f;
+    row[G::IP - 1] = 0.f;
   }
 
   // ---- staging geometry: thread -> (column, first row slot)
-  const int col = tid % Wst;             // Wst is a power of two <= 256
-  const int rstep = NTHR / Wst;
-  const int rs0 = tid / Wst;
-  const int nrows = CK * IR;
-  const int row0 = first_row<MODE, KS>(oy0);
+  const int col = tid % G::WST;
+  const int rs0 = tid / G::WST;
+  int row0;
+  if constexpr (KS == 1) row0 = oy0;
+  else if constexpr (MODE == MODE_S2) row0 = 2 * oy0 - 1;
+  else row0 = oy0 - 1;
   const int sx = MODE == MODE_UP ? (col >> 1) : col;
+  constexpr size_t plane = (size_t)HS * HS;
 
-  float stg[NIT];
+  float stg[G::NIT];
+  // branch-free: out-of-image / padded-channel elements load a valid address
+  // and are replaced by zero
   auto load_chunk = [&](int k) {
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int fr = rs0 + it * rstep;
-      float v = 0.f;
-      if (fr < nrows) {
-        const int c = (int)(((unsigned)fr * (unsigned)a.ir_magic) >> 19), r = fr - c * IR;
-        const int cg = k * CK + c;
-        const int iy = row0 + r;
-        if (cg < Cin && iy >= 0 && iy < Hst) {
-          const int sy = MODE == MODE_UP ? (iy >> 1) : iy;
-          const float* src = cg < Ca ? a.srcA + ((size_t)b * Ca + cg) * a.Hs * a.Ws
-                                     : a.srcB + ((size_t)b * a.Cb + (cg - Ca)) * a.Hs * a.Ws;
-          v = src[sy * a.Ws + sx];
-        }
-      }
-      stg[it] = v;
+    for (int it = 0; it < G::NIT; ++it) {
+      const int fr = rs0 + it * G::RSTEP;
+      const int c = fr / G::IR, r = fr - c * G::IR;
+      const int cg = k * CK + c;
+      const int iy = row0 + r;
+      const bool ok = (fr < G::NROWS) && cg < Cin && iy >= 0 && iy < HST;
+      const int cgc = ok ? cg : 0;
+      const int sy = ok ? (MODE == MODE_UP ? (iy >> 1) : iy) : 0;
+      const float* src = cgc < Ca ? a.srcA + ((size_t)b * Ca + cgc) * plane
+                                  : a.srcB + ((size_t)b * a.Cb + (cgc - Ca)) * plane;
+      stg[it] = src[sy * HS + sx];   // raw; the zero select happens in store_chunk
     }
   };
-  auto store_chunk = [&](int k, float* buf) {
+  auto store_chunk = [&](int k, float* img) {
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int fr = rs0 + it * rstep;
-      if (fr < nrows) {
-        const int c = (int)(((unsigned)fr * (unsigned)a.ir_magic) >> 19), r = fr - c * IR;
+    for (int it = 0; it < G::NIT; ++it) {
+      const int fr = rs0 + it * G::RSTEP;
+      if (fr < G::NROWS) {
+        const int c = fr / G::IR, r = fr - c * G::IR;
         const int cg = k * CK + c;
         const int iy = row0 + r;
+        const bool ok = cg < Cin && iy >= 0 && iy < HST;
         float v = stg[it];
         if constexpr (ACT != ACT_NONE) {
-          if (cg < Cin && iy >= 0 && iy < Hst) {
-            const float2 g = a.gn[(size_t)b * Cin + cg];
-            v = v * g.x + g.y;  // ATen's folded GroupNorm: x*scale + shift
-            if constexpr (ACT == ACT_GN_SILU) v = v / (1.0f + expf(-v));
-          }
+          const float2 g = gtab[ok ? cg : 0];
+          v = fmaf(v, g.x, g.y);  // ATen's folded GroupNorm: x*scale + shift
+          if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
         }
-        buf[fr * IP + col + 1] = v;
+        img[(c >> 1) * G::HP + (c & 1) * G::CP + r * G::IP + col + 1] = ok ? v : 0.f;
       }
     }
   };
+
+  // ---- weight slice DMA: chunk k of this workgroup's BN/32 tiles -> wim[buf]
+  const int tile_wg = blockIdx.y * (G::BN / 32);
+  // LDS-DMA by inline asm: hipcc's own global_load_lds bookkeeping waits
+  // vmcnt(0) before every DMA (serialising them); here they are counted by
+  // hand -- the single wait is the vmcnt(0) ahead of the chunk's barrier.
+  auto dma_weights = [&](int k, float* wdst) {
+#pragma unroll
+    for (int j = 0; j < (G::NGL + 3) / 4; ++j) {
+      const int ins = wave + 4 * j;                 // wave-uniform
+      if (ins < G::NGL) {
+        const int f = ins * 256 + lane * 4;          // float index in the slice
+        const int ti = f / G::TW, wi = f - ti * G::TW;
+        const float* src = a.wpk + ((size_t)(tile_wg + ti) * nchunk + k) * G::TW + wi;
+        const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr(wdst + ins * 256));
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(dst)
+            : "memory");
+      }
+    }
+  };
+  auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
   // ---- per-lane LDS operand bases (pixel tiles t = 0, 1 of this wave)
   int lbase[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const int pl = wpx * 64 + t * 32 + l32;   // pixel within the workgroup tile
-    const int oyl = pl / Wo, ox = pl - oyl * Wo;
+    const int pl = wpx * 64 + t * 32 + l32;
+    const int oyl = pl / WO, ox = pl - oyl * WO;
     int rb, cb;
     if constexpr (KS == 1) { rb = oyl; cb = ox + 1; }
     else if constexpr (MODE == MODE_S2) { rb = 2 * oyl; cb = 2 * ox; }
     else { rb = oyl; cb = ox; }
-    lbase[t] = h * 4 * ICH + rb * IP + cb;
+    lbase[t] = h * G::HP + rb * G::IP + cb;
   }
-
-  // ---- weight stream of this wave's two 32-cout tiles
-  const int nchunk = a.nchunk;
-  const int tile0 = blockIdx.y * (BN / 32) + wco * 2;
-  const float4* wp0 = reinterpret_cast<const float4*>(a.wpk) + (size_t)tile0 * nchunk * NG * 64 + lane;
-  const float4* wp1 = wp0 + (size_t)nchunk * NG * 64;
-  const int gtotal = nchunk * NG;
-  int gnext = 0;
-  float4 wn0 = wp0[0], wn1 = wp1[0];
+  const int abase = (wco * 2) * G::TW + lane * 2;
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -145,41 +195,49 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
+  dma_weights(0, wim);
+  if constexpr (ACT != ACT_NONE) __syncthreads();  // gtab visible to store_chunk
   load_chunk(0);
-  store_chunk(0, smem);
+  store_chunk(0, xim);
+  dma_wait();
   __syncthreads();
 
   for (int k = 0; k < nchunk; ++k) {
-    const float* buf = smem + (k & 1) * CHB;
-    if (k + 1 < nchunk) load_chunk(k + 1);
+    const int cur = k & 1;
+    const float* xb = xim + cur * G::XB;
+    const float* wb = wim + cur * G::WB;
+    if (k + 1 < nchunk) {
+      dma_weights(k + 1, wim + (cur ^ 1) * G::WB);
+      load_chunk(k + 1);
+    }
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const float4 w0 = wn0, w1 = wn1;
-      gnext = gnext + 1 < gtotal ? gnext + 1 : gnext;
-      wn0 = wp0[(size_t)gnext * 64];
-      wn1 = wp1[(size_t)gnext * 64];
-      const float wa0[4] = {w0.x, w0.y, w0.z, w0.w};
-      const float wa1[4] = {w1.x, w1.y, w1.z, w1.w};
+    for (int sp = 0; sp < G::SPC / 2; ++sp) {
+      const float2 w0 = *reinterpret_cast<const float2*>(wb + abase + sp * 128);
+      const float2 w1 = *reinterpret_cast<const float2*>(wb + abase + G::TW + sp * 128);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int s = g * 4 + s4;
+      for (int e = 0; e < 2; ++e) {
+        const int s = 2 * sp + e;
         int off;
-        if constexpr (KS == 1) off = s * ICH;
-        else off = (s / 9) * ICH + ((s % 9) / 3) * IP + (s % 3);
-        const float b0 = buf[lbase[0] + off];
-        const float b1 = buf[lbase[1] + off];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa0[s4], b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa0[s4], b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa1[s4], b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa1[s4], b1, acc[1][1], 0, 0, 0);
+        if constexpr (KS == 1) off = s * G::CP;
+        else off = (s / 9) * G::CP + ((s % 9) / 3) * G::IP + (s % 3);
+        const float b0 = xb[lbase[0] + off];
+        const float b1 = xb[lbase[1] + off];
+        const float a0 = e ? w0.y : w0.x;
+        const float a1 = e ? w1.y : w1.x;
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
       }
     }
-    if (k + 1 < nchunk) store_chunk(k + 1, smem + ((k + 1) & 1) * CHB);
+    if (k + 1 < nchunk) store_chunk(k + 1, xim + (cur ^ 1) * G::XB);
+    dma_wait();
     __syncthreads();
   }
 
   // ---- epilogue: bias (+ per-sample channel add) (+ residual), NCHW store
-  const size_t HWo = (size_t)a.Ho * Wo;
+  constexpr size_t HWo = (size_t)WO * WO;
+  const int tile0 = tile_wg + wco * 2;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -202,27 +260,42 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   }
 }
 
-template <int KS, int MODE, int ACT>
-static hipError_t launch_t(const ConvArgs& a, int B, hipStream_t s) {
-  const int wco = (a.Cout >= 128) ? 2 : 1;
-  const int bm = 64 * (4 / wco), bn = 64 * wco;
-  const size_t lds = (size_t)2 * CK * a.IR * a.IP * sizeof(float);
-  dim3 grid((unsigned)((size_t)a.Ho * a.Wo / bm), (unsigned)((a.Cout + bn - 1) / bn), (unsigned)B);
-  if (wco == 2) {
-    if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, 2>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    conv_kernel<KS, MODE, ACT, 2><<<grid, NTHR, lds, s>>>(a);
-  } else {
-    if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, 1>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    conv_kernel<KS, MODE, ACT, 1><<<grid, NTHR, lds, s>>>(a);
-  }
+template <int KS, int MODE, int ACT, int WCO, int WO>
+static hipError_t launch_g(const ConvArgs& a, int B, hipStream_t s) {
+  using G = ConvGeom<KS, MODE, WCO, WO>;
+  const size_t lds = G::LDS + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, WCO, WO>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  dim3 grid((unsigned)(WO * WO / G::BM), (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
+  conv_kernel<KS, MODE, ACT, WCO, WO><<<grid, NTHR, lds, s>>>(a);
   return hipGetLastError();
 }
 
+template <int KS, int MODE, int ACT, int WCO>
+static hipError_t launch_w(const ConvArgs& a, int B, hipStream_t s) {
+  switch (a.Wo) {
+    case 16: return launch_g<KS, MODE, ACT, WCO, 16>(a, B, s);
+    case 32: return launch_g<KS, MODE, ACT, WCO, 32>(a, B, s);
+    case 64: return launch_g<KS, MODE, ACT, WCO, 64>(a, B, s);
+    case 128:
+      if constexpr (MODE != MODE_S2) return launch_g<KS, MODE, ACT, WCO, 128>(a, B, s);
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int KS, int MODE, int ACT>
+static hipError_t launch_t(const ConvArgs& a, int B, hipStream_t s) {
+  if (a.Cout >= 128) return launch_w<KS, MODE, ACT, 2>(a, B, s);
+  return launch_w<KS, MODE, ACT, 1>(a, B, s);
+}
+
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
+  if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
+  const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
+  if (a.Wo != expect) return hipErrorInvalidValue;
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_t<3, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_t<3, MODE_S1, ACT_GN_SILU>(a, B, s);
   if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_t<3, MODE_S2, ACT_NONE>(a, B, s);
@@ -232,33 +305,33 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
   return hipErrorInvalidValue;
 }
 
-// ---- weight packing: W (Cout, Cin, ks, ks) -> [co_tile32][chunk][group][lane][4]
-// Cout is padded to a multiple of 128 (so a 2-tile wave never reads past the
+// ---- weight packing: W (Cout, Cin, ks, ks) -> [co_tile32][chunk][step pair][lane][2]
+// Cout is padded to a multiple of 128 (a workgroup's tiles never run past the
 // end), Cin to a multiple of CK; padding is zero.
 size_t conv_packed_floats(int cin, int cout, int ks) {
   const size_t tiles = (size_t)((cout + 127) / 128) * 4;
   const size_t nchunk = (size_t)((cin + CK - 1) / CK);
-  return tiles * nchunk * conv_groups(ks) * 64 * 4;
+  return tiles * nchunk * (ks == 3 ? 18 : 2) * 64;
 }
 
 __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout, int ks,
                                  int nchunk, size_t total, float* __restrict__ dst) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int NG = conv_groups(ks);
-  const int e = (int)(i & 3);
-  const int lane = (int)((i >> 2) & 63);
-  size_t rest = i >> 8;
-  const int g = (int)(rest % NG);
-  rest /= NG;
+  const int spc = ks == 3 ? 18 : 2;
+  const int e = (int)(i & 1);
+  const int lane = (int)((i >> 1) & 63);
+  size_t rest = i >> 7;
+  const int sp = (int)(rest % (spc / 2));
+  rest /= (spc / 2);
   const int k = (int)(rest % nchunk);
   const int tile = (int)(rest / nchunk);
-  const int s = g * 4 + e;
+  const int s = 2 * sp + e;
   const int hh = lane >> 5;
   const int co = tile * 32 + (lane & 31);
   int ci, ky, kx;
-  if (ks == 3) { ci = k * CK + hh * 4 + s / 9; ky = (s % 9) / 3; kx = s % 3; }
-  else { ci = k * CK + hh * 4 + s; ky = 0; kx = 0; }
+  if (ks == 3) { ci = k * CK + hh * 2 + s / 9; ky = (s % 9) / 3; kx = s % 3; }
+  else { ci = k * CK + hh * 2 + s; ky = 0; kx = 0; }
   float v = 0.f;
   if (co < cout && ci < cin) v = w[(((size_t)co * cin + ci) * ks + ky) * ks + kx];
   dst[i] = v;
