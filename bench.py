@@ -1,32 +1,34 @@
-"""Benchmark: denoising steps/s of the conditional-DDPM sampler on MI355X.
+"""Benchmark: denoising steps/s of the conditional DDPM sampler on MI355X.
 
-Workload (BASELINE.json configs[1] restated on the reference model, SURVEY.md
-8d "R2"): ConditionalDiffusionModel(29, 128) (the only denoiser the reference
-has), batch 64 members per GPU, condition (64, 14, 4693) fp32, T = 1000,
-faithful mode -- the condition encoder is re-evaluated at every step exactly as
-the reference's sample_model does (ERT_Conditional_Diffusion.py:108-118).
+Headline workload = BASELINE.json configs[1] exactly: "64x64 grid, 3-level
+U-Net (ch=64), T=1000, batch 64, fp32, 1xMI355X" -- the build-defined
+conditional U-Net of SURVEY.md 8a' (ertdiff.ConditionalUNet "U2": 14.19 M
+parameters, 16.26 GFLOP per sample-step; PARITY UNPINNED vs the reference,
+which has no U-Net; pinned to the build's own fp32 spec oracle/unet_torch.py).
+A step = one reverse update of all B members (time/condition embedding, the
+U-Net forward, the DDPM update).  The timed region replays a captured step
+graph --steps times (inputs resident in HBM); barrier + synchronize on each
+side, max over ranks.  One process per GPU (torchrun); members are sharded
+(rank r owns global members r*B..r*B+B-1, noise keyed by global member id),
+the only collective on the data path is one RCCL broadcast of the
+conditioning tensor from rank 0 before timing.
 
-A step = one reverse update of all B members (encoder + head + update).  The
-timed region replays captured hipGraphs of whole chains / chain segments with
-inputs already resident in HBM; exactly --steps steps are timed between a
-barrier + synchronize on each side, max over ranks.  One process per GPU
-(torchrun); members are sharded (rank r owns global members r*B..r*B+B-1,
-noise keyed by global member id) and the only collective on the data path is
-one RCCL broadcast of the conditioning tensor from rank 0 before timing.
-
-The faithful chain runs as ONE persistent kernel per chain
-(faithful_chain_kernel: encoder strip workers streaming ahead of per-member
-step chains, chain.hip); mode "faithful_steps" times the per-step schedule
-(an encoder and a head launch per step) instead.
+extra.reference_model: the same measurement for the reference's OWN denoiser
+(ConditionalDiffusionModel(29,128), SURVEY.md 8d "R2", parity pinned
+bit-exactly to ERT_Conditional_Diffusion.py), faithful mode (the encoder
+re-evaluated every step, as sample_model does), one persistent
+faithful_chain_kernel launch per 1000-step chain; with its own roofline and
+CPU baseline (oracle/ref_torch.py, bit-identical to the reference).
 
 Extra objects on the JSON line:
-  roofline      the dominant kernel: faithful_chain_kernel (fp32 faithful) --
-                algorithmic FLOP of the reference model per member-step x B x
-                steps per launch / launch duration (HIP events on the launching
-                stream); fp32 MFMA-bound.  extra.roofline_strip: the per-step
-                schedule's strip kernel the same way.
-  cpu_baseline  the reference algorithm on PyTorch-CPU (oracle/ref_torch.py,
-                bit-identical to the reference) on rank 0, bounded sample.
+  roofline      the dominant kernel of the headline: the U-Net's fp32-MFMA
+                implicit-GEMM conv kernels (conv_kernel<...>, ~93 % of the
+                step): algorithmic conv FLOP of one step / the step's duration
+                (HIP events on the launching stream around whole step graphs,
+                so GroupNorm statistics and the small kernels count against
+                it: a lower bound on the conv kernels' own rate).
+  cpu_baseline  the U-Net spec (oracle/unet_torch.py) on PyTorch-CPU on rank 0,
+                bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -62,10 +64,18 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=1000, help="untimed steps (a multiple of T keeps every chain launch T steps long)")
+    ap.add_argument("--steps", type=int, default=200, help="timed U-Net denoising steps")
+    ap.add_argument("--warmup", type=int, default=20, help="untimed U-Net steps")
     ap.add_argument("--batch", type=int, default=64, help="members per GPU")
     ap.add_argument("--T", type=int, default=1000)
+    ap.add_argument("--unet", choices=["U1", "U2", "U3", "U5"], default="U2",
+                    help="headline network (U2 = BASELINE configs[1])")
+    ap.add_argument("--cpu-unet-seconds", type=float, default=10.0)
+    ap.add_argument("--no-reference", action="store_true",
+                    help="skip the reference-model (R2) measurement in extra")
+    ap.add_argument("--ref-steps", type=int, default=2000)
+    ap.add_argument("--ref-warmup", type=int, default=1000,
+                    help="untimed R2 steps (a multiple of T keeps every chain launch T steps long)")
     ap.add_argument("--mode", choices=["faithful", "faithful_steps", "hoisted"], default="faithful")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -250,8 +260,24 @@ def train_bench(dev, steps=200, B=32, T=500):
             "train_ms_per_step": round(el / steps * 1e3, 4), "train_final_loss": round(float(loss), 5)}
 
 
+def _tune_cpu_allocator():
+    """Give the CPU baseline its best case: glibc's default mmap threshold
+    makes every fresh multi-MB conv output an mmap + page-fault zero-fill, so
+    the same reference code measures 2-13x slower in a fresh process than
+    after a large earlier allocation raised the threshold.  Raise it (and the
+    trim threshold) up front so every CPU number is the fast, stable one."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        libc.mallopt(-3, 1 << 30)        # M_MMAP_THRESHOLD
+        libc.mallopt(-1, (1 << 31) - 1)  # M_TRIM_THRESHOLD
+    except OSError:
+        pass
+
+
 def cpu_train_baseline(seconds, B=32, T=500):
     from oracle import ref_torch as RT
+    _tune_cpu_allocator()
     threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
     torch.set_num_threads(threads)
     torch.manual_seed(42)
@@ -277,6 +303,7 @@ def cpu_baseline(seconds, B, T, mode):
     """Reference algorithm on PyTorch-CPU (the oracle restatement, which is
     bit-identical to ERT_Conditional_Diffusion.py's sample_model), bounded."""
     from oracle import ref_torch as RT
+    _tune_cpu_allocator()
     threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(1042)
@@ -300,15 +327,13 @@ def cpu_baseline(seconds, B, T, mode):
             "seconds": round(el, 2)}
 
 
-def main():
-    a = parse()
-    rank, world, dev = setup_dist()
+def bench_reference(a, rank, world, dev):
+    """R2: the reference's own denoiser, faithful mode (extra.reference_model)."""
     B, T = a.batch, a.T
     torch.manual_seed(42)
     model = ertdiff.ConditionalDiffusionModel(P, 128).to(dev).eval()
     model.precision = a.precision
-    # synthetic conditioning batch in the MinMax domain [0,1) (:257-261); one
-    # RCCL broadcast from rank 0 is the only collective on the data path
+    # synthetic conditioning batch in the MinMax domain [0,1) (:257-261)
     g = torch.Generator(device=dev).manual_seed(1042)
     cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
     if world > 1:
@@ -318,62 +343,166 @@ def main():
     x_T = ertdiff.philox_normal(B, P, T, 1, 2042, offset, dev)
 
     plan_of = make_plans(model, cond, sched, T, B, a.mode, 2042, offset)
-    prepare(plan_of, a.steps, T, x_T)                  # build + replay the timed plans once
-    run_steps(plan_of, a.warmup, T, x_T)              # untimed warmup
+    prepare(plan_of, a.ref_steps, T, x_T)              # build + replay the timed plans once
+    run_steps(plan_of, a.ref_warmup, T, x_T)          # untimed warmup
     torch.cuda.synchronize(dev)
-    el = time_steps(plan_of, a.steps, T, x_T, world, dev)
-    value = world * a.steps / el
+    el = time_steps(plan_of, a.ref_steps, T, x_T, world, dev)
+    value = world * a.ref_steps / el
     if a.mode != "hoisted":
         for n, p in plan_of.cache.items():
             if p.status() != 0:
                 raise RuntimeError(f"faithful sampler plan n_run={n} timed out (status {p.status()})")
-
-    extra = {}
+    out = {"workload": f"R2: ConditionalDiffusionModel(29,128) (the reference's denoiser, parity "
+                       f"pinned) {a.mode} DDPM sampling, cond ({B},14,{L_MEAS}), T={T}",
+           "value": round(value, 2), "unit": "denoising-steps/sec", "steps": a.ref_steps,
+           "warmup": a.ref_warmup, "ms_per_step": round(el / a.ref_steps * 1e3, 5)}
     if a.mode == "faithful" and not a.no_steps_schedule:
         splan = make_plans(model, cond, sched, T, B, "faithful_steps", 2042, offset)
         prepare(splan, T, T, x_T)
         sel = time_steps(splan, T, T, x_T, world, dev)
-        extra["faithful_steps_schedule_steps_per_s"] = round(world * T / sel, 1)
+        out["faithful_steps_schedule_steps_per_s"] = round(world * T / sel, 1)
     if not a.no_hoisted and a.mode == "faithful":
         hplan = make_plans(model, cond, sched, T, B, "hoisted", 2042, offset)
         prepare(hplan, T, T, x_T)
         run_steps(hplan, T, T, x_T)
         hel = time_steps(hplan, T, T, x_T, world, dev)
-        extra["hoisted_steps_per_s"] = round(world * T / hel, 1)
+        out["hoisted_steps_per_s"] = round(world * T / hel, 1)
     roof_strip = None if a.no_strip_roofline else strip_kernel_roofline(model, cond, B, a.precision,
                                                                         a.roofline_reps, dev)
     if a.mode == "faithful" and a.precision == "fp32":
-        roof = chain_kernel_roofline(plan_of(T), B, T, 5, dev)
-        extra["roofline_strip"] = roof_strip
+        out["roofline"] = chain_kernel_roofline(plan_of(T), B, T, 5, dev)
+        out["roofline_strip"] = roof_strip
     else:
-        roof = roof_strip
+        out["roofline"] = roof_strip
     if not a.no_train:
-        extra.update(train_bench(dev))
-    cpu = None
+        out.update(train_bench(dev))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.cpu_seconds, B, T, "faithful")
-        if "hoisted_steps_per_s" in extra:
+        out["cpu_baseline"] = cpu
+        out["vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        if "hoisted_steps_per_s" in out:
             hc = cpu_baseline(max(3.0, a.cpu_seconds / 3), B, T, "hoisted")
-            extra["cpu_hoisted_steps_per_s"] = hc["value"]
+            out["cpu_hoisted_steps_per_s"] = hc["value"]
         if not a.no_train:
-            extra["cpu_train_steps_per_s"] = cpu_train_baseline(max(3.0, a.cpu_seconds / 3))
+            out["cpu_train_steps_per_s"] = cpu_train_baseline(max(3.0, a.cpu_seconds / 3))
+    out["member_steps_per_s"] = round(value * B, 1)
+    out["step_tflops"] = round(STEP_FLOP_PER_MEMBER * B / (el / a.ref_steps) / 1e12 * world, 2)
+    return out
+
+
+def cpu_unet_baseline(name, seconds, B, T):
+    """The U-Net spec (oracle/unet_torch.py) on PyTorch-CPU, bounded sample."""
+    from oracle import unet_torch as U
+    _tune_cpu_allocator()
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = U.CONFIGS[name]
+    W = U.init_weights(cfg, 0)
+    cond = torch.rand(B, 14, L_MEAS, generator=torch.Generator().manual_seed(1042))
+    base = torch.randn(3, B, cfg.param_dim, generator=torch.Generator().manual_seed(2042))
+
+    class _Cycled:  # (T, B, P) noise view over 3 draws: the CPU sample never needs more
+        shape = (T,) + tuple(base.shape[1:])
+
+        def __getitem__(self, k):
+            return base[k % 3]
+    noise = _Cycled()
+    U.sample(cond, W, cfg, T, noise, max_steps=1)          # warm
+    t0 = time.perf_counter()
+    U.sample(cond, W, cfg, T, noise, max_steps=1)
+    per = time.perf_counter() - t0
+    n = int(max(2, min(T, seconds / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    U.sample(cond, W, cfg, T, noise, max_steps=n)
+    el = time.perf_counter() - t0
+    return {"value": round(n / el, 4), "unit": "denoising-steps/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} of {T} steps of sample_model around the U-Net spec "
+                      f"(oracle/unet_torch.py, {name}), B={B}, cond (B,14,{L_MEAS}) fp32, "
+                      f"torch {torch.__version__} CPU, {threads} threads",
+            "seconds": round(el, 2)}
+
+
+def main():
+    a = parse()
+    rank, world, dev = setup_dist()
+    B, T = a.batch, a.T
+    from ertdiff.unet import CONFIGS, unet_flops
+    spec = CONFIGS[a.unet]
+    flops = unet_flops(**spec)
+    model = ertdiff.ConditionalUNet.from_config(a.unet, seed=0).to(dev).eval()
+    Pu = model.param_dim
+    g = torch.Generator(device=dev).manual_seed(1042)
+    cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
+    if world > 1:
+        dist.broadcast(cond, src=0)      # the one collective on the data path
+    sched = ertdiff.get_diffusion_schedule(T, device=dev)
+    offset = rank * B
+    x_T = ertdiff.philox_normal(B, Pu, T, 1, 2042, offset, dev)
+    timed = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=a.steps,
+                                    seed=2042, member_offset=offset)
+    warm = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1,
+                                   n_run=max(1, a.warmup), seed=2042, member_offset=offset)
+    warm.x.copy_(x_T)
+    warm.launch()                        # graph upload + warmup steps
+    timed.x.copy_(x_T)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    timed.launch(stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    ev_s = e0.elapsed_time(e1) * 1e-3
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    if not torch.isfinite(timed.x).all():
+        raise RuntimeError("U-Net sampler produced non-finite values")
+    value = world * a.steps / el
+    step_s = el / a.steps
+    conv_flop_step = flops["conv"] * B
+    achieved = conv_flop_step / (ev_s / a.steps) / 1e12
+    traffic = _traffic(f"unet_{a.unet}_B{B}_step")
+    roof = {"kernel": "conv_kernel<KS,MODE,ACT,WCO,WO> (all convs of one U-Net step)",
+            "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+            "avg_us_per_step": round(ev_s / a.steps * 1e6, 1),
+            "timing": f"HIP events on the launching stream around {a.steps} replayed step graphs "
+                      "(GroupNorm statistics, dense and update kernels included: a lower bound)",
+            "algorithmic_flop_per_step": conv_flop_step,
+            "flop_basis": f"{flops['conv']} conv FLOP per sample-step ({a.unet}, counted per layer, "
+                          f"= torch FlopCounter) x {B} members"}
+    extra = {"unet_step_tflops_all": round(flops["total"] * B / step_s / 1e12 * world, 2),
+             "unet_flop_per_sample_step": flops, "member_steps_per_s": round(value * B, 1)}
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_unet_baseline(a.unet, a.cpu_unet_seconds, B, T)
+        extra["vs_cpu_baseline"] = round(value / cpu["value"], 1)
+    del timed, warm
+    if not a.no_reference:
+        extra["reference_model"] = bench_reference(a, rank, world, dev)
     if rank == 0:
-        step_s = el / a.steps
-        extra.update({
-            "member_steps_per_s": round(value * B, 1),
-            "step_tflops": round(STEP_FLOP_PER_MEMBER * B / step_s / 1e12 * world, 2),
-            "vs_cpu_baseline": round(value / cpu["value"], 1) if cpu else None,
-        })
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "denoising-steps/sec",
+            "metric": METRIC, "value": round(value, 3), "unit": "denoising-steps/sec",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(step_s * 1e3, 5), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32" if a.precision == "fp32" else "bf16-operand/f32",
-            "data": "synthetic: cond U[0,1) (B,14,4693), seed-42 default-init weights, philox noise",
-            "config": {"workload": f"R2: ConditionalDiffusionModel(29,128) {a.mode} DDPM sampling, "
-                                   f"cond ({B},14,{L_MEAS}), T={T}",
-                       "global_batch": B * world, "members_per_gpu": B, "T": T, "mode": a.mode,
-                       "precision": a.precision, "parallelism": f"dp{world} (member shards)"},
+            "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: cond U[0,1) (B,14,4693), seeded uniform(+-1/sqrt(fan_in)) weights, "
+                    "philox noise",
+            "config": {"workload": f"{a.unet}: {spec['image']}x{spec['image']} grid, "
+                                   f"{len(spec['ch_mult'])}-level U-Net (ch={spec['ch']}"
+                                   f"{', mid attention' if spec['attn'] else ''}), T={T}, batch {B}, "
+                                   f"fp32 (BASELINE configs[1]; build-defined, SURVEY 8a')",
+                       "global_batch": B * world, "members_per_gpu": B, "T": T,
+                       "steps_timed": f"t = {T - 1} .. {T - a.steps}",
+                       "precision": "fp32", "parallelism": f"dp{world} (member shards)"},
             "roofline": roof, "cpu_baseline": cpu, "extra": extra,
         }
         print(json.dumps(line), flush=True)

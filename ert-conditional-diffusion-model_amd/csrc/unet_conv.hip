@@ -129,24 +129,26 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
       stg[it] = src[sy * HS + sx];   // raw; the zero select happens in store_chunk
     }
   };
+  // one staged element: GroupNorm(+SiLU) and the LDS write (element it of chunk k)
+  auto store_elem = [&](int it, int k, float* img) {
+    const int fr = rs0 + it * G::RSTEP;
+    if (fr < G::NROWS) {
+      const int c = fr / G::IR, r = fr - c * G::IR;
+      const int cg = k * CK + c;
+      const int iy = row0 + r;
+      const bool ok = cg < Cin && iy >= 0 && iy < HST;
+      float v = stg[it];
+      if constexpr (ACT != ACT_NONE) {
+        const float2 g = gtab[ok ? cg : 0];
+        v = fmaf(v, g.x, g.y);  // ATen's folded GroupNorm: x*scale + shift
+        if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+      }
+      img[(c >> 1) * G::HP + (c & 1) * G::CP + r * G::IP + col + 1] = ok ? v : 0.f;
+    }
+  };
   auto store_chunk = [&](int k, float* img) {
 #pragma unroll
-    for (int it = 0; it < G::NIT; ++it) {
-      const int fr = rs0 + it * G::RSTEP;
-      if (fr < G::NROWS) {
-        const int c = fr / G::IR, r = fr - c * G::IR;
-        const int cg = k * CK + c;
-        const int iy = row0 + r;
-        const bool ok = cg < Cin && iy >= 0 && iy < HST;
-        float v = stg[it];
-        if constexpr (ACT != ACT_NONE) {
-          const float2 g = gtab[ok ? cg : 0];
-          v = fmaf(v, g.x, g.y);  // ATen's folded GroupNorm: x*scale + shift
-          if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
-        }
-        img[(c >> 1) * G::HP + (c & 1) * G::CP + r * G::IP + col + 1] = ok ? v : 0.f;
-      }
-    }
+    for (int it = 0; it < G::NIT; ++it) store_elem(it, k, img);
   };
 
   // ---- weight slice DMA: chunk k of this workgroup's BN/32 tiles -> wim[buf]
@@ -202,6 +204,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   dma_wait();
   __syncthreads();
 
+  constexpr int H0 = G::SPC / 4;  // first step pair that carries staging work
   for (int k = 0; k < nchunk; ++k) {
     const int cur = k & 1;
     const float* xb = xim + cur * G::XB;
@@ -229,8 +232,15 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
         acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
       }
+      // the next chunk's staging work, spread over the second half of the
+      // step pairs: its VALU issues in the gaps of this chunk's MFMAs
+      // (a 32x32x2 f32 MFMA occupies the SIMD's matrix pipe for 64 cycles)
+      if (k + 1 < nchunk && sp >= H0) {
+#pragma unroll
+        for (int it = 0; it < G::NIT; ++it)
+          if (H0 + it % (G::SPC / 2 - H0) == sp) store_elem(it, k + 1, xim + (cur ^ 1) * G::XB);
+      }
     }
-    if (k + 1 < nchunk) store_chunk(k + 1, xim + (cur ^ 1) * G::XB);
     dma_wait();
     __syncthreads();
   }

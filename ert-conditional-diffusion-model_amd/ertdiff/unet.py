@@ -66,6 +66,53 @@ def param_layout(cfg: ErtdUnetConfig) -> List[Tuple[str, Tuple[int, ...]]]:
     return out
 
 
+def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, attn=False,
+               groups=32) -> Dict[str, int]:
+    """Algorithmic FLOP per sample-step (multiply-add = 2) of the U-Net forward:
+    convs, attention core (QK^T and PV) and the dense layers; elementwise work
+    (GroupNorm, SiLU, adds) is not counted."""
+    cfg = make_config(image, ch, ch_mult, num_res, attn, groups)
+    layout = param_layout(cfg)
+    conv = dense = 0
+    # spatial size per conv: walk the layout names
+    res_of = {}
+    r = image
+    nl = len(ch_mult)
+    for i in range(nl):
+        res_of[f"down.{i}"] = r
+        if i != nl - 1:
+            r //= 2
+    res_of["mid"] = r
+    for i in reversed(range(nl)):
+        res_of[f"up.{i}"] = image >> i
+    for name, shape in layout:
+        if not name.endswith(".weight") or name.startswith("condition_encoder"):
+            continue
+        parts = name.split(".")
+        if len(shape) == 4:
+            if parts[0] in ("conv_in", "conv_out"):
+                hw = image
+            elif parts[0] == "mid":
+                hw = res_of["mid"]
+            else:
+                hw = res_of[f"{parts[0]}.{parts[1]}"]
+                if parts[2] == "downsample":
+                    hw //= 2
+                elif parts[2] == "upsample":     # runs at the doubled resolution
+                    hw *= 2
+            conv += 2 * shape[0] * shape[1] * shape[2] * shape[3] * hw * hw
+        elif len(shape) == 2:
+            dense += 2 * shape[0] * shape[1]
+    attn_f = 0
+    if attn:
+        C = ch * ch_mult[-1]
+        N = res_of["mid"] ** 2
+        attn_f = 2 * 2 * N * N * C
+    enc = 6_308_736 + 14_426_112 + 2 * 64 * 128   # the reference's condition encoder (SURVEY 8a)
+    return {"conv": conv, "attention": attn_f, "dense": dense, "condition_encoder": enc,
+            "total": conv + attn_f + dense + enc}
+
+
 class ConditionalUNet(nn.Module):
     """eps(x, t, condition) with a 2-D U-Net over x viewed as (B,1,image,image).
 

@@ -211,17 +211,23 @@ def forward(x, t, cond, W: Weights, cfg: UNetConfig, return_emb: bool = False):
 
 
 @torch.no_grad()
-def sample(cond, W: Weights, cfg: UNetConfig, T: int, noise, num_steps=None, temperature=1.0):
+def sample(cond, W: Weights, cfg: UNetConfig, T: int, noise, num_steps=None, temperature=1.0,
+           max_steps=None):
     """sample_model (ERT_Conditional_Diffusion.py:102-119) around this U-Net, with
     injected noise (noise[0] = x_T, noise[k] = z for t = n-k) and the same
-    float64-scalar update expressions."""
+    float64-scalar update expressions.  ``max_steps`` stops early (bounded
+    CPU-baseline samples)."""
     betas = torch.linspace(1e-4, 0.02, T)
     alphas = 1.0 - betas
     alpha_bar = torch.cumprod(alphas, dim=0)
     n = T if num_steps is None else num_steps
     B = cond.shape[0] if noise is None else noise.shape[1]
     x = noise[0].clone()
+    done = 0
     for t_ in reversed(range(n)):
+        if max_steps is not None and done >= max_steps:
+            break
+        done += 1
         tt = torch.full((B,), t_, dtype=torch.long)
         pred = forward(x, tt, cond, W, cfg)
         coef = (1 - alphas[t_]) / (math.sqrt(1 - alpha_bar[t_]) + 1e-8)

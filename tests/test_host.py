@@ -182,3 +182,19 @@ def test_unet_forward_raises_off_gpu():
     m = ertdiff.ConditionalUNet.from_config("U1", seed=0)
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 1024), torch.zeros(1, dtype=torch.long), torch.zeros(1, 14, 9))
+
+
+@pytest.mark.parametrize("name", ["U1", "U3"])
+def test_unet_flop_count_matches_torch(name):
+    """bench.py's algorithmic FLOP per sample-step equals torch's FlopCounter
+    on the spec module."""
+    from torch.utils.flop_counter import FlopCounterMode
+    from oracle import unet_torch as U
+    from ertdiff.unet import CONFIGS, unet_flops
+    cfg = U.CONFIGS[name]
+    W = U.init_weights(cfg, 0)
+    with FlopCounterMode(display=False) as fc:
+        U.forward(torch.randn(1, cfg.param_dim), torch.tensor([3]), torch.rand(1, 14, 97), W, cfg)
+    enc_97 = 2 * 14 * 3 * 32 * 49 + 2 * 32 * 3 * 64 * 25 + 2 * 64 * 128  # encoder at L=97
+    f = unet_flops(**CONFIGS[name])
+    assert f["total"] - f["condition_encoder"] + enc_97 == fc.get_total_flops()

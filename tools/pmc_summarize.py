@@ -38,4 +38,25 @@ for key, name in KERNELS.items():
         "workload": "bench.py R2 faithful, B=64, L=4693, T=1000 (chain: one launch = 1000 steps)",
     }
     print(key, json.dumps(rec[key]))
+# U-Net: every ertd::unet:: kernel of the run, summed, per denoising step
+unet_steps = int(os.environ.get("UNET_STEPS", "0"))
+unet_key = os.environ.get("UNET_KEY", "unet_U2_B64_step")
+if unet_steps > 0:
+    fk = per_launch(fetch_dir, "FETCH_SIZE", "ertd::unet::")
+    wk = per_launch(write_dir, "WRITE_SIZE", "ertd::unet::")
+    if fk and wk:
+        rec[unet_key] = {
+            "kernel": "all ertd::unet:: kernels of one U-Net sampler step",
+            "hbm_bytes_per_launch": int((2 * sum(fk) * 1024 + sum(wk) * 1024) / unet_steps),
+            "fetch_size_kib_per_step": sum(fk) / unet_steps,
+            "write_size_kib_per_step": sum(wk) / unet_steps,
+            "dispatches": [len(fk), len(wk)], "steps": unet_steps,
+            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), summed over "
+                      "every ertd::unet:: dispatch / steps; bytes = 2*FETCH_SIZE*1024 + "
+                      "WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
+            "workload": "bench.py U2, B=64, L=4693 (steps incl. warmup)",
+        }
+        print(unet_key, json.dumps(rec[unet_key]))
+    else:
+        print(f"no ertd::unet:: rows ({len(fk)} fetch, {len(wk)} write)")
 json.dump(rec, open(out, "w"), indent=1)
