@@ -12,7 +12,6 @@
 namespace ertd {
 namespace unet {
 
-constexpr int CK = 4;       // input channels per K-chunk of the implicit GEMM
 constexpr int NTHR = 256;   // conv workgroup: 4 waves, each a 64 (cout) x 64 (pixel) tile
 constexpr double GN_EPS = 1e-5;   // GroupNorm eps (oracle/unet_torch.py)
 

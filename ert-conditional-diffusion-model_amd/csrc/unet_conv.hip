@@ -12,7 +12,7 @@
 // The output width WO is a template parameter, so every LDS offset of the
 // inner loop is an immediate.
 //
-// K is walked in chunks of CK = 4 input channels.  Per chunk:
+// K is walked in chunks of 4 input channels (3x3; 32 for 1x1).  Per chunk:
 //   * the weight slice (BN couts x 4 channels x 9 taps, pre-packed in MFMA
 //     fragment order) is copied global -> LDS by LDS-DMA (global_load_lds,
 //     16 B per lane) one chunk ahead, so the MFMA loop issues no global loads;
@@ -32,10 +32,21 @@
 // Skip concatenations (the up path) are read from two source tensors in place
 // (channels [0,Ca) from srcA, [Ca,Ca+Cb) from srcB); the nearest x2 Upsample is
 // folded into the staging address (source row/col = staged row/col >> 1).
+#include <cstdlib>
+
 #include "unet.h"
 
 namespace ertd {
 namespace unet {
+
+// ERTD_UNET_TPX=1|2 forces the wave tile (diagnostics); 0 = automatic
+static int conv_tpx_override() {
+  static int v = [] {
+    const char* e = getenv("ERTD_UNET_TPX");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 
 // LDS byte address of a pointer into dynamic shared memory (the M0 base of an
 // LDS-DMA instruction)
@@ -43,23 +54,28 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <int KS, int MODE, int WCO, int WO>
+// channels per K-chunk: 4 for 3x3 (36-deep K per chunk), 32 for 1x1 (32-deep)
+__host__ __device__ constexpr int conv_ck(int ks) { return ks == 3 ? 4 : 32; }
+
+template <int KS, int MODE, int WCO, int WO, int TPX>
 struct ConvGeom {
   static constexpr int WPX = 4 / WCO;
-  static constexpr int BM = 64 * WPX;                 // output pixels per workgroup
+  static constexpr int BM = 32 * TPX * WPX;           // output pixels per workgroup
   static constexpr int BN = 64 * WCO;                 // output channels per workgroup
   static constexpr int WST = MODE == MODE_S2 ? 2 * WO : WO;   // staged image width
   static constexpr int R = BM / WO;                   // output rows per workgroup
   static constexpr int IR = KS == 1 ? R : (MODE == MODE_S2 ? 2 * R + 1 : R + 2);
   static constexpr int IP = WST + 2;                  // LDS row pitch (zero column each side)
   static constexpr int CP = IR * IP;                  // channel pitch
-  static constexpr int HP = 2 * CP + (MODE == MODE_S2 ? 1 : 0);  // lane-half (channel pair) pitch
+  static constexpr int CKK = conv_ck(KS);             // input channels per chunk
+  static constexpr int CH = CKK / 2;                  // channels per lane half
+  static constexpr int HP = CH * CP + (MODE == MODE_S2 ? 1 : 0);  // lane-half pitch
   static constexpr int XB = (2 * HP + 3) / 4 * 4;     // input image floats per buffer
-  static constexpr int SPC = KS == 3 ? 18 : 2;        // k-steps per chunk
+  static constexpr int SPC = KS == 3 ? 9 * CH : CH;   // k-steps per chunk
   static constexpr int TW = SPC * 64;                 // weight floats per 32-cout tile and chunk
   static constexpr int WB = (BN / 32) * TW;           // weight floats per buffer
   static constexpr int RSTEP = NTHR / WST;            // staged rows per thread pass
-  static constexpr int NROWS = CK * IR;
+  static constexpr int NROWS = CKK * IR;
   static constexpr int NIT = (NROWS + RSTEP - 1) / RSTEP;
   static constexpr int NGL = WB / 256;                // 16-B-per-lane DMA instructions per chunk
   static constexpr size_t LDS = (size_t)(2 * XB + 2 * WB) * sizeof(float);
@@ -68,9 +84,9 @@ struct ConvGeom {
   static_assert(WB % 256 == 0, "weight slice must be whole DMA instructions");
 };
 
-template <int KS, int MODE, int ACT, int WCO, int WO>
+template <int KS, int MODE, int ACT, int WCO, int WO, int TPX>
 __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
-  using G = ConvGeom<KS, MODE, WCO, WO>;
+  using G = ConvGeom<KS, MODE, WCO, WO, TPX>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* wim = smem;                  // [2][WB] weight slices (DMA targets, 16-B aligned)
   float* xim = smem + 2 * G::WB;      // [2][XB] input images
@@ -87,6 +103,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   const int Cin = a.Cin, Ca = a.Ca;
   constexpr int HS = MODE == MODE_UP ? WO / 2 : G::WST;   // source height = width (square)
   constexpr int HST = MODE == MODE_UP ? WO : G::WST;      // staged image height
+  constexpr int CK = G::CKK;
   const int nchunk = (Cin + CK - 1) / CK;
 
   // ---- GroupNorm table of this sample, zero halo columns of both images
@@ -96,7 +113,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   for (int r = tid; r < 2 * CK * G::IR; r += NTHR) {  // rows of [buf][c][row]
     const int buf = r / (CK * G::IR), rem = r - buf * (CK * G::IR);
     const int c = rem / G::IR, rr = rem - c * G::IR;
-    float* row = xim + buf * G::XB + (c >> 1) * G::HP + (c & 1) * G::CP + rr * G::IP;
+    float* row = xim + buf * G::XB + (c / G::CH) * G::HP + (c % G::CH) * G::CP + rr * G::IP;
     row[0] = 0.f;
     row[G::IP - 1] = 0.f;
   }
@@ -143,7 +160,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
         v = fmaf(v, g.x, g.y);  // ATen's folded GroupNorm: x*scale + shift
         if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
       }
-      img[(c >> 1) * G::HP + (c & 1) * G::CP + r * G::IP + col + 1] = ok ? v : 0.f;
+      img[(c / G::CH) * G::HP + (c % G::CH) * G::CP + r * G::IP + col + 1] = ok ? v : 0.f;
     }
   };
   auto store_chunk = [&](int k, float* img) {
@@ -177,11 +194,11 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   };
   auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
-  // ---- per-lane LDS operand bases (pixel tiles t = 0, 1 of this wave)
-  int lbase[2];
+  // ---- per-lane LDS operand bases (pixel tiles t < TPX of this wave)
+  int lbase[TPX];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int pl = wpx * 64 + t * 32 + l32;
+  for (int t = 0; t < TPX; ++t) {
+    const int pl = wpx * 32 * TPX + t * 32 + l32;
     const int oyl = pl / WO, ox = pl - oyl * WO;
     int rb, cb;
     if constexpr (KS == 1) { rb = oyl; cb = ox + 1; }
@@ -191,11 +208,11 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   }
   const int abase = (wco * 2) * G::TW + lane * 2;
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][TPX];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    for (int j = 0; j < TPX; ++j) acc[i][j] = f32x16{};
 
   dma_weights(0, wim);
   if constexpr (ACT != ACT_NONE) __syncthreads();  // gtab visible to store_chunk
@@ -223,14 +240,16 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
         int off;
         if constexpr (KS == 1) off = s * G::CP;
         else off = (s / 9) * G::CP + ((s % 9) / 3) * G::IP + (s % 3);
-        const float b0 = xb[lbase[0] + off];
-        const float b1 = xb[lbase[1] + off];
+        float bv[TPX];
+#pragma unroll
+        for (int t = 0; t < TPX; ++t) bv[t] = xb[lbase[t] + off];
         const float a0 = e ? w0.y : w0.x;
         const float a1 = e ? w1.y : w1.x;
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < TPX; ++t) {
+          acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[t], acc[0][t], 0, 0, 0);
+          acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[t], acc[1][t], 0, 0, 0);
+        }
       }
       // the next chunk's staging work, spread over the second half of the
       // step pairs: its VALU issues in the gaps of this chunk's MFMAs
@@ -245,52 +264,80 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue: bias (+ per-sample channel add) (+ residual), NCHW store
+  // ---- epilogue: bias (+ per-sample channel add) (+ residual), NCHW store.
+  // All loads of a 32-cout tile are issued before any of its stores: out and
+  // res may not alias, but without the explicit phases hipcc must assume they
+  // do and serialises every residual load behind the previous store.
   constexpr size_t HWo = (size_t)WO * WO;
   const int tile0 = tile_wg + wco * 2;
+  const float* __restrict__ resp = a.res;
+  float* __restrict__ outp = a.out;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
+    float bias[16], eb[16], rv[16][TPX];
+    size_t obase[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      co = co < a.Cout ? co : a.Cout - 1;
+      obase[r] = ((size_t)b * a.Cout + co) * HWo + p0 + wpx * 32 * TPX + l32;
+      bias[r] = a.bias[co];
+      eb[r] = a.ebias ? a.ebias[(size_t)b * a.eb_stride + co] : 0.f;
+#pragma unroll
+      for (int j = 0; j < TPX; ++j) rv[r][j] = resp ? resp[obase[r] + j * 32] : 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (co >= a.Cout) continue;
-      const float bias = a.bias[co];
-      const float eb = a.ebias ? a.ebias[(size_t)b * a.eb_stride + co] : 0.f;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const size_t p = (size_t)p0 + wpx * 64 + j * 32 + l32;
-        const size_t o = ((size_t)b * a.Cout + co) * HWo + p;
+      for (int j = 0; j < TPX; ++j) {
         // the oracle's op order: conv(+bias), then + emb, then + residual
-        float v = acc[i][j][r] + bias;
-        if (a.ebias) v = v + eb;
-        if (a.res) v = v + a.res[o];
-        a.out[o] = v;
+        float v = acc[i][j][r] + bias[r];
+        if (a.ebias) v = v + eb[r];
+        if (resp) v = v + rv[r][j];
+        outp[obase[r] + j * 32] = v;
       }
     }
   }
 }
 
-template <int KS, int MODE, int ACT, int WCO, int WO>
+template <int KS, int MODE, int ACT, int WCO, int WO, int TPX>
 static hipError_t launch_g(const ConvArgs& a, int B, hipStream_t s) {
-  using G = ConvGeom<KS, MODE, WCO, WO>;
+  using G = ConvGeom<KS, MODE, WCO, WO, TPX>;
   const size_t lds = G::LDS + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, WCO, WO>,
+    (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, WCO, WO, TPX>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((unsigned)(WO * WO / G::BM), (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
-  conv_kernel<KS, MODE, ACT, WCO, WO><<<grid, NTHR, lds, s>>>(a);
+  conv_kernel<KS, MODE, ACT, WCO, WO, TPX><<<grid, NTHR, lds, s>>>(a);
   return hipGetLastError();
+}
+
+// Wave tile 64 co x 32*TPX px.  TPX = 1 (half the pixels per workgroup, twice
+// the workgroups) when the TPX = 2 grid would leave CUs with fewer than 4
+// workgroups (the 16x16 / 32x32 levels at B = 64).
+template <int KS, int MODE, int ACT, int WCO, int WO>
+static hipError_t launch_p(const ConvArgs& a, int B, hipStream_t s) {
+  const long long wg2 = (long long)(WO * WO / (64 * (4 / WCO))) * ((a.Cout + 64 * WCO - 1) / (64 * WCO)) * B;
+  int tpx = conv_tpx_override();
+  if (tpx == 0) tpx = 1;  // measured: TPX=1 (5 waves/SIMD) beats TPX=2 at every U2 layer
+  (void)wg2;
+  if constexpr (32 * (4 / WCO) >= WO) {
+    if (tpx == 1) return launch_g<KS, MODE, ACT, WCO, WO, 1>(a, B, s);
+  }
+  return launch_g<KS, MODE, ACT, WCO, WO, 2>(a, B, s);
 }
 
 template <int KS, int MODE, int ACT, int WCO>
 static hipError_t launch_w(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
-    case 16: return launch_g<KS, MODE, ACT, WCO, 16>(a, B, s);
-    case 32: return launch_g<KS, MODE, ACT, WCO, 32>(a, B, s);
-    case 64: return launch_g<KS, MODE, ACT, WCO, 64>(a, B, s);
+    case 16: return launch_p<KS, MODE, ACT, WCO, 16>(a, B, s);
+    case 32: return launch_p<KS, MODE, ACT, WCO, 32>(a, B, s);
+    case 64: return launch_p<KS, MODE, ACT, WCO, 64>(a, B, s);
     case 128:
-      if constexpr (MODE != MODE_S2) return launch_g<KS, MODE, ACT, WCO, 128>(a, B, s);
+      if constexpr (MODE != MODE_S2) return launch_p<KS, MODE, ACT, WCO, 128>(a, B, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -319,16 +366,18 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
 // Cout is padded to a multiple of 128 (a workgroup's tiles never run past the
 // end), Cin to a multiple of CK; padding is zero.
 size_t conv_packed_floats(int cin, int cout, int ks) {
+  const int ck = conv_ck(ks);
   const size_t tiles = (size_t)((cout + 127) / 128) * 4;
-  const size_t nchunk = (size_t)((cin + CK - 1) / CK);
-  return tiles * nchunk * (ks == 3 ? 18 : 2) * 64;
+  const size_t nchunk = (size_t)((cin + ck - 1) / ck);
+  return tiles * nchunk * (ks == 3 ? 9 * ck / 2 : ck / 2) * 64;
 }
 
 __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout, int ks,
                                  int nchunk, size_t total, float* __restrict__ dst) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int spc = ks == 3 ? 18 : 2;
+  const int ck = conv_ck(ks), ch = ck / 2;
+  const int spc = ks == 3 ? 9 * ch : ch;
   const int e = (int)(i & 1);
   const int lane = (int)((i >> 1) & 63);
   size_t rest = i >> 7;
@@ -340,8 +389,8 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout,
   const int hh = lane >> 5;
   const int co = tile * 32 + (lane & 31);
   int ci, ky, kx;
-  if (ks == 3) { ci = k * CK + hh * 2 + s / 9; ky = (s % 9) / 3; kx = s % 3; }
-  else { ci = k * CK + hh * 2 + s; ky = 0; kx = 0; }
+  if (ks == 3) { ci = k * ck + hh * ch + s / 9; ky = (s % 9) / 3; kx = s % 3; }
+  else { ci = k * ck + hh * ch + s; ky = 0; kx = 0; }
   float v = 0.f;
   if (co < cout && ci < cin) v = w[(((size_t)co * cin + ci) * ks + ky) * ks + kx];
   dst[i] = v;
@@ -349,7 +398,7 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout,
 
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s) {
   const size_t total = conv_packed_floats(cin, cout, ks);
-  const int nchunk = (cin + CK - 1) / CK;
+  const int nchunk = (cin + conv_ck(ks) - 1) / conv_ck(ks);
   pack_conv_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cout, ks, nchunk, total, dst);
   return hipGetLastError();
 }

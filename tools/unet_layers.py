@@ -1,0 +1,73 @@
+"""Per-layer efficiency of the U-Net convs from a rocprofv3 kernel trace of
+tools/unet_probe.py or bench.py (diagnostic).
+
+    python tools/unet_layers.py gpurun_out/<dir>/run_kernel_trace.csv [U2] [B]
+
+Replays the layer walk of unet_capi.hip (execution order of the convs) and
+zips it with the last step's conv dispatches in the trace."""
+import csv
+import sys
+
+cfgname = sys.argv[2] if len(sys.argv) > 2 else "U2"
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+CFG = {"U1": (32, 32, (1, 2), 2, False), "U2": (64, 64, (1, 2, 4), 2, False),
+       "U3": (64, 64, (1, 2, 4), 2, True)}[cfgname]
+image, ch0, mult, nres, attn = CFG
+
+
+def walk():
+    L = []
+    conv = lambda n, cin, cout, ks, wo: L.append((n, cin, cout, ks, wo))
+    H = image
+    conv("conv_in", 1, ch0, 3, H)
+    hs = [ch0]
+    ch = ch0
+    for i, m in enumerate(mult):
+        for r in range(nres):
+            o = ch0 * m
+            conv(f"d{i}r{r}.conv1", ch, o, 3, H)
+            if ch != o:
+                conv(f"d{i}r{r}.skip", ch, o, 1, H)
+            conv(f"d{i}r{r}.conv2", o, o, 3, H)
+            ch = o
+            hs.append(ch)
+        if i != len(mult) - 1:
+            conv(f"d{i}.down", ch, ch, 3, H // 2)
+            H //= 2
+            hs.append(ch)
+    for nm in ("mid1", "mid2"):
+        conv(f"{nm}.conv1", ch, ch, 3, H)
+        conv(f"{nm}.conv2", ch, ch, 3, H)
+        if nm == "mid1" and attn:
+            conv("attn.qkv", ch, 3 * ch, 1, H)
+            conv("attn.proj", ch, ch, 1, H)
+    for i in reversed(range(len(mult))):
+        for r in range(nres + 1):
+            o = ch0 * mult[i]
+            cin = ch + hs.pop()
+            conv(f"u{i}r{r}.conv1", cin, o, 3, H)
+            conv(f"u{i}r{r}.skip", cin, o, 1, H)
+            conv(f"u{i}r{r}.conv2", o, o, 3, H)
+            ch = o
+        if i != 0:
+            conv(f"u{i}.up", ch, ch, 3, H * 2)
+            H *= 2
+    conv("conv_out", ch, 1, 3, H)
+    return L
+
+
+layers = walk()
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_kernel<" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+last = rows[-len(layers):]
+tot_t = tot_f = 0
+for (n, cin, cout, ks, wo), r in zip(layers, last):
+    us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
+    fl = 2 * cin * cout * ks * ks * wo * wo * B
+    tot_t += us
+    tot_f += fl
+    tmpl = r["Kernel_Name"][r["Kernel_Name"].find("<"):r["Kernel_Name"].find(">") + 1]
+    wgs = int(r["Grid_Size_X"]) // 256 * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+    print(f"{n:14s} {cin:4d}->{cout:4d} k{ks} {wo:3d}  {tmpl:22s} wg {wgs:5d}  {us:8.1f} us  "
+          f"{fl / us / 1e6:7.1f} TF  {fl / us / 1e6 / 157.3 * 100:5.1f}%")
+print(f"total {tot_t:.0f} us, {tot_f / tot_t / 1e6:.1f} TF")
