@@ -38,6 +38,12 @@ struct ConvArgs {
 };
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
+// bf16-operand variant (unet_conv_bf16.hip): same arguments, wpk packed by
+// launch_pack_conv_bf16
+hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
+size_t conv_packed_floats_bf16(int cin, int cout, int ks);
+hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, float* dst,
+                                 hipStream_t s);
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s);

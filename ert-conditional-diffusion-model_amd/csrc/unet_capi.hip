@@ -40,6 +40,7 @@ bool cfg_ok(const ertd_unet_config* c) {
     if (c->ch_mult[i] < 1 || C % c->groups) return false;
   }
   if (c->ch % c->groups) return false;
+  if (c->precision != ERTD_PREC_FP32 && c->precision != ERTD_PREC_BF16) return false;
   if (c->attn) {
     const int Cm = c->ch * c->ch_mult[c->n_levels - 1];
     const int r = c->image >> (c->n_levels - 1);
@@ -163,7 +164,10 @@ Layout layout(const ertd_unet_config* c) {
     if (p.name.rfind("condition_encoder.", 0) == 0) continue;
     if (ends_with(p.name, ".emb.weight") || ends_with(p.name, ".emb.bias")) continue;
     L.off[p.name] = o;
-    if (p.shape.size() == 4) o += a64(conv_packed_floats(p.shape[1], p.shape[0], p.shape[2]));
+    if (p.shape.size() == 4)
+      o += a64(c->precision == ERTD_PREC_BF16
+                   ? conv_packed_floats_bf16(p.shape[1], p.shape[0], p.shape[2])
+                   : conv_packed_floats(p.shape[1], p.shape[0], p.shape[2]));
     else o += a64(p.numel());
   }
   L.total = o;
@@ -226,7 +230,8 @@ struct Walk {
     a.res = res; a.out = out;
     a.Cin = Cin; a.Cout = Cout;
     a.Hs = Hs; a.Ws = Ws; a.Ho = Ho; a.Wo = Wo;
-    chk(launch_conv(ks, mode, act, a, B, s));
+    chk(c->precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
+                                       : launch_conv(ks, mode, act, a, B, s));
     return out;
   }
 
@@ -498,6 +503,60 @@ struct ertd_unet_plan {
 
 extern "C" {
 
+// ---- single operators of the U-Net (the SURVEY 8a' operator rows), for
+// per-operator parity tests and microbenchmarks -----------------------------
+
+size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision) {
+  if (cin < 1 || cout < 1 || (ks != 1 && ks != 3)) return 0;
+  const size_t f = precision == ERTD_PREC_BF16 ? conv_packed_floats_bf16(cin, cout, ks)
+                                               : conv_packed_floats(cin, cout, ks);
+  return f * sizeof(float);
+}
+
+int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
+                const float* bias, int Cout, int ks, int mode, const float* gn, int act,
+                const float* ebias, int eb_stride, const float* res, float* out, int precision,
+                void* ws, size_t ws_bytes, void* stream) {
+  const int Cin = Ca + Cb;
+  if (!x || !w || !bias || !out || !ws || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
+      Cout < 1 || (ks != 1 && ks != 3) || mode < MODE_S1 || mode > MODE_UP ||
+      (ks == 1 && mode != MODE_S1) || act < ACT_NONE || act > ACT_GN || (act != ACT_NONE && !gn) ||
+      (precision != ERTD_PREC_FP32 && precision != ERTD_PREC_BF16))
+    return ERTD_EINVAL;
+  if (ertd_conv2d_workspace_bytes(Cin, Cout, ks, precision) > ws_bytes) return ERTD_ENOSPC;
+  hipStream_t s = (hipStream_t)stream;
+  float* pk = (float*)ws;
+  hipError_t e = precision == ERTD_PREC_BF16 ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s)
+                                             : launch_pack_conv(w, Cin, Cout, ks, pk, s);
+  if (e != hipSuccess) return (int)e;
+  ConvArgs a{};
+  a.srcA = x; a.srcB = x2; a.Ca = Ca; a.Cb = Cb;
+  a.gn = (const float2*)gn;
+  a.wpk = pk; a.bias = bias; a.ebias = ebias; a.eb_stride = eb_stride; a.res = res; a.out = out;
+  a.Cin = Cin; a.Cout = Cout; a.Hs = H; a.Ws = H;
+  a.Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  a.Wo = a.Ho;
+  e = precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
+                                  : launch_conv(ks, mode, act, a, B, s);
+  return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
+}
+
+int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B, int HW,
+                          int groups, const float* gamma, const float* beta, float* out,
+                          void* stream) {
+  const int C = Ca + Cb;
+  if (!x || !gamma || !beta || !out || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
+      groups < 1 || C % groups || HW < 4 || HW % 4)
+    return ERTD_EINVAL;
+  GnArgs g{x, x2, Ca, Cb, HW, groups, gamma, beta, (float2*)out};
+  return rcode(launch_gn_stats(g, B, (hipStream_t)stream));
+}
+
+int ertd_attention(const float* qkv, int B, int C, int N, float* out, void* stream) {
+  if (!qkv || !out || B < 1 || N != 256 || C < 2 || C % 256) return ERTD_EINVAL;
+  return rcode(launch_attention(qkv, C, N, out, nullptr, B, (hipStream_t)stream));
+}
+
 int ertd_unet_n_params(const ertd_unet_config* c) {
   if (!cfg_ok(c)) return ERTD_EINVAL;
   return (int)enumerate(c).size();
@@ -555,7 +614,11 @@ int ertd_unet_pack(const ertd_unet_config* c, const float* const* params, const 
       e = hipMemcpyAsync(packed + L.ball + col, src, p.numel() * sizeof(float),
                          hipMemcpyDeviceToDevice, s);
     } else if (p.shape.size() == 4) {
-      e = launch_pack_conv(src, p.shape[1], p.shape[0], p.shape[2], packed + L.off.at(p.name), s);
+      e = c->precision == ERTD_PREC_BF16
+              ? launch_pack_conv_bf16(src, p.shape[1], p.shape[0], p.shape[2],
+                                      packed + L.off.at(p.name), s)
+              : launch_pack_conv(src, p.shape[1], p.shape[0], p.shape[2],
+                                 packed + L.off.at(p.name), s);
     } else if (p.shape.size() == 2) {
       e = launch_transpose(src, p.shape[0], p.shape[1], packed + L.off.at(p.name), p.shape[0], s);
     } else {

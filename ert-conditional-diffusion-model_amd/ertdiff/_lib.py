@@ -72,6 +72,11 @@ SIGNATURES = {
                              _F, _F, _F, _VP, _VP, _SZ, _VP]),
     "ertd_postprocess": (_I, [_VP, ctypes.c_longlong, _I, ctypes.c_double, ctypes.c_double, _VP,
                               _VP, _VP, _VP, _VP, _VP]),
+    "ertd_conv2d_workspace_bytes": (_SZ, [_I, _I, _I, _I]),
+    "ertd_conv2d": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP,
+                         _I, _VP, _SZ, _VP]),
+    "ertd_group_norm_stats": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _VP]),
+    "ertd_attention": (_I, [_VP, _I, _I, _I, _VP, _VP]),
     "ertd_unet_n_params": (_I, [_VP]),
     "ertd_unet_param_info": (_I, [_VP, _I, ctypes.c_char_p, _I, _VP, ctypes.POINTER(_I)]),
     "ertd_unet_packed_floats": (_SZ, [_VP]),

@@ -30,7 +30,7 @@ from .schedule import step_tables, timestep_frequencies
 class ErtdUnetConfig(ctypes.Structure):
     _fields_ = [("image", ctypes.c_int), ("ch", ctypes.c_int), ("n_levels", ctypes.c_int),
                 ("ch_mult", ctypes.c_int * 4), ("num_res", ctypes.c_int), ("attn", ctypes.c_int),
-                ("groups", ctypes.c_int)]
+                ("groups", ctypes.c_int), ("precision", ctypes.c_int)]
 
 
 # SURVEY.md 8a' table (U4 = U2's network on the 1024-member ensemble)
@@ -42,11 +42,14 @@ CONFIGS: Dict[str, dict] = {
 }
 
 
+_PRECISIONS = {"fp32": 0, "bf16": 1}
+
+
 def make_config(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, attn=False,
-                groups=32) -> ErtdUnetConfig:
+                groups=32, precision: str = "fp32") -> ErtdUnetConfig:
     m = list(ch_mult) + [0] * (4 - len(ch_mult))
     return ErtdUnetConfig(int(image), int(ch), len(ch_mult), (ctypes.c_int * 4)(*m), int(num_res),
-                          int(bool(attn)), int(groups))
+                          int(bool(attn)), int(groups), _PRECISIONS[precision])
 
 
 def param_layout(cfg: ErtdUnetConfig) -> List[Tuple[str, Tuple[int, ...]]]:
@@ -123,11 +126,11 @@ class ConditionalUNet(nn.Module):
     """
 
     def __init__(self, image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, attn=False,
-                 groups=32, seed: Optional[int] = None):
+                 groups=32, seed: Optional[int] = None, precision: str = "fp32"):
         super().__init__()
         self.spec = dict(image=image, ch=ch, ch_mult=tuple(ch_mult), num_res=num_res, attn=attn,
                          groups=groups)
-        self.cfg = make_config(image, ch, ch_mult, num_res, attn, groups)
+        self.cfg = make_config(image, ch, ch_mult, num_res, attn, groups, precision)
         self.image = image
         self.param_dim = image * image
         self.layout = param_layout(self.cfg)
@@ -156,8 +159,21 @@ class ConditionalUNet(nn.Module):
         self._ws: Dict = {}
 
     @classmethod
-    def from_config(cls, name: str, seed: Optional[int] = None) -> "ConditionalUNet":
-        return cls(**CONFIGS[name], seed=seed)
+    def from_config(cls, name: str, seed: Optional[int] = None,
+                    precision: str = "fp32") -> "ConditionalUNet":
+        return cls(**CONFIGS[name], seed=seed, precision=precision)
+
+    @property
+    def precision(self) -> str:
+        return "bf16" if self.cfg.precision == 1 else "fp32"
+
+    def set_precision(self, precision: str) -> None:
+        """fp32 convs (default) or bf16 conv operands with fp32 accumulation;
+        the packed weights are rebuilt on the next call."""
+        self.cfg.precision = _PRECISIONS[precision]
+        self._packed = None
+        self._packed_key = None
+        self._ws = {}
 
     def _params(self) -> List[torch.Tensor]:
         sd = dict(self.named_parameters())
@@ -330,3 +346,69 @@ class UNetSamplerPlan:
             self.close()
         except Exception:
             pass
+
+
+# ---- single operators (ertd_conv2d / ertd_group_norm_stats / ertd_attention) ----------
+_MODES2D = {"same": 0, "down": 1, "up": 2}
+_ACTS = {"none": 0, "gn_silu": 1, "gn": 2}
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, *, mode: str = "same",
+           act: str = "none", gn: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None,
+           ebias: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
+           precision: str = "fp32") -> torch.Tensor:
+    """One U-Net convolution on the HIP kernel: conv(act(cat(x, x2))) + bias
+    (+ ebias[:, :, None, None]) (+ res); padding 1 for 3x3 (stride 2 for
+    mode="down", nearest x2 upsample first for mode="up").  gn: (B, Cin, 2)
+    {scale, shift} as returned by group_norm_stats."""
+    dev = _lib.require_device(x, weight, bias)
+    x = _lib.f32c(x, "x")
+    B, Ca, H, _ = x.shape
+    Cb = 0 if x2 is None else x2.shape[1]
+    Cout, Cin, ks, _ = weight.shape
+    if Cin != Ca + Cb:
+        raise RuntimeError("ertdiff: weight in-channels != input channels")
+    Ho = H // 2 if mode == "down" else (2 * H if mode == "up" else H)
+    out = torch.empty(B, Cout, Ho, Ho, dtype=torch.float32, device=dev)
+    prec = _PRECISIONS[precision]
+    n = _lib.lib().ertd_conv2d_workspace_bytes(Cin, Cout, ks, prec)
+    ws = torch.empty(max(n, 256), dtype=torch.uint8, device=dev)
+    w = _lib.f32c(weight, "weight")
+    bb = _lib.f32c(bias, "bias")
+    eb = None if ebias is None else _lib.f32c(ebias, "ebias")
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().ertd_conv2d(
+            x.data_ptr(), Ca, _lib.ptr(None if x2 is None else _lib.f32c(x2, "x2")), Cb, B, H,
+            w.data_ptr(), bb.data_ptr(), Cout, ks, _MODES2D[mode],
+            _lib.ptr(None if gn is None else _lib.f32c(gn, "gn")), _ACTS[act], _lib.ptr(eb),
+            0 if eb is None else eb.shape[1], _lib.ptr(None if res is None else _lib.f32c(res, "res")),
+            out.data_ptr(), prec, ws.data_ptr(), ws.numel(), _lib.stream_of(dev)), "conv2d")
+    return out
+
+
+def group_norm_stats(x: torch.Tensor, groups: int, gamma: torch.Tensor, beta: torch.Tensor,
+                     x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(B, C, 2) {scale, shift}: GroupNorm(cat(x, x2)) == x*scale + shift per channel."""
+    dev = _lib.require_device(x, gamma, beta)
+    x = _lib.f32c(x, "x")
+    B, Ca, H, W = x.shape
+    Cb = 0 if x2 is None else x2.shape[1]
+    out = torch.empty(B, Ca + Cb, 2, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().ertd_group_norm_stats(
+            x.data_ptr(), Ca, _lib.ptr(None if x2 is None else _lib.f32c(x2, "x2")), Cb, B, H * W,
+            groups, _lib.f32c(gamma, "gamma").data_ptr(), _lib.f32c(beta, "beta").data_ptr(),
+            out.data_ptr(), _lib.stream_of(dev)), "group_norm_stats")
+    return out
+
+
+def attention(qkv: torch.Tensor) -> torch.Tensor:
+    """qkv (B, 3C, N) -> (B, C, N): v softmax(q^T k / sqrt(C))^T (single head)."""
+    dev = _lib.require_device(qkv)
+    qkv = _lib.f32c(qkv, "qkv")
+    B, C3, N = qkv.shape
+    out = torch.empty(B, C3 // 3, N, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().ertd_attention(qkv.data_ptr(), B, C3 // 3, N, out.data_ptr(),
+                                             _lib.stream_of(dev)), "attention")
+    return out

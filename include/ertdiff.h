@@ -234,7 +234,31 @@ typedef struct ertd_unet_config {
   int num_res;     /* ResBlocks per level on the way down (num_res+1 up)    */
   int attn;        /* 1: mid-block attention (needs 16x16 and C % 256 == 0) */
   int groups;      /* GroupNorm groups (32)                                 */
+  int precision;   /* ERTD_PREC_FP32 (fp32 MFMA convs) or ERTD_PREC_BF16
+                      (bf16 conv operands, fp32 accumulate/activations)    */
 } ertd_unet_config;
+
+/* Single U-Net operators (the SURVEY 8a' operator rows; used by per-operator
+ * parity tests and microbenchmarks).
+ * ertd_conv2d: out (B,Cout,Ho,Ho) = conv(act(cat(x (B,Ca,H,H), x2 (B,Cb,H,H))))
+ *   + bias (+ ebias[b][co], row stride eb_stride) (+ res), ks 1|3, mode
+ *   0 stride 1 / 1 stride 2 (Downsample) / 2 nearest-x2 upsample then conv;
+ *   act 0 none / 1 GroupNorm+SiLU / 2 GroupNorm, gn = (B, Cin) float2
+ *   {scale, shift} from ertd_group_norm_stats; precision FP32 | BF16;
+ *   H in {16,32,64,128} (Ho likewise); ws >= ertd_conv2d_workspace_bytes
+ *   (the packed weights).
+ * ertd_group_norm_stats: per (sample, channel) {gamma*rstd, beta-mean*gamma*rstd}
+ *   of cat(x, x2) over `groups` groups (eps 1e-5), out (B, Ca+Cb) float2.
+ * ertd_attention: qkv (B, 3C, N) -> out (B, C, N) = v softmax(q^T k / sqrt C)^T, N = 256. */
+size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision);
+int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
+                const float* bias, int Cout, int ks, int mode, const float* gn, int act,
+                const float* ebias, int eb_stride, const float* res, float* out, int precision,
+                void* ws, size_t ws_bytes, void* stream);
+int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B, int HW,
+                          int groups, const float* gamma, const float* beta, float* out,
+                          void* stream);
+int ertd_attention(const float* qkv, int B, int C, int N, float* out, void* stream);
 
 /* Parameter tensors in state_dict order: count, and (name, shape) of one.  */
 int ertd_unet_n_params(const ertd_unet_config* cfg);

@@ -138,29 +138,36 @@ def sinusoid(t: torch.Tensor, dim: int) -> torch.Tensor:
     return torch.cat([torch.sin(arg), torch.cos(arg)], dim=1)
 
 
+def _conv_bf16(x, w, b, **kw):
+    """The bf16-operand conv of the HIP path (cfg precision bf16): the conv
+    input (after GroupNorm/SiLU) and the weights are rounded to bf16 (RNE),
+    products and sums in fp32."""
+    return F.conv2d(x.bfloat16().float(), w.bfloat16().float(), b, **kw)
+
+
 def _gn_silu(x, W, n, groups):
     return F.silu(F.group_norm(x, groups, W[f"{n}.weight"], W[f"{n}.bias"], eps=1e-5))
 
 
-def _res(x, emb_act, W, n, groups):
-    h = F.conv2d(_gn_silu(x, W, f"{n}.norm1", groups), W[f"{n}.conv1.weight"],
-                 W[f"{n}.conv1.bias"], padding=1)
+def _res(x, emb_act, W, n, groups, cv=F.conv2d):
+    h = cv(_gn_silu(x, W, f"{n}.norm1", groups), W[f"{n}.conv1.weight"],
+           W[f"{n}.conv1.bias"], padding=1)
     h = h + F.linear(emb_act, W[f"{n}.emb.weight"], W[f"{n}.emb.bias"])[:, :, None, None]
-    h = F.conv2d(_gn_silu(h, W, f"{n}.norm2", groups), W[f"{n}.conv2.weight"],
-                 W[f"{n}.conv2.bias"], padding=1)
+    h = cv(_gn_silu(h, W, f"{n}.norm2", groups), W[f"{n}.conv2.weight"],
+           W[f"{n}.conv2.bias"], padding=1)
     if f"{n}.skip.weight" in W:
-        x = F.conv2d(x, W[f"{n}.skip.weight"], W[f"{n}.skip.bias"])
+        x = cv(x, W[f"{n}.skip.weight"], W[f"{n}.skip.bias"])
     return x + h
 
 
-def _attn(x, W, n, groups):
+def _attn(x, W, n, groups, cv=F.conv2d):
     B, C, Hh, Ww = x.shape
-    qkv = F.conv2d(F.group_norm(x, groups, W[f"{n}.norm.weight"], W[f"{n}.norm.bias"], eps=1e-5),
-                   W[f"{n}.qkv.weight"], W[f"{n}.qkv.bias"]).reshape(B, 3, C, Hh * Ww)
+    qkv = cv(F.group_norm(x, groups, W[f"{n}.norm.weight"], W[f"{n}.norm.bias"], eps=1e-5),
+             W[f"{n}.qkv.weight"], W[f"{n}.qkv.bias"]).reshape(B, 3, C, Hh * Ww)
     q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
     a = torch.softmax(torch.einsum("bci,bcj->bij", q, k) / math.sqrt(C), dim=-1)
     o = torch.einsum("bij,bcj->bci", a, v).reshape(B, C, Hh, Ww)
-    return x + F.conv2d(o, W[f"{n}.proj.weight"], W[f"{n}.proj.bias"])
+    return x + cv(o, W[f"{n}.proj.weight"], W[f"{n}.proj.bias"])
 
 
 def condition_embedding(cond, W):
@@ -178,35 +185,37 @@ def embedding(t, cond, W, cfg: UNetConfig):
     return e + F.linear(condition_embedding(cond, W), W["cond_proj.weight"], W["cond_proj.bias"])
 
 
-def forward(x, t, cond, W: Weights, cfg: UNetConfig, return_emb: bool = False):
+def forward(x, t, cond, W: Weights, cfg: UNetConfig, return_emb: bool = False, bf16: bool = False):
+    """eps; ``bf16`` = the HIP path's bf16-operand convs (``_conv_bf16``)."""
     B = x.shape[0]
     g = cfg.groups
+    cv = _conv_bf16 if bf16 else F.conv2d
     emb = embedding(t, cond, W, cfg)
     ea = F.silu(emb)
-    h = F.conv2d(x.reshape(B, 1, cfg.image, cfg.image), W["conv_in.weight"], W["conv_in.bias"],
-                 padding=1)
+    h = cv(x.reshape(B, 1, cfg.image, cfg.image), W["conv_in.weight"], W["conv_in.bias"],
+           padding=1)
     hs = [h]
     nl = len(cfg.ch_mult)
     for i in range(nl):
         for r in range(cfg.num_res):
-            h = _res(h, ea, W, f"down.{i}.res.{r}", g)
+            h = _res(h, ea, W, f"down.{i}.res.{r}", g, cv)
             hs.append(h)
         if i != nl - 1:
-            h = F.conv2d(h, W[f"down.{i}.downsample.weight"], W[f"down.{i}.downsample.bias"],
-                         stride=2, padding=1)
+            h = cv(h, W[f"down.{i}.downsample.weight"], W[f"down.{i}.downsample.bias"],
+                   stride=2, padding=1)
             hs.append(h)
-    h = _res(h, ea, W, "mid.res1", g)
+    h = _res(h, ea, W, "mid.res1", g, cv)
     if cfg.attn:
-        h = _attn(h, W, "mid.attn", g)
-    h = _res(h, ea, W, "mid.res2", g)
+        h = _attn(h, W, "mid.attn", g, cv)
+    h = _res(h, ea, W, "mid.res2", g, cv)
     for i in reversed(range(nl)):
         for r in range(cfg.num_res + 1):
-            h = _res(torch.cat([h, hs.pop()], dim=1), ea, W, f"up.{i}.res.{r}", g)
+            h = _res(torch.cat([h, hs.pop()], dim=1), ea, W, f"up.{i}.res.{r}", g, cv)
         if i != 0:
             h = F.interpolate(h, scale_factor=2, mode="nearest")
-            h = F.conv2d(h, W[f"up.{i}.upsample.weight"], W[f"up.{i}.upsample.bias"], padding=1)
+            h = cv(h, W[f"up.{i}.upsample.weight"], W[f"up.{i}.upsample.bias"], padding=1)
     h = _gn_silu(h, W, "norm_out", g)
-    out = F.conv2d(h, W["conv_out.weight"], W["conv_out.bias"], padding=1).reshape(B, -1)
+    out = cv(h, W["conv_out.weight"], W["conv_out.bias"], padding=1).reshape(B, -1)
     return (out, emb) if return_emb else out
 
 

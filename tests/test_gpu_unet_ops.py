@@ -1,0 +1,105 @@
+"""The U-Net's operators one by one (SURVEY.md 8a' operator rows) against
+torch on the CPU with identical inputs: 3x3 conv (stride 1 / stride-2
+Downsample / nearest-x2 Upsample), 1x1 conv, the GroupNorm(+SiLU) prologue,
+skip concatenation, bias/embedding/residual epilogue, GroupNorm statistics,
+single-head attention.  fp32: <= 1e-5 rel-L2.  bf16 operands: against torch
+with the same bf16 rounding of the activated input and the weights, fp32
+accumulation: <= 1e-4 rel-L2 (products are exact; only the summation order and
+the ulp of the fused SiLU differ)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ertdiff.unet import attention, conv2d, group_norm_stats
+from oracle import ref_numpy as RN
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).float()
+
+
+def _ref_conv(x, w, b, mode, act, gn, bf16):
+    if act != "none":
+        x = x * gn[..., 0][:, :, None, None] + gn[..., 1][:, :, None, None]
+        if act == "gn_silu":
+            x = F.silu(x)
+    if bf16:
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    ks = w.shape[-1]
+    if mode == "up":
+        x = F.interpolate(x, scale_factor=2, mode="nearest")
+    return F.conv2d(x, w, b, stride=2 if mode == "down" else 1, padding=ks // 2)
+
+
+CASES = [  # (Ca, Cb, Cout, H, ks, mode, act)
+    (64, 0, 64, 64, 3, "same", "gn_silu"),
+    (128, 64, 128, 32, 3, "same", "gn_silu"),    # skip concatenation read in place
+    (256, 256, 256, 16, 3, "same", "gn_silu"),
+    (64, 0, 64, 64, 3, "down", "none"),
+    (128, 0, 128, 32, 3, "down", "none"),
+    (128, 0, 128, 32, 3, "up", "none"),
+    (256, 0, 256, 16, 3, "up", "none"),
+    (192, 0, 64, 64, 1, "same", "none"),
+    (384, 128, 256, 16, 1, "same", "none"),
+    (256, 0, 768, 16, 1, "same", "gn"),          # attention qkv
+    (1, 0, 64, 64, 3, "same", "none"),           # conv_in (Cin 1)
+    (64, 0, 1, 64, 3, "same", "gn_silu"),        # conv_out (Cout 1)
+]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("Ca,Cb,Cout,H,ks,mode,act", CASES)
+def test_conv2d(Ca, Cb, Cout, H, ks, mode, act, precision, cuda_dev):
+    B = 2
+    x = _rand((B, Ca, H, H), 1)
+    x2 = _rand((B, Cb, H, H), 2) if Cb else None
+    w = _rand((Cout, Ca + Cb, ks, ks), 3, 1.0 / np.sqrt((Ca + Cb) * ks * ks))
+    b = _rand((Cout,), 4, 0.1)
+    gn = None
+    if act != "none":
+        gn = torch.stack([_rand((B, Ca + Cb), 5, 0.3) + 1.0, _rand((B, Ca + Cb), 6, 0.2)], -1)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), mode=mode, act=act,
+                 gn=None if gn is None else gn.to(cuda_dev),
+                 x2=None if x2 is None else x2.to(cuda_dev), precision=precision).cpu()
+    xin = x if x2 is None else torch.cat([x, x2], 1)
+    ref = _ref_conv(xin, w, b, mode, act, gn, precision == "bf16")
+    err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
+    assert err < (1e-4 if precision == "bf16" else 1e-5), err
+
+
+def test_conv2d_epilogue(cuda_dev):
+    B, C, H = 2, 128, 32
+    x, w, b = _rand((B, C, H, H), 7), _rand((C, C, 3, 3), 8, 0.03), _rand((C,), 9)
+    eb, res = _rand((B, C), 10), _rand((B, C, H, H), 11)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), ebias=eb.to(cuda_dev),
+                 res=res.to(cuda_dev)).cpu()
+    ref = F.conv2d(x, w, b, padding=1) + eb[:, :, None, None] + res
+    assert RN.rel_l2(out.double().numpy(), ref.double().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("Ca,Cb,H", [(64, 0, 64), (256, 128, 16), (128, 64, 32)])
+def test_group_norm_stats(Ca, Cb, H, cuda_dev):
+    B, G = 3, 32
+    x = _rand((B, Ca, H, H), 12, 2.0) + 0.5
+    x2 = _rand((B, Cb, H, H), 13) if Cb else None
+    gamma, beta = _rand((Ca + Cb,), 14) + 1, _rand((Ca + Cb,), 15)
+    ss = group_norm_stats(x.to(cuda_dev), G, gamma.to(cuda_dev), beta.to(cuda_dev),
+                          x2=None if x2 is None else x2.to(cuda_dev)).cpu()
+    xin = x if x2 is None else torch.cat([x, x2], 1)
+    y = xin * ss[..., 0][:, :, None, None] + ss[..., 1][:, :, None, None]
+    ref = F.group_norm(xin, G, gamma, beta, eps=1e-5)
+    assert RN.rel_l2(y.double().numpy(), ref.double().numpy()) < 1e-5
+
+
+def test_attention(cuda_dev):
+    B, C, N = 2, 256, 256
+    qkv = _rand((B, 3 * C, N), 16, 0.5)
+    out = attention(qkv.to(cuda_dev)).cpu()
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    a = torch.softmax(torch.einsum("bci,bcj->bij", q, k) / 16.0, dim=-1)
+    ref = torch.einsum("bij,bcj->bci", a, v)
+    assert RN.rel_l2(out.double().numpy(), ref.double().numpy()) < 1e-5

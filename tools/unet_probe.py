@@ -23,9 +23,10 @@ def main():
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--L", type=int, default=4693)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    m = ertdiff.ConditionalUNet.from_config(a.config, seed=0).to(dev).eval()
+    m = ertdiff.ConditionalUNet.from_config(a.config, seed=0, precision=a.precision).to(dev).eval()
     cond = torch.rand(a.B, 14, a.L, device=dev)
     x = torch.randn(a.B, m.param_dim, device=dev)
     t = torch.full((a.B,), 500, dtype=torch.long, device=dev)
@@ -51,7 +52,7 @@ def main():
     torch.cuda.synchronize()
     step = e0.elapsed_time(e1) / 1e3 / a.steps
     g = GFLOP.get(a.config, 0) * a.B
-    print(f"{a.config} B={a.B}: forward {fwd*1e3:.2f} ms ({g/fwd/1e3:.1f} TFLOP/s), "
+    print(f"{a.config} {a.precision} B={a.B}: forward {fwd*1e3:.2f} ms ({g/fwd/1e3:.1f} TFLOP/s), "
           f"sampler step {step*1e3:.2f} ms ({g/step/1e3:.1f} TFLOP/s) -> {1/step:.1f} steps/s",
           flush=True)
 
