@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--unet", choices=["U1", "U2", "U3", "U5"], default="U2",
                     help="headline network (U2 = BASELINE configs[1])")
     ap.add_argument("--cpu-unet-seconds", type=float, default=10.0)
+    ap.add_argument("--no-u3", action="store_true",
+                    help="skip the configs[2] measurement (U3: + mid attention, B=256, bf16)")
     ap.add_argument("--no-reference", action="store_true",
                     help="skip the reference-model (R2) measurement in extra")
     ap.add_argument("--ref-steps", type=int, default=2000)
@@ -423,6 +425,49 @@ def cpu_unet_baseline(name, seconds, B, T):
             "seconds": round(el, 2)}
 
 
+def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev):
+    """A further BASELINE config (not the headline): same timing discipline,
+    reported under extra.  Weak scaling over member shards like the headline."""
+    from ertdiff.unet import CONFIGS, unet_flops
+    fl = unet_flops(**CONFIGS[name])
+    model = ertdiff.ConditionalUNet.from_config(name, seed=0, precision=precision).to(dev).eval()
+    g = torch.Generator(device=dev).manual_seed(1043)
+    cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
+    if world > 1:
+        dist.broadcast(cond, src=0)
+    sched = ertdiff.get_diffusion_schedule(T, device=dev)
+    offset = rank * B
+    x_T = ertdiff.philox_normal(B, model.param_dim, T, 1, 2043, offset, dev)
+    timed = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=steps,
+                                    seed=2043, member_offset=offset)
+    warm = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=max(1, warmup),
+                                   seed=2043, member_offset=offset)
+    warm.x.copy_(x_T)
+    warm.launch()
+    timed.x.copy_(x_T)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    t0 = time.perf_counter()
+    timed.launch(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    if not torch.isfinite(timed.x).all():
+        raise RuntimeError(f"{name} sampler produced non-finite values")
+    step_s = el / steps
+    conv_tf = fl["conv"] * B / step_s / 1e12
+    peak = PEAK_FP32_TFLOPS if precision == "fp32" else PEAK_BF16_TFLOPS
+    return {"config": f"{name} B={B} {precision} T={T}", "value": round(world * steps / el, 3),
+            "unit": "denoising-steps/sec", "ms_per_step": round(step_s * 1e3, 4),
+            "conv_tflops": round(conv_tf, 2), "conv_peak_tflops": peak,
+            "conv_frac": round(conv_tf / peak, 4), "steps": steps, "warmup": warmup,
+            "member_steps_per_s": round(world * steps / el * B, 1)}
+
+
 def main():
     a = parse()
     rank, world, dev = setup_dist()
@@ -486,6 +531,8 @@ def main():
         cpu = cpu_unet_baseline(a.unet, a.cpu_unet_seconds, B, T)
         extra["vs_cpu_baseline"] = round(value / cpu["value"], 1)
     del timed, warm
+    if not a.no_u3:
+        extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev)
     if not a.no_reference:
         extra["reference_model"] = bench_reference(a, rank, world, dev)
     if rank == 0:

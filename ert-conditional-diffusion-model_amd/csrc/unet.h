@@ -44,6 +44,9 @@ hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B,
 size_t conv_packed_floats_bf16(int cin, int cout, int ks);
 hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, float* dst,
                                  hipStream_t s);
+// Cout = 1, 3x3 stride 1 (conv_out; unet_conv_out.hip): per-pixel fp32 fma
+// chains, weights read from either packing (bf16: staged input rounded too)
+hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStream_t s);
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s);

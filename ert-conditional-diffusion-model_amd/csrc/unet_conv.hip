@@ -84,7 +84,10 @@ struct ConvGeom {
   static_assert(WB % 256 == 0, "weight slice must be whole DMA instructions");
 };
 
-template <int KS, int MODE, int ACT, int WCO, int WO, int TPX>
+// STG = input staging schedule: 0 = rows loaded one chunk ahead, LDS stores
+// interleaved into the second 3/4 of the chunk's MFMAs; 1 = rows loaded two
+// chunks ahead, stored at the top of the chunk.
+template <int KS, int MODE, int ACT, int WCO, int WO, int TPX, int STG>
 __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   using G = ConvGeom<KS, MODE, WCO, WO, TPX>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -218,15 +221,28 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   if constexpr (ACT != ACT_NONE) __syncthreads();  // gtab visible to store_chunk
   load_chunk(0);
   store_chunk(0, xim);
+  if constexpr (STG == 1) {
+    if (nchunk > 1) load_chunk(1);
+  }
   dma_wait();
   __syncthreads();
 
-  constexpr int H0 = G::SPC / 4;  // first step pair that carries staging work
+  constexpr int H0 = G::SPC / 4;  // STG 0: first step pair that carries staging work
   for (int k = 0; k < nchunk; ++k) {
     const int cur = k & 1;
     const float* xb = xim + cur * G::XB;
     const float* wb = wim + cur * G::WB;
-    if (k + 1 < nchunk) {
+    if constexpr (STG == 1) {
+      // input rows two chunks ahead: chunk k+1's registers were loaded during
+      // chunk k-1 and completed at its closing vmcnt(0), so the stores below
+      // never wait on memory; chunk k+2's loads and chunk k+1's weight DMA
+      // then have a whole chunk of MFMAs to land.
+      if (k + 1 < nchunk) {
+        store_chunk(k + 1, xim + (cur ^ 1) * G::XB);
+        if (k + 2 < nchunk) load_chunk(k + 2);
+        dma_weights(k + 1, wim + (cur ^ 1) * G::WB);
+      }
+    } else if (k + 1 < nchunk) {
       dma_weights(k + 1, wim + (cur ^ 1) * G::WB);
       load_chunk(k + 1);
     }
@@ -254,7 +270,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
       // the next chunk's staging work, spread over the second half of the
       // step pairs: its VALU issues in the gaps of this chunk's MFMAs
       // (a 32x32x2 f32 MFMA occupies the SIMD's matrix pipe for 64 cycles)
-      if (k + 1 < nchunk && sp >= H0) {
+      if (STG == 0 && k + 1 < nchunk && sp >= H0) {
 #pragma unroll
         for (int it = 0; it < G::NIT; ++it)
           if (H0 + it % (G::SPC / 2 - H0) == sp) store_elem(it, k + 1, xim + (cur ^ 1) * G::XB);
@@ -268,51 +284,75 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   // All loads of a 32-cout tile are issued before any of its stores: out and
   // res may not alias, but without the explicit phases hipcc must assume they
   // do and serialises every residual load behind the previous store.
-  constexpr size_t HWo = (size_t)WO * WO;
+  // Phases of 8 accumulator rows with 32-bit offsets from one per-lane base
+  // keep the epilogue's live registers below the main loop's.
+  constexpr int HWo = WO * WO;
   const int tile0 = tile_wg + wco * 2;
-  const float* __restrict__ resp = a.res;
-  float* __restrict__ outp = a.out;
+  const size_t lbase0 = (size_t)b * a.Cout * HWo + p0 + wpx * 32 * TPX + l32;
+  const float* __restrict__ resp = a.res ? a.res + lbase0 : nullptr;
+  float* __restrict__ outp = a.out + lbase0;
+  const float* ebp = a.ebias ? a.ebias + (size_t)b * a.eb_stride : nullptr;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    float bias[16], eb[16], rv[16][TPX];
-    size_t obase[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      co = co < a.Cout ? co : a.Cout - 1;
-      obase[r] = ((size_t)b * a.Cout + co) * HWo + p0 + wpx * 32 * TPX + l32;
-      bias[r] = a.bias[co];
-      eb[r] = a.ebias ? a.ebias[(size_t)b * a.eb_stride + co] : 0.f;
+    for (int ph = 0; ph < 2; ++ph) {
+      float bias[8], eb[8], rv[8][TPX];
+      int off[8];
 #pragma unroll
-      for (int j = 0; j < TPX; ++j) rv[r][j] = resp ? resp[obase[r] + j * 32] : 0.f;
-    }
+      for (int q = 0; q < 8; ++q) {
+        const int r = ph * 8 + q;
+        int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        co = co < a.Cout ? co : a.Cout - 1;
+        off[q] = co * HWo;
+        bias[q] = a.bias[co];
+        eb[q] = ebp ? ebp[co] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (co >= a.Cout) continue;
+        for (int j = 0; j < TPX; ++j) rv[q][j] = resp ? resp[off[q] + j * 32] : 0.f;
+      }
 #pragma unroll
-      for (int j = 0; j < TPX; ++j) {
-        // the oracle's op order: conv(+bias), then + emb, then + residual
-        float v = acc[i][j][r] + bias[r];
-        if (a.ebias) v = v + eb[r];
-        if (resp) v = v + rv[r][j];
-        outp[obase[r] + j * 32] = v;
+      for (int q = 0; q < 8; ++q) {
+        const int r = ph * 8 + q;
+        const int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= a.Cout) continue;
+#pragma unroll
+        for (int j = 0; j < TPX; ++j) {
+          // the oracle's op order: conv(+bias), then + emb, then + residual
+          float v = acc[i][j][r] + bias[q];
+          if (ebp) v = v + eb[q];
+          if (resp) v = v + rv[q][j];
+          outp[off[q] + j * 32] = v;
+        }
       }
     }
   }
 }
 
-template <int KS, int MODE, int ACT, int WCO, int WO, int TPX>
-static hipError_t launch_g(const ConvArgs& a, int B, hipStream_t s) {
+// ERTD_UNET_STAGE=0|1 picks the staging schedule (diagnostics); default 1
+static int conv_stage() {
+  static int v = [] {
+    const char* e = getenv("ERTD_UNET_STAGE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <int KS, int MODE, int ACT, int WCO, int WO, int TPX, int STG>
+static hipError_t launch_gs(const ConvArgs& a, int B, hipStream_t s) {
   using G = ConvGeom<KS, MODE, WCO, WO, TPX>;
   const size_t lds = G::LDS + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, WCO, WO, TPX>,
+    (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, WCO, WO, TPX, STG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((unsigned)(WO * WO / G::BM), (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
-  conv_kernel<KS, MODE, ACT, WCO, WO, TPX><<<grid, NTHR, lds, s>>>(a);
+  conv_kernel<KS, MODE, ACT, WCO, WO, TPX, STG><<<grid, NTHR, lds, s>>>(a);
   return hipGetLastError();
+}
+
+template <int KS, int MODE, int ACT, int WCO, int WO, int TPX>
+static hipError_t launch_g(const ConvArgs& a, int B, hipStream_t s) {
+  if (conv_stage() == 0) return launch_gs<KS, MODE, ACT, WCO, WO, TPX, 0>(a, B, s);
+  return launch_gs<KS, MODE, ACT, WCO, WO, TPX, 1>(a, B, s);
 }
 
 // Wave tile 64 co x 32*TPX px.  TPX = 1 (half the pixels per workgroup, twice
@@ -343,9 +383,18 @@ static hipError_t launch_w(const ConvArgs& a, int B, hipStream_t s) {
   }
 }
 
+// ERTD_UNET_WCO=1 forces 64-cout workgroups everywhere (diagnostics); 0 = automatic
+static int conv_wco_override() {
+  static int v = [] {
+    const char* e = getenv("ERTD_UNET_WCO");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int KS, int MODE, int ACT>
 static hipError_t launch_t(const ConvArgs& a, int B, hipStream_t s) {
-  if (a.Cout >= 128) return launch_w<KS, MODE, ACT, 2>(a, B, s);
+  if (a.Cout >= 128 && conv_wco_override() != 1) return launch_w<KS, MODE, ACT, 2>(a, B, s);
   return launch_w<KS, MODE, ACT, 1>(a, B, s);
 }
 
@@ -353,6 +402,8 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;
+  if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)
+    return launch_conv_out(act, a, B, false, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_t<3, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_t<3, MODE_S1, ACT_GN_SILU>(a, B, s);
   if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_t<3, MODE_S2, ACT_NONE>(a, B, s);

@@ -300,6 +300,8 @@ hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B,
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;
+  if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)
+    return launch_conv_out(act, a, B, true, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_hw<3, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_hw<3, MODE_S1, ACT_GN_SILU>(a, B, s);
   if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_hw<3, MODE_S2, ACT_NONE>(a, B, s);

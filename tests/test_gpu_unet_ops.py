@@ -48,6 +48,9 @@ CASES = [  # (Ca, Cb, Cout, H, ks, mode, act)
     (256, 0, 768, 16, 1, "same", "gn"),          # attention qkv
     (1, 0, 64, 64, 3, "same", "none"),           # conv_in (Cin 1)
     (64, 0, 1, 64, 3, "same", "gn_silu"),        # conv_out (Cout 1)
+    (32, 24, 1, 32, 3, "same", "gn_silu"),       # Cout 1, concat, partial 16-ch chunk
+    (20, 0, 1, 16, 3, "same", "none"),           # Cout 1, whole image in one workgroup
+    (128, 0, 1, 128, 3, "same", "gn_silu"),      # Cout 1 at U5's resolution
 ]
 
 
@@ -75,6 +78,17 @@ def test_conv2d_epilogue(cuda_dev):
     B, C, H = 2, 128, 32
     x, w, b = _rand((B, C, H, H), 7), _rand((C, C, 3, 3), 8, 0.03), _rand((C,), 9)
     eb, res = _rand((B, C), 10), _rand((B, C, H, H), 11)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), ebias=eb.to(cuda_dev),
+                 res=res.to(cuda_dev)).cpu()
+    ref = F.conv2d(x, w, b, padding=1) + eb[:, :, None, None] + res
+    assert RN.rel_l2(out.double().numpy(), ref.double().numpy()) < 1e-5
+
+
+def test_conv2d_out_epilogue(cuda_dev):
+    """Cout = 1 path (csrc/unet_conv_out.hip) with the embedding and residual adds."""
+    B, C, H = 3, 48, 32
+    x, w, b = _rand((B, C, H, H), 17), _rand((1, C, 3, 3), 18, 0.05), _rand((1,), 19)
+    eb, res = _rand((B, 1), 20), _rand((B, 1, H, H), 21)
     out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), ebias=eb.to(cuda_dev),
                  res=res.to(cuda_dev)).cpu()
     ref = F.conv2d(x, w, b, padding=1) + eb[:, :, None, None] + res
