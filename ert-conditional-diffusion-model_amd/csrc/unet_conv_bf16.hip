@@ -199,17 +199,20 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   load_chunk(0);
 #pragma unroll
   for (int it = 0; it < G::NIT; ++it) store_elem(it, 0, xim);
+  if (nchunk > 1) load_chunk(1);
   dma_wait();
   __syncthreads();
 
-  constexpr int H0 = G::SPC / 2;
+  // rows two chunks ahead, stored at the top of the chunk (unet_conv.hip STG 1)
   for (int k = 0; k < nchunk; ++k) {
     const int cur = k & 1;
     const char* xb = xim + cur * G::XB;
     const char* wb = wim + cur * G::WBB;
     if (k + 1 < nchunk) {
+#pragma unroll
+      for (int it = 0; it < G::NIT; ++it) store_elem(it, k + 1, xim + (cur ^ 1) * G::XB);
+      if (k + 2 < nchunk) load_chunk(k + 2);
       dma_weights(k + 1, wim + (cur ^ 1) * G::WBB);
-      load_chunk(k + 1);
     }
 #pragma unroll
     for (int s = 0; s < G::SPC; ++s) {
@@ -225,44 +228,46 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
         acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bv, acc[0][t], 0, 0, 0);
         acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bv, acc[1][t], 0, 0, 0);
       }
-      if (k + 1 < nchunk && s >= H0) {
-#pragma unroll
-        for (int it = 0; it < G::NIT; ++it)
-          if (H0 + it % (G::SPC - H0) == s) store_elem(it, k + 1, xim + (cur ^ 1) * G::XB);
-      }
     }
     dma_wait();
     __syncthreads();
   }
 
-  // ---- epilogue (as unet_conv.hip): loads of a tile before its stores
-  constexpr size_t HWo = (size_t)WO * WO;
-  const float* __restrict__ resp = a.res;
-  float* __restrict__ outp = a.out;
+  // ---- epilogue (as unet_conv.hip): 8-row phases, loads before stores
+  constexpr int HWo = WO * WO;
+  const size_t lbase0 = (size_t)b * a.Cout * HWo + p0 + wave * 32 * TPX + l32;
+  const float* __restrict__ resp = a.res ? a.res + lbase0 : nullptr;
+  float* __restrict__ outp = a.out + lbase0;
+  const float* ebp = a.ebias ? a.ebias + (size_t)b * a.eb_stride : nullptr;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    float bias[16], eb[16], rv[16][TPX];
-    size_t obase[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      int co = (tile_wg + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      co = co < a.Cout ? co : a.Cout - 1;
-      obase[r] = ((size_t)b * a.Cout + co) * HWo + p0 + wave * 32 * TPX + l32;
-      bias[r] = a.bias[co];
-      eb[r] = a.ebias ? a.ebias[(size_t)b * a.eb_stride + co] : 0.f;
+    for (int ph = 0; ph < 2; ++ph) {
+      float bias[8], eb[8], rv[8][TPX];
+      int off[8];
 #pragma unroll
-      for (int t = 0; t < TPX; ++t) rv[r][t] = resp ? resp[obase[r] + t * 32] : 0.f;
-    }
+      for (int q = 0; q < 8; ++q) {
+        const int r = ph * 8 + q;
+        int co = (tile_wg + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        co = co < a.Cout ? co : a.Cout - 1;
+        off[q] = co * HWo;
+        bias[q] = a.bias[co];
+        eb[q] = ebp ? ebp[co] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = (tile_wg + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (co >= a.Cout) continue;
+        for (int t = 0; t < TPX; ++t) rv[q][t] = resp ? resp[off[q] + t * 32] : 0.f;
+      }
 #pragma unroll
-      for (int t = 0; t < TPX; ++t) {
-        float v = acc[i][t][r] + bias[r];
-        if (a.ebias) v = v + eb[r];
-        if (resp) v = v + rv[r][t];
-        outp[obase[r] + t * 32] = v;
+      for (int q = 0; q < 8; ++q) {
+        const int r = ph * 8 + q;
+        const int co = (tile_wg + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= a.Cout) continue;
+#pragma unroll
+        for (int t = 0; t < TPX; ++t) {
+          float v = acc[i][t][r] + bias[q];
+          if (ebp) v = v + eb[q];
+          if (resp) v = v + rv[q][t];
+          outp[off[q] + t * 32] = v;
+        }
       }
     }
   }
@@ -281,10 +286,18 @@ static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int KS, int MODE, int ACT>
-static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
-  // TPX = 2 (256-pixel tiles) except stride 2 / 1x1 (staging registers)
-  constexpr int TP = (MODE == MODE_S2 || KS == 1) ? 1 : 2;
+// ERTD_UNET_BF16_TPX=1 forces 128-pixel tiles for the 3x3 stride-1/upsample
+// convs (diagnostics); 0 = automatic
+static int convh_tpx_override() {
+  static int v = [] {
+    const char* e = getenv("ERTD_UNET_BF16_TPX");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int KS, int MODE, int ACT, int TP>
+static hipError_t launch_hwt(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
     case 16: return launch_hg<KS, MODE, ACT, 16, TP>(a, B, s);
     case 32: return launch_hg<KS, MODE, ACT, 32, TP>(a, B, s);
@@ -293,6 +306,17 @@ static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
       if constexpr (MODE != MODE_S2) return launch_hg<KS, MODE, ACT, 128, TP>(a, B, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
+  }
+}
+
+template <int KS, int MODE, int ACT>
+static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
+  // TPX = 2 (256-pixel tiles) except stride 2 / 1x1 (staging registers)
+  if constexpr (MODE == MODE_S2 || KS == 1) {
+    return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
+  } else {
+    if (convh_tpx_override() == 1) return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
+    return launch_hwt<KS, MODE, ACT, 2>(a, B, s);
   }
 }
 

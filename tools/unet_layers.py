@@ -57,7 +57,7 @@ def walk():
 
 
 layers = walk()
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_kernel<" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_kernel<" in r["Kernel_Name"] or "conv_out_kernel<" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 last = rows[-len(layers):]
 tot_t = tot_f = 0
