@@ -15,6 +15,7 @@ from .train import DiffusionForwardFn, train_step, validation_loss
 from .ensemble import member_range, sample_ensemble
 from .postproc import compact, postprocess, sample_realisations
 from .unet import ConditionalUNet, UNetSamplerPlan, sample_unet
+from .kde import ensemble_mode, kde_mode, mode_kde_calculation
 
 __all__ = [
     "ConditionalDiffusionModel", "get_timestep_embedding", "get_diffusion_schedule", "q_sample",
@@ -23,5 +24,6 @@ __all__ = [
     "DiffusionDataset", "check_param_bounds", "bounds_mask", "load_best_model",
     "save_checkpoint", "STATE_KEYS", "train_step", "validation_loss", "DiffusionForwardFn",
     "sample_ensemble", "member_range", "postprocess", "sample_realisations", "compact",
-    "ConditionalUNet", "UNetSamplerPlan", "sample_unet",
+    "ConditionalUNet", "UNetSamplerPlan", "sample_unet", "kde_mode", "ensemble_mode",
+    "mode_kde_calculation",
 ]

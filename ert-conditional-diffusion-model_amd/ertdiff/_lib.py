@@ -93,6 +93,9 @@ SIGNATURES = {
     "ertd_unet_plan_destroy": (_I, [_VP]),
     "ertd_plan_launch": (_I, [_VP, _VP]),
     "ertd_plan_destroy": (_I, [_VP]),
+    "ertd_kde_mode": (_I, [_VP, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _I, ctypes.c_double,
+                           ctypes.c_double, _VP, _VP, _VP, _VP, _VP]),
+    "ertd_minmax_f64": (_I, [_VP, ctypes.c_longlong, _VP, _VP, _VP]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

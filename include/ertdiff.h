@@ -298,6 +298,26 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* cfg, const float* packe
 int ertd_unet_plan_launch(ertd_unet_plan* plan, void* stream);
 int ertd_unet_plan_destroy(ertd_unet_plan* plan);
 
+/* ---- Ensemble KDE mode (csrc/kde.hip) -------------
+ * Replaces the reference's per-cell loop ERT_Conditional_Diffusion.py:747-762
+ * (scipy.stats.gaussian_kde per cell of sim_data, evaluated on
+ * np.linspace(lo, hi, grid), mode = grid point of the first maximum) and
+ * mode_kde_calculation :166-181 (one array, its own range, 1000 points).
+ * x: (n, ld) float64 row-major on the device, cell c = column c < cells.
+ * range_mode 0: grid over [lo, hi]; 1: each cell's own [min, max];
+ * 2: [lo, hi] read from range_dev (2 doubles, e.g. ertd_minmax_f64's output).
+ * mode (cells) receives the mode; index (cells, optional) the grid index, -1
+ * where the cell's variance is 0 (gaussian_kde raises there); density
+ * (cells, optional) the KDE value at the mode.  Requires 2 <= n <= 20480.   */
+int ertd_kde_mode(const double* x, int n, long long cells, long long ld, int grid, int range_mode,
+                  double lo, double hi, const double* range_dev, double* mode, int* index,
+                  double* density, void* stream);
+
+/* min and max of count float64 values: out2 = {min, max} (device);
+ * work: 2 * ERTD_MINMAX_BLOCKS doubles of device scratch.                  */
+#define ERTD_MINMAX_BLOCKS 1024
+int ertd_minmax_f64(const double* x, long long count, double* work, double* out2, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,3 +71,8 @@ def gpu_model(golden_weights, cuda_dev):
     m = ertdiff.ConditionalDiffusionModel(29, 128)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in golden_weights.items()})
     return m.to(cuda_dev).eval()
+
+
+@pytest.fixture(scope="session")
+def kde_kat():
+    return load_golden("kde_kat.npz")

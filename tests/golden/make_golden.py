@@ -270,7 +270,43 @@ def gen_postproc_chain(ref, ref_dir, out_dir):
                         n_valid=n_valid)
 
 
-GENERATORS = ("forward", "schedule", "sampler", "train", "postproc", "postproc_chain")
+def kde_ensemble(n=40, cells=48):
+    """Synthetic ensemble (n, cells): per-cell location/scale spread over a
+    wide global range, every 4th cell bimodal, every 6th log-normal (skewed)."""
+    z = synth_normal((n, cells), 81).astype(np.float64)
+    u = synth_uniform((3, cells), 82).astype(np.float64)
+    loc = 40.0 * u[0] - 20.0
+    scale = 0.05 + 3.0 * u[1]
+    x = loc + scale * z
+    for c in range(0, cells, 4):
+        x[: n // 2, c] += 6.0 * scale[c]
+    for c in range(1, cells, 6):
+        x[:, c] = loc[c] + np.exp(0.8 * z[:, c])
+    return x
+
+
+def gen_kde(ref, out_dir):
+    """KDE mode (:166-181 mode_kde_calculation, called as the reference defines
+    it; :747-762 the ensemble-mode loop, restated around scipy's
+    gaussian_kde, the reference's dependency -- scipy 1.15.3 here)."""
+    from scipy import stats
+    ref["stats"] = stats          # the reference's `from scipy import stats` (its import cell)
+    x = kde_ensemble()
+    grid = 5000
+    x_range = np.linspace(np.min(x), np.max(x), grid)
+    idx = np.array([int(np.argmax(stats.gaussian_kde(x[:, c])(x_range))) for c in range(x.shape[1])])
+    arrays = x[:, :8].T.copy()
+    modes = np.array([ref["mode_kde_calculation"](a) for a in arrays], dtype=np.float64)
+    arr_idx = np.array([int(np.argmin(np.abs(np.linspace(a.min(), a.max(), 1000) - m)))
+                        for a, m in zip(arrays, modes)])
+    for a, m, k in zip(arrays, modes, arr_idx):
+        assert np.linspace(a.min(), a.max(), 1000)[k] == m
+    np.savez_compressed(os.path.join(out_dir, "kde_kat.npz"), x=x, grid=grid,
+                        lo=np.min(x), hi=np.max(x), idx_global=idx, mode_global=x_range[idx],
+                        arrays=arrays, mode_arrays=modes, idx_arrays=arr_idx)
+
+
+GENERATORS = ("forward", "schedule", "sampler", "train", "postproc", "postproc_chain", "kde")
 
 
 def main():
@@ -293,6 +329,8 @@ def main():
         gen_postproc(ref, args.ref, args.out)
     if "postproc_chain" in args.only:
         gen_postproc_chain(ref, args.ref, args.out)
+    if "kde" in args.only:
+        gen_kde(ref, args.out)
     for f in sorted(os.listdir(args.out)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(args.out, f)))
