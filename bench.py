@@ -73,6 +73,7 @@ def parse():
     ap.add_argument("--cpu-unet-seconds", type=float, default=10.0)
     ap.add_argument("--no-u3", action="store_true",
                     help="skip the configs[2] measurement (U3: + mid attention, B=256, bf16)")
+    ap.add_argument("--no-kde", action="store_true", help="skip the KDE-mode measurement")
     ap.add_argument("--no-reference", action="store_true",
                     help="skip the reference-model (R2) measurement in extra")
     ap.add_argument("--ref-steps", type=int, default=2000)
@@ -468,6 +469,50 @@ def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev):
             "member_steps_per_s": round(world * steps / el * B, 1)}
 
 
+def bench_kde(dev, world, rank, n=100, cells=4693 * 14, grid=5000, reps=3, cpu_cells=300,
+              cpu=True):
+    """the ensemble-mode reduction (:747-762) at the
+    reference's shape -- 65,702 cells (4693 x 14), n realisations, 5000-point
+    grid over the global range -- timed with HIP events; CPU baseline = the
+    reference's scipy loop on a bounded sample of cells."""
+    g = torch.Generator(device=dev).manual_seed(7)
+    loc = torch.rand(cells, generator=g, device=dev, dtype=torch.float64) * 40 - 20
+    sc = torch.rand(cells, generator=g, device=dev, dtype=torch.float64) * 2 + 0.05
+    x = loc + sc * torch.randn(n, cells, generator=g, device=dev, dtype=torch.float64)
+    ertdiff.kde_mode(x, grid=grid)                      # warm
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ertdiff.kde_mode(x, grid=grid, raise_singular=False)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    out = {"workload": f"ensemble mode: {cells} cells x n={n} realisations, {grid}-point grid "
+                       "(global range), float64", "ms": round(ms, 3),
+           "cells_per_s": round(cells / (ms * 1e-3), 1),
+           "pair_evals_per_s": round(n * grid * cells / (ms * 1e-3), 1),
+           "timing": f"HIP events around {reps} calls (min/max pre-pass + kde_mode_kernel)"}
+    if cpu and rank == 0:
+        import numpy as np
+        xc = x[:, :cpu_cells].cpu().numpy()
+        lo, hi = float(x.min()), float(x.max())
+        from scipy import stats
+        x_range = np.linspace(lo, hi, grid)
+        t0 = time.perf_counter()
+        for c in range(cpu_cells):                       # the reference loop body
+            int(np.argmax(stats.gaussian_kde(xc[:, c])(x_range)))
+        el = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(cpu_cells / el, 2), "unit": "cells/s", "cores": 1,
+                               "kind": "reference",
+                               "sample": f"{cpu_cells} cells of the same ensemble through the "
+                                         "reference loop body (scipy.stats.gaussian_kde + argmax), "
+                                         "1 thread", "seconds": round(el, 2)}
+        out["vs_cpu_baseline"] = round(out["cells_per_s"] / out["cpu_baseline"]["value"], 1)
+    return out
+
+
 def main():
     a = parse()
     rank, world, dev = setup_dist()
@@ -533,6 +578,8 @@ def main():
     del timed, warm
     if not a.no_u3:
         extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev)
+    if not a.no_kde:
+        extra["kde_mode"] = bench_kde(dev, world, rank, cpu=not a.no_cpu_baseline)
     if not a.no_reference:
         extra["reference_model"] = bench_reference(a, rank, world, dev)
     if rank == 0:

@@ -4,7 +4,7 @@
 # Writes gpurun_out/kernel_traffic.json; copy it to profiles/ (read by bench.py).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out profiles; export TMPDIR=/tmp
-ARGS="--steps 20 --warmup 5 --ref-steps 1000 --ref-warmup 0 --no-cpu-baseline --no-hoisted --no-train --no-steps-schedule --roofline-reps 20 --no-u3 ${BENCH_ARGS:-}"
+ARGS="--steps 20 --warmup 5 --ref-steps 1000 --ref-warmup 0 --no-cpu-baseline --no-hoisted --no-train --no-steps-schedule --roofline-reps 20 --no-u3 --no-kde ${BENCH_ARGS:-}"
 for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf gpurun_out/pmc_$c
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_$c -o run \
