@@ -78,7 +78,11 @@ __global__ __launch_bounds__(NTHR) void conv_out_kernel(ConvArgs a) {
   float acc = 0.f;
   for (int c0 = 0; c0 < Cin; c0 += OCC) {
     __syncthreads();  // tables visible / previous chunk consumed
-    for (int e = tid; e < OCC * G::IR * WO; e += NTHR) {
+    constexpr int NE = (OCC * G::IR * WO + NTHR - 1) / NTHR;   // staged elements per thread
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const int e = tid + k * NTHR;
+      if (OCC * G::IR * WO % NTHR != 0 && e >= OCC * G::IR * WO) break;
       const int c = e / (G::IR * WO), rem = e - c * (G::IR * WO);
       const int r = rem / WO, x = rem - r * WO;
       const int cg = c0 + c, iy = oy0 - 1 + r;

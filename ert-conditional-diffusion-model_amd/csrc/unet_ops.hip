@@ -22,15 +22,31 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(GnArgs a) {
   const int cpg = C / a.groups;
   const int HW = a.HW;
   double s = 0.0, ss = 0.0;
-  for (int cl = 0; cl < cpg; ++cl) {
-    const int c = g * cpg + cl;
-    const float* src = c < a.Ca ? a.srcA + ((size_t)b * a.Ca + c) * HW
-                                : a.srcB + ((size_t)b * a.Cb + (c - a.Ca)) * HW;
+  auto acc4 = [&](const float4 v) {
+    s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+    ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  };
+  const int c0 = g * cpg;
+  if (c0 + cpg <= a.Ca || c0 >= a.Ca) {
+    // the group's channels are one contiguous run of cpg*HW floats: one flat
+    // loop keeps every thread busy (cpg*HW/4 float4s), 4 loads in flight
+    const float* src = c0 < a.Ca ? a.srcA + ((size_t)b * a.Ca + c0) * HW
+                                 : a.srcB + ((size_t)b * a.Cb + (c0 - a.Ca)) * HW;
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    for (int i = tid; i < HW / 4; i += 256) {
-      const float4 v = s4[i];
-      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
-      ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    const int n4 = cpg * HW / 4;
+    int i = tid;
+    for (; i + 3 * 256 < n4; i += 4 * 256) {
+      const float4 v0 = s4[i], v1 = s4[i + 256], v2 = s4[i + 512], v3 = s4[i + 768];
+      acc4(v0); acc4(v1); acc4(v2); acc4(v3);
+    }
+    for (; i < n4; i += 256) acc4(s4[i]);
+  } else {
+    for (int cl = 0; cl < cpg; ++cl) {   // a group split by the skip concatenation
+      const int c = c0 + cl;
+      const float* src = c < a.Ca ? a.srcA + ((size_t)b * a.Ca + c) * HW
+                                  : a.srcB + ((size_t)b * a.Cb + (c - a.Ca)) * HW;
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      for (int i = tid; i < HW / 4; i += 256) acc4(s4[i]);
     }
   }
 #pragma unroll
