@@ -35,6 +35,8 @@ struct ConvArgs {
   int Cin, Cout;
   int Hs, Ws;            // source spatial size
   int Ho, Wo;            // output spatial size
+  void* bimg;            // bf16 3x3 GN / Upsample convs: scratch for the pre-transformed
+                         // input, conv_bf16_image_bytes(Cin, B, Ho, Wo) bytes (null: stage fp32)
 };
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
@@ -42,6 +44,7 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
 // launch_pack_conv_bf16
 hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
 size_t conv_packed_floats_bf16(int cin, int cout, int ks);
+size_t conv_bf16_image_bytes(int cin, int B, int H, int W);
 hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, float* dst,
                                  hipStream_t s);
 // Cout = 1, 3x3 stride 1 (conv_out; unet_conv_out.hip): per-pixel fp32 fma

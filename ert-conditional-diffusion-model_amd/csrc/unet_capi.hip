@@ -216,6 +216,11 @@ struct Walk {
     if (mode == MODE_S2) { Ho = Hs / 2; Wo = Ws / 2; }
     if (mode == MODE_UP) { Ho = Hs * 2; Wo = Ws * 2; }
     if (!out) out = alloc((size_t)B * Cout * Ho * Wo);
+    // bf16 stride-1 convs stage a pre-transformed bf16 copy of their input
+    float* bimg = nullptr;
+    if (c->precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
+        ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
+      bimg = alloc((conv_bf16_image_bytes(Ca + Cb, B, Ho, Wo) + 3) / 4);
     if (dry) return out;
     if (Cin != Ca + Cb) {
       chk(hipErrorInvalidValue);
@@ -230,6 +235,7 @@ struct Walk {
     a.res = res; a.out = out;
     a.Cin = Cin; a.Cout = Cout;
     a.Hs = Hs; a.Ws = Ws; a.Ho = Ho; a.Wo = Wo;
+    a.bimg = bimg;
     chk(c->precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
                                        : launch_conv(ks, mode, act, a, B, s));
     return out;
@@ -536,8 +542,17 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   a.Cin = Cin; a.Cout = Cout; a.Hs = H; a.Ws = H;
   a.Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   a.Wo = a.Ho;
+  void* bimg = nullptr;
+  if (precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
+      ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE))) {
+    // stream-ordered scratch for the pre-transformed input (freed on the stream)
+    e = hipMallocAsync(&bimg, conv_bf16_image_bytes(Cin, B, a.Ho, a.Wo), s);
+    if (e != hipSuccess) return rcode(e);
+    a.bimg = bimg;
+  }
   e = precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
                                   : launch_conv(ks, mode, act, a, B, s);
+  if (bimg) (void)hipFreeAsync(bimg, s);
   return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
 }
 

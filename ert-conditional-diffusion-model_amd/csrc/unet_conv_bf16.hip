@@ -59,7 +59,11 @@ struct GeomH {
   static_assert(XB % 16 == 0 && TWB % 1024 == 0, "alignment");
 };
 
-template <int KS, int MODE, int ACT, int WO, int TPX>
+// PRE: the input was already transformed (GN/SiLU, bf16 RNE, channel padding)
+// by act_bf16_kernel into a.bimg = [B][ceil(Cin/16)][H][W][16] bf16 -- the LDS
+// image layout row by row -- so staging is LDS-DMA of whole rows (stride-1
+// convs only): no staging VALU in the conv at all.
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE>
 __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   using G = GeomH<KS, MODE, WO, TPX>;
   extern __shared__ __attribute__((aligned(16))) char smemh[];
@@ -83,8 +87,14 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   if constexpr (ACT != ACT_NONE) {
     for (int c = tid; c < Cin; c += NTHR) gtab[c] = a.gn[(size_t)b * Cin + c];
   }
+  if constexpr (PRE) {
+    // every LDS image byte starts at zero: halo columns and out-of-image rows
+    // are never written by the row DMA
+    for (int i = tid; i < 2 * G::XB / 16; i += NTHR)
+      reinterpret_cast<u32x4*>(xim)[i] = u32x4{0u, 0u, 0u, 0u};
+  }
   // zero halo pixels (cols 0 and IP-1) of every row, group, buffer
-  for (int r = tid; r < 2 * G::NG * G::IR * 2; r += NTHR) {
+  for (int r = tid; !PRE && r < 2 * G::NG * G::IR * 2; r += NTHR) {
     const int side = r & 1, rest = r >> 1;
     const int buf = rest / (G::NG * G::IR), rem = rest - buf * (G::NG * G::IR);
     const int g = rem / G::IR, rr = rem - g * G::IR;
@@ -175,6 +185,33 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   };
   auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
+  // PRE: chunk k's rows of the pre-transformed image -> img (LDS-DMA, 16 B per
+  // lane, one instruction per 1 KB of a row; a 16-pixel row is half a wave)
+  constexpr int RB = G::WST * 32;                          // bytes per image row
+  constexpr int IPR = RB >= 1024 ? RB / 1024 : 1;          // DMA instructions per row
+  const int G16 = (Cin + 15) / 16;
+  auto dma_rows = [&](int k, char* img) {
+    for (int q = wave; q < G::NG * G::IR * IPR; q += 4) {  // wave-uniform
+      const int g = q / (G::IR * IPR), rr = q - g * (G::IR * IPR);
+      const int r = rr / IPR, part = rr - r * IPR;
+      const int iy = row0 + r;
+      const int gg = k * G::NG + g;
+      if (iy < 0 || iy >= HST || gg >= G16) continue;
+      if (RB < 1024 && lane >= RB / 16) continue;
+      const char* src = reinterpret_cast<const char*>(a.bimg) +
+                        (((size_t)b * G16 + gg) * HST + iy) * RB + part * 1024 + lane * 16;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(
+          lds_addr_h(img + g * G::GB + (r * G::IP + 1) * 32 + part * 1024));
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(src), "s"(dst)
+          : "memory");
+    }
+  };
+
   int lbase[TPX];
 #pragma unroll
   for (int t = 0; t < TPX; ++t) {
@@ -194,12 +231,18 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
 #pragma unroll
     for (int t = 0; t < TPX; ++t) acc[i][t] = f32x16{};
 
-  dma_weights(0, wim);
-  if constexpr (ACT != ACT_NONE) __syncthreads();
-  load_chunk(0);
+  if constexpr (PRE) {
+    __syncthreads();                     // zeroed images before any DMA lands
+    dma_weights(0, wim);
+    dma_rows(0, xim);
+  } else {
+    dma_weights(0, wim);
+    if constexpr (ACT != ACT_NONE) __syncthreads();
+    load_chunk(0);
 #pragma unroll
-  for (int it = 0; it < G::NIT; ++it) store_elem(it, 0, xim);
-  if (nchunk > 1) load_chunk(1);
+    for (int it = 0; it < G::NIT; ++it) store_elem(it, 0, xim);
+    if (nchunk > 1) load_chunk(1);
+  }
   dma_wait();
   __syncthreads();
 
@@ -209,9 +252,13 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
     const char* xb = xim + cur * G::XB;
     const char* wb = wim + cur * G::WBB;
     if (k + 1 < nchunk) {
+      if constexpr (PRE) {
+        dma_rows(k + 1, xim + (cur ^ 1) * G::XB);
+      } else {
 #pragma unroll
-      for (int it = 0; it < G::NIT; ++it) store_elem(it, k + 1, xim + (cur ^ 1) * G::XB);
-      if (k + 2 < nchunk) load_chunk(k + 2);
+        for (int it = 0; it < G::NIT; ++it) store_elem(it, k + 1, xim + (cur ^ 1) * G::XB);
+        if (k + 2 < nchunk) load_chunk(k + 2);
+      }
       dma_weights(k + 1, wim + (cur ^ 1) * G::WBB);
     }
 #pragma unroll
@@ -273,17 +320,105 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   }
 }
 
-template <int KS, int MODE, int ACT, int WO, int TPX>
+// The input transform of the PRE path: x (srcA | srcB, fp32 NCHW) -> GN/SiLU
+// (ATen's folded x*scale+shift, x*rcp(1+exp(-x))) -> bf16 RNE, written as
+// [B][ceil(Cin/16)][H][W][16] with zero padding channels.  One thread per
+// (sample, 16-channel group, pixel): 16 coalesced channel-plane loads, one
+// 32-B store.  Applied once per activation instead of once per output-channel
+// tile and halo row of every conv workgroup.
+// UPS: nearest x2 upsample folded in (output pixel (y, x) reads source
+// (y/2, x/2)), so an Upsample conv becomes a stride-1 conv on the image.
+template <int ACT, bool UPS = false>
+__global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G16, int HW) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)B * G16 * HW) return;
+  const int po = (int)(i % HW);
+  const int p = UPS ? ((po / a.Wo) >> 1) * a.Ws + ((po % a.Wo) >> 1) : po;
+  const int HWs = UPS ? a.Ws * a.Ws : HW;
+  const long long r = i / HW;
+  const int g = (int)(r % G16), b = (int)(r / G16);
+  const int Cin = a.Cin, Ca = a.Ca;
+  unsigned w[8];
+#pragma unroll
+  for (int j2 = 0; j2 < 8; ++j2) {
+    unsigned bits[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int c = g * 16 + 2 * j2 + e;
+      bits[e] = 0u;
+      if (c < Cin) {
+        const float* src = c < Ca ? a.srcA + ((size_t)b * Ca + c) * HWs
+                                  : a.srcB + ((size_t)b * a.Cb + (c - Ca)) * HWs;
+        float v = src[p];
+        if constexpr (ACT != ACT_NONE) {
+          const float2 gs = a.gn[(size_t)b * Cin + c];
+          v = fmaf(v, gs.x, gs.y);
+          if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+        }
+        bits[e] = bf16_bits(v);
+      }
+    }
+    w[j2] = bits[0] | (bits[1] << 16);
+  }
+  u32x4* dst = reinterpret_cast<u32x4*>(static_cast<char*>(a.bimg) + (size_t)i * 32);
+  dst[0] = u32x4{w[0], w[1], w[2], w[3]};
+  dst[1] = u32x4{w[4], w[5], w[6], w[7]};
+}
+
+size_t conv_bf16_image_bytes(int cin, int B, int H, int W) {
+  return (size_t)B * ((cin + 15) / 16) * H * W * 32;
+}
+
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false>
 static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
   using G = GeomH<KS, MODE, WO, TPX>;
   const size_t lds = G::LDS + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)conv_bf16_kernel<KS, MODE, ACT, WO, TPX>,
+    (void)hipFuncSetAttribute((const void*)conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((unsigned)(WO * WO / G::BM), (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
-  conv_bf16_kernel<KS, MODE, ACT, WO, TPX><<<grid, NTHR, lds, s>>>(a);
+  conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE><<<grid, NTHR, lds, s>>>(a);
   return hipGetLastError();
+}
+
+// ERTD_UNET_BF16_PRE=0 keeps the register staging for stride-1 convs (diagnostics)
+static int convh_pre() {
+  static int v = [] {
+    const char* e = getenv("ERTD_UNET_BF16_PRE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <int KS, int TP>
+static hipError_t launch_pre_w(const ConvArgs& a, int B, hipStream_t s) {
+  switch (a.Wo) {
+    case 16: return launch_hg<KS, MODE_S1, ACT_NONE, 16, TP, true>(a, B, s);
+    case 32: return launch_hg<KS, MODE_S1, ACT_NONE, 32, TP, true>(a, B, s);
+    case 64: return launch_hg<KS, MODE_S1, ACT_NONE, 64, TP, true>(a, B, s);
+    case 128: return launch_hg<KS, MODE_S1, ACT_NONE, 128, TP, true>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// stride-1 (or upsample) conv through the pre-transformed image: transform,
+// then the conv as stride 1 on the image
+static hipError_t launch_conv_pre(int ks, int mode, int act, const ConvArgs& a, int B,
+                                  hipStream_t s) {
+  const int HW = a.Wo * a.Wo, G16 = (a.Cin + 15) / 16;
+  const long long n = (long long)B * G16 * HW;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (mode == MODE_UP) act_bf16_kernel<ACT_NONE, true><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else if (act == ACT_GN_SILU) act_bf16_kernel<ACT_GN_SILU><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else if (act == ACT_GN) act_bf16_kernel<ACT_GN><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else act_bf16_kernel<ACT_NONE><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  ConvArgs c = a;
+  c.Hs = c.Ws = a.Wo;   // the image is at the output resolution
+  if (ks == 1) return launch_pre_w<1, 1>(c, B, s);
+  return launch_pre_w<3, 2>(c, B, s);
 }
 
 // ERTD_UNET_BF16_TPX=1 forces 128-pixel tiles for the 3x3 stride-1/upsample
@@ -326,6 +461,12 @@ hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B,
   if (a.Wo != expect) return hipErrorInvalidValue;
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)
     return launch_conv_out(act, a, B, true, s);
+  // the pre-transform pays where the staging VALU is heaviest: 3x3 convs with
+  // a GroupNorm(+SiLU) prologue and the Upsample convs (measured on U3 B=256:
+  // the extra read+write pass costs more than it saves for 1x1 convs)
+  if (a.bimg && convh_pre() == 1 && ks == 3 &&
+      ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
+    return launch_conv_pre(ks, mode, act, a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_hw<3, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_hw<3, MODE_S1, ACT_GN_SILU>(a, B, s);
   if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_hw<3, MODE_S2, ACT_NONE>(a, B, s);
