@@ -37,6 +37,7 @@ struct ConvArgs {
   int Ho, Wo;            // output spatial size
   void* bimg;            // bf16 3x3 GN / Upsample convs: scratch for the pre-transformed
                          // input, conv_bf16_image_bytes(Cin, B, Ho, Wo) bytes (null: stage fp32)
+  int bimg_ready;        // 1: bimg already holds the transformed input (launch_gn_act_bf16)
 };
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
@@ -61,6 +62,12 @@ struct GnArgs {
   float2* out;           // (B, Ca+Cb) {gamma*rstd, beta - mean*gamma*rstd}
 };
 hipError_t launch_gn_stats(const GnArgs& a, int B, hipStream_t s);
+// GroupNorm statistics + apply (+ SiLU) + bf16 image of a 3x3 stride-1 bf16
+// conv's input in one pass (unet_conv_bf16.hip); writes a.out like
+// launch_gn_stats and the [B][C/16][H][W][16] image; shapes gated by
+// gn_act_bf16_fits (C/16 whole, <= 64 activations per thread)
+bool gn_act_bf16_fits(int C, int groups, int HW);
+hipError_t launch_gn_act_bf16(const GnArgs& a, bool silu, void* bimg, int B, hipStream_t s);
 
 // y[b][o] = bias[o] (+ add[b][o]) + sum_k Wt[k][o] * in(b, k)
 enum DenseIn { DIN_PLAIN = 0, DIN_SILU = 1, DIN_SINUSOID = 2 };

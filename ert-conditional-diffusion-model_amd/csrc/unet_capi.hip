@@ -6,6 +6,7 @@
 // Everything is enqueued on the caller's stream; the library allocates
 // nothing.  Workspace = one NCHW buffer per layer output (bump allocator over
 // the caller's ws), so a whole step can be captured into a hipGraph.
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <map>
@@ -198,9 +199,29 @@ struct Walk {
 
   float2* gnbuf = nullptr;
 
-  void gn_stats(const float* A, int Ca, const float* Bs, int Cb, int HW, const std::string& n) {
+  // bf16: the statistics of a 3x3 GN+SiLU conv's input are computed by the
+  // fused gn_act_bf16_kernel together with its bf16 image (one read of the
+  // activation); the launch is deferred to conv()
+  GnArgs pend{};
+  bool has_pend = false;
+  static bool fuse_gn_env() {
+    static const bool v = [] {
+      const char* e = getenv("ERTD_UNET_BF16_FUSEGN");
+      return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+  }
+
+  void gn_stats(const float* A, int Ca, const float* Bs, int Cb, int HW, const std::string& n,
+                bool fusable = false) {
     if (dry) return;
     GnArgs g{A, Bs, Ca, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"), gnbuf};
+    if (fusable && c->precision == ERTD_PREC_BF16 && fuse_gn_env() &&
+        gn_act_bf16_fits(Ca + Cb, c->groups, HW)) {
+      pend = g;
+      has_pend = true;
+      return;
+    }
     chk(launch_gn_stats(g, B, s));
   }
 
@@ -236,6 +257,15 @@ struct Walk {
     a.Cin = Cin; a.Cout = Cout;
     a.Hs = Hs; a.Ws = Ws; a.Ho = Ho; a.Wo = Wo;
     a.bimg = bimg;
+    if (has_pend) {
+      has_pend = false;
+      if (bimg && ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) {
+        chk(launch_gn_act_bf16(pend, true, bimg, B, s));
+        a.bimg_ready = 1;
+      } else {
+        chk(launch_gn_stats(pend, B, s));
+      }
+    }
     chk(c->precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
                                        : launch_conv(ks, mode, act, a, B, s));
     return out;
@@ -245,12 +275,12 @@ struct Walk {
                   int Ww, int cout, const float* ebias_all) {
     const int HW = Hh * Ww;
     const float* eb = ebias_all ? ebias_all + L->eboff.at(n) : nullptr;
-    gn_stats(A, Ca, Bs, Cb, HW, n + ".norm1");
+    gn_stats(A, Ca, Bs, Cb, HW, n + ".norm1", true);
     float* h1 = conv(n + ".conv1", 3, MODE_S1, ACT_GN_SILU, A, Ca, Bs, Cb, Hh, Ww, eb, nullptr);
     const float* resid = A;
     if (Ca + Cb != cout) resid = conv(n + ".skip", 1, MODE_S1, ACT_NONE, A, Ca, Bs, Cb, Hh, Ww,
                                       nullptr, nullptr);
-    gn_stats(h1, cout, nullptr, 0, HW, n + ".norm2");
+    gn_stats(h1, cout, nullptr, 0, HW, n + ".norm2", true);
     return conv(n + ".conv2", 3, MODE_S1, ACT_GN_SILU, h1, cout, nullptr, 0, Hh, Ww, nullptr, resid);
   }
 
@@ -565,6 +595,17 @@ int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B
     return ERTD_EINVAL;
   GnArgs g{x, x2, Ca, Cb, HW, groups, gamma, beta, (float2*)out};
   return rcode(launch_gn_stats(g, B, (hipStream_t)stream));
+}
+
+int ertd_group_norm_act_bf16(const float* x, int Ca, const float* x2, int Cb, int B, int H,
+                             int groups, const float* gamma, const float* beta, float* out,
+                             void* img, int silu, void* stream) {
+  const int C = Ca + Cb;
+  if (!x || !gamma || !beta || !out || !img || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
+      groups < 1 || H < 1 || !gn_act_bf16_fits(C, groups, H * H))
+    return ERTD_EINVAL;
+  GnArgs g{x, x2, Ca, Cb, H * H, groups, gamma, beta, (float2*)out};
+  return rcode(launch_gn_act_bf16(g, silu != 0, img, B, (hipStream_t)stream));
 }
 
 int ertd_attention(const float* qkv, int B, int C, int N, float* out, void* stream) {

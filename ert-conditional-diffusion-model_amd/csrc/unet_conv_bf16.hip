@@ -365,6 +365,151 @@ __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G1
   dst[1] = u32x4{w[4], w[5], w[6], w[7]};
 }
 
+// ---- fused GroupNorm statistics + apply + SiLU + bf16 image (3x3 GN convs) ----------
+// One workgroup per (channel set, sample); a channel set is lcm(C/groups, 16)
+// channels = NB 16-channel image blocks holding whole groups.  Thread t owns
+// NREC pixels p = t + nthr*k and ALL of the set's channels at them, so:
+//  - loads: per (channel, k) one coalesced 256-B row per wave, all issued up
+//    front into registers (the activation is read from HBM once);
+//  - statistics: the thread's values of one group are summed in float64 in
+//    a fixed order, one wave reduction per group, then a fixed-order sum of
+//    the waves' partials (the sum / sum-of-squares form of gn_stats_kernel);
+//    {scale, shift} per channel also go to `gn` (for convs that stage fp32);
+//  - output: x*scale+shift, SiLU, bf16 RNE, and the thread writes its whole
+//    32-B pixel records of the [B][C/16][H][W][16] image (consecutive lanes =
+//    consecutive records) -- no transpose.
+// Replaces gn_stats_kernel + act_bf16_kernel: one fp32 read of the activation
+// instead of two.
+__host__ __device__ constexpr int ga_gcd(int a, int b) { return b == 0 ? a : ga_gcd(b, a % b); }
+
+template <bool SILU, int NREC, int NB>
+__global__ __launch_bounds__(1024) void gn_act_bf16_kernel(GnArgs g, void* bimg) {
+  constexpr int NCH = NB * 16;
+  __shared__ double2 part[8][16];   // [group in set][wave]
+  __shared__ float2 tab[NCH];
+  const int C = g.Ca + g.Cb, HW = g.HW;
+  const int cpg = C / g.groups;
+  const int nthr = HW / NREC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int set = blockIdx.x, b = blockIdx.y;
+  const int c0 = set * NCH;
+
+  float v[NCH][NREC];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int cg = c0 + c;
+    const float* src = cg < g.Ca ? g.srcA + ((size_t)b * g.Ca + cg) * HW
+                                 : g.srcB + ((size_t)b * g.Cb + (cg - g.Ca)) * HW;
+#pragma unroll
+    for (int k = 0; k < NREC; ++k) v[c][k] = src[tid + k * nthr];
+  }
+  double s = 0.0, ss = 0.0;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+    for (int k = 0; k < NREC; ++k) {
+      s += (double)v[c][k];
+      ss += (double)v[c][k] * v[c][k];
+    }
+    if ((c + 1) % cpg == 0) {   // last channel of a group: reduce over the wave
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o);
+        ss += __shfl_xor(ss, o);
+      }
+      if (lane == 0) part[c / cpg][w] = make_double2(s, ss);
+      s = 0.0;
+      ss = 0.0;
+    }
+  }
+  __syncthreads();
+  if (tid < NCH) {
+    const int gi = tid / cpg;
+    const int nw = nthr / 64;
+    double S = 0.0, SS = 0.0;
+    for (int k = 0; k < nw; ++k) {
+      S += part[gi][k].x;
+      SS += part[gi][k].y;
+    }
+    const double n = (double)cpg * HW;
+    const double mean = S / n;
+    double var = SS / n - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
+    const int cg = c0 + tid;
+    const float scale = rstd * g.gamma[cg];
+    const float shift = -scale * (float)mean + g.beta[cg];
+    tab[tid] = make_float2(scale, shift);
+    g.out[(size_t)b * C + cg] = make_float2(scale, shift);
+  }
+  __syncthreads();
+  char* base = static_cast<char*>(bimg) + ((size_t)b * (C / 16) + (size_t)set * NB) * HW * 32;
+#pragma unroll
+  for (int blk = 0; blk < NB; ++blk) {
+#pragma unroll
+    for (int k = 0; k < NREC; ++k) {
+      unsigned u[8];
+#pragma unroll
+      for (int j2 = 0; j2 < 8; ++j2) {
+        unsigned bits[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int c = blk * 16 + 2 * j2 + e;
+          const float2 t = tab[c];
+          float x = fmaf(v[c][k], t.x, t.y);
+          if constexpr (SILU) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+          bits[e] = bf16_bits(x);
+        }
+        u[j2] = bits[0] | (bits[1] << 16);
+      }
+      u32x4* dst = reinterpret_cast<u32x4*>(base + ((size_t)blk * HW + tid + k * nthr) * 32);
+      dst[0] = u32x4{u[0], u[1], u[2], u[3]};
+      dst[1] = u32x4{u[4], u[5], u[6], u[7]};
+    }
+  }
+}
+
+// shape plan of the fused path: records per thread (NREC) and image blocks per
+// set (NB); false -> gn_stats + the conv's own transform
+static bool ga_plan(int C, int groups, int HW, int* nrec, int* nb) {
+  if (C % 16 || groups < 1 || C % groups || HW < 64 || HW % 64) return false;
+  const int cpg = C / groups;
+  const int bch = cpg / ga_gcd(cpg, 16) * 16;
+  if (C % bch || bch / cpg > 8) return false;
+  const int NB = bch / 16;
+  const int NREC = HW <= 1024 ? 1 : HW / 1024;
+  if (HW > 1024 && HW % 1024) return false;
+  if (!((NB == 1 && (NREC == 1 || NREC == 2 || NREC == 4)) || (NB == 3 && NREC == 1)))
+    return false;
+  *nrec = NREC;
+  *nb = NB;
+  return true;
+}
+
+bool gn_act_bf16_fits(int C, int groups, int HW) {
+  int r, n;
+  return ga_plan(C, groups, HW, &r, &n);
+}
+
+template <bool SILU>
+static hipError_t launch_ga(const GnArgs& g, int nrec, int nb, void* bimg, int B, hipStream_t s) {
+  const int C = g.Ca + g.Cb;
+  dim3 grid((unsigned)(C / (16 * nb)), (unsigned)B);
+  const int thr = g.HW / nrec;
+  if (nb == 3) gn_act_bf16_kernel<SILU, 1, 3><<<grid, thr, 0, s>>>(g, bimg);
+  else if (nrec == 1) gn_act_bf16_kernel<SILU, 1, 1><<<grid, thr, 0, s>>>(g, bimg);
+  else if (nrec == 2) gn_act_bf16_kernel<SILU, 2, 1><<<grid, thr, 0, s>>>(g, bimg);
+  else gn_act_bf16_kernel<SILU, 4, 1><<<grid, thr, 0, s>>>(g, bimg);
+  return hipGetLastError();
+}
+
+hipError_t launch_gn_act_bf16(const GnArgs& g, bool silu, void* bimg, int B, hipStream_t s) {
+  int nrec, nb;
+  if (!bimg || !ga_plan(g.Ca + g.Cb, g.groups, g.HW, &nrec, &nb)) return hipErrorInvalidValue;
+  return silu ? launch_ga<true>(g, nrec, nb, bimg, B, s) : launch_ga<false>(g, nrec, nb, bimg, B, s);
+}
+
 size_t conv_bf16_image_bytes(int cin, int B, int H, int W) {
   return (size_t)B * ((cin + 15) / 16) * H * W * 32;
 }
@@ -409,7 +554,9 @@ static hipError_t launch_conv_pre(int ks, int mode, int act, const ConvArgs& a, 
   const int HW = a.Wo * a.Wo, G16 = (a.Cin + 15) / 16;
   const long long n = (long long)B * G16 * HW;
   const unsigned blocks = (unsigned)((n + 255) / 256);
-  if (mode == MODE_UP) act_bf16_kernel<ACT_NONE, true><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  if (a.bimg_ready) {
+    // image already written by gn_act_bf16_kernel
+  } else if (mode == MODE_UP) act_bf16_kernel<ACT_NONE, true><<<blocks, 256, 0, s>>>(a, B, G16, HW);
   else if (act == ACT_GN_SILU) act_bf16_kernel<ACT_GN_SILU><<<blocks, 256, 0, s>>>(a, B, G16, HW);
   else if (act == ACT_GN) act_bf16_kernel<ACT_GN><<<blocks, 256, 0, s>>>(a, B, G16, HW);
   else act_bf16_kernel<ACT_NONE><<<blocks, 256, 0, s>>>(a, B, G16, HW);

@@ -76,6 +76,7 @@ SIGNATURES = {
     "ertd_conv2d": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP,
                          _I, _VP, _SZ, _VP]),
     "ertd_group_norm_stats": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _VP]),
+    "ertd_group_norm_act_bf16": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _VP, _I, _VP]),
     "ertd_attention": (_I, [_VP, _I, _I, _I, _VP, _VP]),
     "ertd_unet_n_params": (_I, [_VP]),
     "ertd_unet_param_info": (_I, [_VP, _I, ctypes.c_char_p, _I, _VP, ctypes.POINTER(_I)]),

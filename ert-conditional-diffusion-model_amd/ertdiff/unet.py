@@ -348,7 +348,8 @@ class UNetSamplerPlan:
             pass
 
 
-# ---- single operators (ertd_conv2d / ertd_group_norm_stats / ertd_attention) ----------
+# ---- single operators (ertd_conv2d / ertd_group_norm_stats / ertd_group_norm_act_bf16 /
+#      ertd_attention) ----------
 _MODES2D = {"same": 0, "down": 1, "up": 2}
 _ACTS = {"none": 0, "gn_silu": 1, "gn": 2}
 
@@ -400,6 +401,27 @@ def group_norm_stats(x: torch.Tensor, groups: int, gamma: torch.Tensor, beta: to
             groups, _lib.f32c(gamma, "gamma").data_ptr(), _lib.f32c(beta, "beta").data_ptr(),
             out.data_ptr(), _lib.stream_of(dev)), "group_norm_stats")
     return out
+
+
+def group_norm_act_bf16(x: torch.Tensor, groups: int, gamma: torch.Tensor, beta: torch.Tensor,
+                        x2: Optional[torch.Tensor] = None, silu: bool = True):
+    """The bf16 path's fused 3x3-conv prologue: ((B, C, 2) {scale, shift} as
+    group_norm_stats, (B, C/16, H, W, 16) int16 bf16 bits of
+    act(GroupNorm(cat(x, x2)))) in one pass over x."""
+    dev = _lib.require_device(x, gamma, beta)
+    x = _lib.f32c(x, "x")
+    B, Ca, H, W = x.shape
+    Cb = 0 if x2 is None else x2.shape[1]
+    C = Ca + Cb
+    out = torch.empty(B, C, 2, dtype=torch.float32, device=dev)
+    img = torch.empty(B, (C + 15) // 16, H, W, 16, dtype=torch.int16, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().ertd_group_norm_act_bf16(
+            x.data_ptr(), Ca, _lib.ptr(None if x2 is None else _lib.f32c(x2, "x2")), Cb, B, H,
+            groups, _lib.f32c(gamma, "gamma").data_ptr(), _lib.f32c(beta, "beta").data_ptr(),
+            out.data_ptr(), img.data_ptr(), 1 if silu else 0, _lib.stream_of(dev)),
+            "group_norm_act_bf16")
+    return out, img
 
 
 def attention(qkv: torch.Tensor) -> torch.Tensor:

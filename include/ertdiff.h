@@ -259,6 +259,15 @@ int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B
                           int groups, const float* gamma, const float* beta, float* out,
                           void* stream);
 int ertd_attention(const float* qkv, int B, int C, int N, float* out, void* stream);
+/* ertd_group_norm_act_bf16: the bf16 path's fused prologue of a 3x3 GN conv
+ *   in one pass -- out as ertd_group_norm_stats, and img = bf16 RNE of
+ *   act(GroupNorm(cat(x, x2))) (act: silu=1 SiLU, 0 none) in the conv's
+ *   [B][C/16][H][H][16] layout (C*H*H*2 bytes per sample).  ERTD_EINVAL
+ *   unless C % 16 == 0, lcm(C/groups, 16) * H*H <= 65536 (and a multiple of
+ *   1024), H*H % 64 == 0.                                                    */
+int ertd_group_norm_act_bf16(const float* x, int Ca, const float* x2, int Cb, int B, int H,
+                             int groups, const float* gamma, const float* beta, float* out,
+                             void* img, int silu, void* stream);
 
 /* Parameter tensors in state_dict order: count, and (name, shape) of one.  */
 int ertd_unet_n_params(const ertd_unet_config* cfg);

@@ -11,7 +11,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from ertdiff.unet import attention, conv2d, group_norm_stats
+from ertdiff.unet import attention, conv2d, group_norm_act_bf16, group_norm_stats
 from oracle import ref_numpy as RN
 
 pytestmark = pytest.mark.gpu
@@ -107,6 +107,50 @@ def test_group_norm_stats(Ca, Cb, H, cuda_dev):
     y = xin * ss[..., 0][:, :, None, None] + ss[..., 1][:, :, None, None]
     ref = F.group_norm(xin, G, gamma, beta, eps=1e-5)
     assert RN.rel_l2(y.double().numpy(), ref.double().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("Ca,Cb,H,silu", [(64, 0, 64, True), (128, 64, 32, True),
+                                          (256, 128, 16, True), (192, 0, 32, False),
+                                          (512, 0, 16, True), (64, 0, 16, True)])
+def test_group_norm_act_bf16(Ca, Cb, H, silu, cuda_dev):
+    """Fused statistics + GN(+SiLU) + bf16 image (the bf16 3x3 convs' prologue):
+    {scale, shift} within 1e-6 of group_norm_stats (same float64 sum/sumsq
+    form, another summation order); image = RNE bf16 of the fp32 activation:
+    >= 99 % of elements bit-equal to torch's, every element within 1 bf16 ulp
+    (the kernel's fast exp/rcp SiLU), pixel records in [B][C/16][H][W][16]."""
+    B, G = 3, 32
+    x = _rand((B, Ca, H, H), 22, 2.0) + 0.5
+    x2 = _rand((B, Cb, H, H), 23) if Cb else None
+    gamma, beta = _rand((Ca + Cb,), 24) + 1, _rand((Ca + Cb,), 25)
+    dx2 = None if x2 is None else x2.to(cuda_dev)
+    ss, img = group_norm_act_bf16(x.to(cuda_dev), G, gamma.to(cuda_dev), beta.to(cuda_dev),
+                                  x2=dx2, silu=silu)
+    ref_ss = group_norm_stats(x.to(cuda_dev), G, gamma.to(cuda_dev), beta.to(cuda_dev), x2=dx2)
+    ss, ref_ss, img = ss.cpu(), ref_ss.cpu(), img.cpu()
+    assert torch.allclose(ss, ref_ss, rtol=1e-6, atol=1e-6)
+    xin = x if x2 is None else torch.cat([x, x2], 1)
+    # the kernel applies x*scale+shift as ONE fma: the reference rounds once too
+    # (float64 product of two floats is exact), else cancellation near zero
+    # differs in relative terms
+    y = (xin.double() * ss[..., 0][:, :, None, None].double()
+         + ss[..., 1][:, :, None, None].double()).float()
+    if silu:
+        y = F.silu(y)
+    C = Ca + Cb
+    ref = y.to(torch.bfloat16).view(torch.int16).reshape(B, C // 16, 16, H, H).permute(0, 1, 3, 4, 2)
+    got_f = img.view(torch.bfloat16).float()
+    ref_f = ref.contiguous().view(torch.bfloat16).float()
+    eq = (img == ref.contiguous()).float().mean().item()
+    assert eq >= 0.99, f"only {eq:.4f} of the image bit-equal"
+    ulp = (ref_f.abs() * 2.0 ** -7).clamp_min(1e-6)
+    assert bool(((got_f - ref_f).abs() <= ulp).all())
+
+
+def test_group_norm_act_bf16_rejects_shapes(cuda_dev):
+    x = torch.zeros(1, 24, 16, 16, device=cuda_dev)   # C % 16 != 0
+    g = torch.ones(24, device=cuda_dev)
+    with pytest.raises(RuntimeError):
+        group_norm_act_bf16(x, 8, g, g)
 
 
 def test_attention(cuda_dev):
