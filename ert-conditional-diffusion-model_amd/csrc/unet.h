@@ -19,7 +19,10 @@ constexpr double GN_EPS = 1e-5;   // GroupNorm eps (oracle/unet_torch.py)
 enum Act { ACT_NONE = 0, ACT_GN_SILU = 1, ACT_GN = 2 };
 // Spatial mode of a 3x3 conv: stride 1, stride 2 (Downsample), nearest x2
 // upsample of the source followed by the stride-1 conv (Upsample).
-enum Mode { MODE_S1 = 0, MODE_S2 = 1, MODE_UP = 2 };
+enum Mode { MODE_S1 = 0, MODE_S2 = 1, MODE_UP = 2,
+            // fp32 kernel only (internal): the Upsample conv as 4 sub-pixel
+            // 2x2 convs at the source resolution (launch_pack_conv_up weights)
+            MODE_UPP = 3 };
 
 struct ConvArgs {
   const float* srcA;     // (B, Ca, Hs, Ws)  channels [0, Ca)
@@ -54,6 +57,9 @@ hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStre
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s);
+// fp32 Upsample conv weights: 4 parity classes of combined 2x2 taps
+size_t conv_packed_floats_up(int cin, int cout);
+hipError_t launch_pack_conv_up(const float* w, int cin, int cout, float* dst, hipStream_t s);
 
 struct GnArgs {
   const float* srcA; const float* srcB; int Ca, Cb;

@@ -168,7 +168,9 @@ Layout layout(const ertd_unet_config* c) {
     if (p.shape.size() == 4)
       o += a64(c->precision == ERTD_PREC_BF16
                    ? conv_packed_floats_bf16(p.shape[1], p.shape[0], p.shape[2])
-                   : conv_packed_floats(p.shape[1], p.shape[0], p.shape[2]));
+                   : (ends_with(p.name, ".upsample.weight")
+                          ? conv_packed_floats_up(p.shape[1], p.shape[0])
+                          : conv_packed_floats(p.shape[1], p.shape[0], p.shape[2])));
     else o += a64(p.numel());
   }
   L.total = o;
@@ -544,8 +546,11 @@ extern "C" {
 
 size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision) {
   if (cin < 1 || cout < 1 || (ks != 1 && ks != 3)) return 0;
-  const size_t f = precision == ERTD_PREC_BF16 ? conv_packed_floats_bf16(cin, cout, ks)
-                                               : conv_packed_floats(cin, cout, ks);
+  size_t f = precision == ERTD_PREC_BF16 ? conv_packed_floats_bf16(cin, cout, ks)
+                                         : conv_packed_floats(cin, cout, ks);
+  // fp32 3x3 convs may be Upsample convs (sub-pixel packing)
+  if (precision != ERTD_PREC_BF16 && ks == 3 && conv_packed_floats_up(cin, cout) > f)
+    f = conv_packed_floats_up(cin, cout);
   return f * sizeof(float);
 }
 
@@ -563,7 +568,8 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   hipStream_t s = (hipStream_t)stream;
   float* pk = (float*)ws;
   hipError_t e = precision == ERTD_PREC_BF16 ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s)
-                                             : launch_pack_conv(w, Cin, Cout, ks, pk, s);
+                 : (ks == 3 && mode == MODE_UP) ? launch_pack_conv_up(w, Cin, Cout, pk, s)
+                                                : launch_pack_conv(w, Cin, Cout, ks, pk, s);
   if (e != hipSuccess) return (int)e;
   ConvArgs a{};
   a.srcA = x; a.srcB = x2; a.Ca = Ca; a.Cb = Cb;
@@ -673,8 +679,10 @@ int ertd_unet_pack(const ertd_unet_config* c, const float* const* params, const 
       e = c->precision == ERTD_PREC_BF16
               ? launch_pack_conv_bf16(src, p.shape[1], p.shape[0], p.shape[2],
                                       packed + L.off.at(p.name), s)
-              : launch_pack_conv(src, p.shape[1], p.shape[0], p.shape[2],
-                                 packed + L.off.at(p.name), s);
+              : (ends_with(p.name, ".upsample.weight")
+                     ? launch_pack_conv_up(src, p.shape[1], p.shape[0], packed + L.off.at(p.name), s)
+                     : launch_pack_conv(src, p.shape[1], p.shape[0], p.shape[2],
+                                        packed + L.off.at(p.name), s));
     } else if (p.shape.size() == 2) {
       e = launch_transpose(src, p.shape[0], p.shape[1], packed + L.off.at(p.name), p.shape[0], s);
     } else {

@@ -31,7 +31,15 @@
 //
 // Skip concatenations (the up path) are read from two source tensors in place
 // (channels [0,Ca) from srcA, [Ca,Ca+Cb) from srcB); the nearest x2 Upsample is
-// folded into the staging address (source row/col = staged row/col >> 1).
+// folded into the staging address (source row/col = staged row/col >> 1) for
+// the bf16 kernel; the fp32 kernel runs the Upsample conv sub-pixel
+// (MODE_UPP): output pixel (2i+a, 2j+b) of conv3x3(nearest_x2(x)) reads only
+// source rows {i-1+a, i+a} and columns {j-1+b, j+b}, so each parity class
+// (a, b) is a 2x2 conv at the SOURCE resolution with taps summed from the
+// 3x3 kernel (a=0: row taps {W0, W1+W2}; a=1: {W0+W1, W2}; same for columns)
+// -- 4 taps per output pixel instead of 9, exact up to the fp32 rounding of
+// the summed weights.  grid.x = 4 classes x pixel tiles; the epilogue
+// scatters each class to its output parity.
 #include <cstdlib>
 
 #include "unet.h"
@@ -55,7 +63,7 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 }
 
 // channels per K-chunk: 4 for 3x3 (36-deep K per chunk), 32 for 1x1 (32-deep)
-__host__ __device__ constexpr int conv_ck(int ks) { return ks == 3 ? 4 : 32; }
+__host__ __device__ constexpr int conv_ck(int ks) { return ks == 3 ? 4 : (ks == 2 ? 8 : 32); }
 
 template <int KS, int MODE, int WCO, int WO, int TPX>
 struct ConvGeom {
@@ -64,14 +72,14 @@ struct ConvGeom {
   static constexpr int BN = 64 * WCO;                 // output channels per workgroup
   static constexpr int WST = MODE == MODE_S2 ? 2 * WO : WO;   // staged image width
   static constexpr int R = BM / WO;                   // output rows per workgroup
-  static constexpr int IR = KS == 1 ? R : (MODE == MODE_S2 ? 2 * R + 1 : R + 2);
+  static constexpr int IR = KS == 1 ? R : (KS == 2 ? R + 1 : (MODE == MODE_S2 ? 2 * R + 1 : R + 2));
   static constexpr int IP = WST + 2;                  // LDS row pitch (zero column each side)
   static constexpr int CP = IR * IP;                  // channel pitch
   static constexpr int CKK = conv_ck(KS);             // input channels per chunk
   static constexpr int CH = CKK / 2;                  // channels per lane half
   static constexpr int HP = CH * CP + (MODE == MODE_S2 ? 1 : 0);  // lane-half pitch
   static constexpr int XB = (2 * HP + 3) / 4 * 4;     // input image floats per buffer
-  static constexpr int SPC = KS == 3 ? 9 * CH : CH;   // k-steps per chunk
+  static constexpr int SPC = KS == 3 ? 9 * CH : (KS == 2 ? 4 * CH : CH);   // k-steps per chunk
   static constexpr int TW = SPC * 64;                 // weight floats per 32-cout tile and chunk
   static constexpr int WB = (BN / 32) * TW;           // weight floats per buffer
   static constexpr int RSTEP = NTHR / WST;            // staged rows per thread pass
@@ -101,7 +109,10 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   const int h = lane >> 5, l32 = lane & 31;
   const int wco = wave % WCO, wpx = wave / WCO;
   const int b = blockIdx.z;
-  const int p0 = blockIdx.x * G::BM;
+  // MODE_UPP: parity class (pa, pb) of this workgroup's output pixels
+  const int cls = MODE == MODE_UPP ? (int)(blockIdx.x & 3) : 0;
+  const int pa = cls >> 1, pb = cls & 1;
+  const int p0 = (MODE == MODE_UPP ? (int)(blockIdx.x >> 2) : (int)blockIdx.x) * G::BM;
   const int oy0 = p0 / WO;
   const int Cin = a.Cin, Ca = a.Ca;
   constexpr int HS = MODE == MODE_UP ? WO / 2 : G::WST;   // source height = width (square)
@@ -127,6 +138,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   int row0;
   if constexpr (KS == 1) row0 = oy0;
   else if constexpr (MODE == MODE_S2) row0 = 2 * oy0 - 1;
+  else if constexpr (MODE == MODE_UPP) row0 = oy0 - 1 + pa;
   else row0 = oy0 - 1;
   const int sx = MODE == MODE_UP ? (col >> 1) : col;
   constexpr size_t plane = (size_t)HS * HS;
@@ -173,6 +185,8 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
 
   // ---- weight slice DMA: chunk k of this workgroup's BN/32 tiles -> wim[buf]
   const int tile_wg = blockIdx.y * (G::BN / 32);
+  const size_t wcls = MODE == MODE_UPP
+                          ? (size_t)cls * ((a.Cout + 127) / 128 * 4) * nchunk * G::TW : 0;
   // LDS-DMA by inline asm: hipcc's own global_load_lds bookkeeping waits
   // vmcnt(0) before every DMA (serialising them); here they are counted by
   // hand -- the single wait is the vmcnt(0) ahead of the chunk's barrier.
@@ -183,7 +197,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
       if (ins < G::NGL) {
         const int f = ins * 256 + lane * 4;          // float index in the slice
         const int ti = f / G::TW, wi = f - ti * G::TW;
-        const float* src = a.wpk + ((size_t)(tile_wg + ti) * nchunk + k) * G::TW + wi;
+        const float* src = a.wpk + wcls + ((size_t)(tile_wg + ti) * nchunk + k) * G::TW + wi;
         const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr(wdst + ins * 256));
         unsigned keep;
         asm volatile(
@@ -205,6 +219,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
     const int oyl = pl / WO, ox = pl - oyl * WO;
     int rb, cb;
     if constexpr (KS == 1) { rb = oyl; cb = ox + 1; }
+    else if constexpr (KS == 2) { rb = oyl; cb = ox + pb; }
     else if constexpr (MODE == MODE_S2) { rb = 2 * oyl; cb = 2 * ox; }
     else { rb = oyl; cb = ox; }
     lbase[t] = h * G::HP + rb * G::IP + cb;
@@ -255,6 +270,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
         const int s = 2 * sp + e;
         int off;
         if constexpr (KS == 1) off = s * G::CP;
+        else if constexpr (KS == 2) off = (s / 4) * G::CP + ((s % 4) / 2) * G::IP + (s % 2);
         else off = (s / 9) * G::CP + ((s % 9) / 3) * G::IP + (s % 3);
         float bv[TPX];
 #pragma unroll
@@ -286,6 +302,38 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   // do and serialises every residual load behind the previous store.
   // Phases of 8 accumulator rows with 32-bit offsets from one per-lane base
   // keep the epilogue's live registers below the main loop's.
+  if constexpr (MODE == MODE_UPP) {
+    // scatter the class's pixels to their output parity (2i+pa, 2j+pb)
+    constexpr int WOUT = 2 * WO, HWO = WOUT * WOUT;
+    const int tile0 = tile_wg + wco * 2;
+    int pix[TPX];
+#pragma unroll
+    for (int j = 0; j < TPX; ++j) {
+      const int ps = p0 + wpx * 32 * TPX + j * 32 + l32;
+      const int oy = ps / WO, ox = ps - oy * WO;
+      pix[j] = (2 * oy + pa) * WOUT + 2 * ox + pb;
+    }
+    float* __restrict__ outb = a.out + (size_t)b * a.Cout * HWO;
+    const float* __restrict__ resb = a.res ? a.res + (size_t)b * a.Cout * HWO : nullptr;
+    const float* ebp = a.ebias ? a.ebias + (size_t)b * a.eb_stride : nullptr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= a.Cout) continue;
+        const float bias = a.bias[co];
+#pragma unroll
+        for (int j = 0; j < TPX; ++j) {
+          float v = acc[i][j][r] + bias;
+          if (ebp) v = v + ebp[co];
+          if (resb) v = v + resb[(size_t)co * HWO + pix[j]];
+          outb[(size_t)co * HWO + pix[j]] = v;
+        }
+      }
+    }
+    return;
+  }
   constexpr int HWo = WO * WO;
   const int tile0 = tile_wg + wco * 2;
   const size_t lbase0 = (size_t)b * a.Cout * HWo + p0 + wpx * 32 * TPX + l32;
@@ -344,7 +392,8 @@ static hipError_t launch_gs(const ConvArgs& a, int B, hipStream_t s) {
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)conv_kernel<KS, MODE, ACT, WCO, WO, TPX, STG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  dim3 grid((unsigned)(WO * WO / G::BM), (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
+  dim3 grid((unsigned)((MODE == MODE_UPP ? 4 : 1) * WO * WO / G::BM),
+            (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
   conv_kernel<KS, MODE, ACT, WCO, WO, TPX, STG><<<grid, NTHR, lds, s>>>(a);
   return hipGetLastError();
 }
@@ -407,7 +456,17 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_t<3, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_t<3, MODE_S1, ACT_GN_SILU>(a, B, s);
   if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_t<3, MODE_S2, ACT_NONE>(a, B, s);
-  if (ks == 3 && mode == MODE_UP && act == ACT_NONE) return launch_t<3, MODE_UP, ACT_NONE>(a, B, s);
+  if (ks == 3 && mode == MODE_UP && act == ACT_NONE) {
+    // sub-pixel: 2x2 taps per class at the source resolution (weights packed
+    // by launch_pack_conv_up); the template width is the SOURCE width
+    const bool w2 = a.Cout >= 128 && conv_wco_override() != 1;
+    switch (a.Ws) {
+      case 16: return w2 ? launch_p<2, MODE_UPP, ACT_NONE, 2, 16>(a, B, s) : launch_p<2, MODE_UPP, ACT_NONE, 1, 16>(a, B, s);
+      case 32: return w2 ? launch_p<2, MODE_UPP, ACT_NONE, 2, 32>(a, B, s) : launch_p<2, MODE_UPP, ACT_NONE, 1, 32>(a, B, s);
+      case 64: return w2 ? launch_p<2, MODE_UPP, ACT_NONE, 2, 64>(a, B, s) : launch_p<2, MODE_UPP, ACT_NONE, 1, 64>(a, B, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (ks == 1 && mode == MODE_S1 && act == ACT_NONE) return launch_t<1, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 1 && mode == MODE_S1 && act == ACT_GN) return launch_t<1, MODE_S1, ACT_GN>(a, B, s);
   return hipErrorInvalidValue;
@@ -420,7 +479,7 @@ size_t conv_packed_floats(int cin, int cout, int ks) {
   const int ck = conv_ck(ks);
   const size_t tiles = (size_t)((cout + 127) / 128) * 4;
   const size_t nchunk = (size_t)((cin + ck - 1) / ck);
-  return tiles * nchunk * (ks == 3 ? 9 * ck / 2 : ck / 2) * 64;
+  return tiles * nchunk * (ks == 3 ? 9 * ck / 2 : (ks == 2 ? 4 * ck / 2 : ck / 2)) * 64;
 }
 
 __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout, int ks,
@@ -445,6 +504,51 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout,
   float v = 0.f;
   if (co < cout && ci < cin) v = w[(((size_t)co * cin + ci) * ks + ky) * ks + kx];
   dst[i] = v;
+}
+
+// Upsample conv: W (Cout, Cin, 3, 3) -> 4 classes (pa, pb) of 2x2 taps in the
+// ks = 2 packed order ([class][co_tile32][chunk][step pair][lane][2]); tap
+// (ty, tx) of class (pa, pb) = sum of W[ky][kx] over ky in S(pa, ty), kx in
+// S(pb, tx), S(0,0) = {0}, S(0,1) = {1,2}, S(1,0) = {0,1}, S(1,1) = {2}
+size_t conv_packed_floats_up(int cin, int cout) { return 4 * conv_packed_floats(cin, cout, 2); }
+
+__global__ void pack_conv_up_kernel(const float* __restrict__ w, int cin, int cout, int nchunk,
+                                    size_t per_class, float* __restrict__ dst) {
+  const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= 4 * per_class) return;
+  const int cls = (int)(gi / per_class);
+  const size_t i = gi - (size_t)cls * per_class;
+  const int pa = cls >> 1, pb = cls & 1;
+  constexpr int ck = conv_ck(2), ch = ck / 2, spc = 4 * ch;
+  const int e = (int)(i & 1);
+  const int lane = (int)((i >> 1) & 63);
+  size_t rest = i >> 7;
+  const int sp = (int)(rest % (spc / 2));
+  rest /= (spc / 2);
+  const int k = (int)(rest % nchunk);
+  const int tile = (int)(rest / nchunk);
+  const int st = 2 * sp + e;
+  const int co = tile * 32 + (lane & 31);
+  const int ci = k * ck + (lane >> 5) * ch + st / 4;
+  const int ty = (st % 4) / 2, tx = st % 2;
+  float v = 0.f;
+  if (co < cout && ci < cin) {
+    const float* wk = w + ((size_t)co * cin + ci) * 9;
+    const int y0 = (pa == 0) ? (ty == 0 ? 0 : 1) : (ty == 0 ? 0 : 2);
+    const int y1 = (pa == 0) ? (ty == 0 ? 0 : 2) : (ty == 0 ? 1 : 2);
+    const int x0 = (pb == 0) ? (tx == 0 ? 0 : 1) : (tx == 0 ? 0 : 2);
+    const int x1 = (pb == 0) ? (tx == 0 ? 0 : 2) : (tx == 0 ? 1 : 2);
+    for (int ky = y0; ky <= y1; ++ky)
+      for (int kx = x0; kx <= x1; ++kx) v += wk[ky * 3 + kx];
+  }
+  dst[gi] = v;
+}
+
+hipError_t launch_pack_conv_up(const float* w, int cin, int cout, float* dst, hipStream_t s) {
+  const size_t per = conv_packed_floats(cin, cout, 2);
+  const int nchunk = (cin + conv_ck(2) - 1) / conv_ck(2);
+  pack_conv_up_kernel<<<(unsigned)((4 * per + 255) / 256), 256, 0, s>>>(w, cin, cout, nchunk, per, dst);
+  return hipGetLastError();
 }
 
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s) {
