@@ -568,7 +568,12 @@ def main():
                       "(GroupNorm statistics, dense and update kernels included: a lower bound)",
             "algorithmic_flop_per_step": conv_flop_step,
             "flop_basis": f"{flops['conv']} conv FLOP per sample-step ({a.unet}, counted per layer, "
-                          f"= torch FlopCounter) x {B} members"}
+                          f"= torch FlopCounter) x {B} members",
+            # the Upsample convs run sub-pixel (4 of 9 taps): the MFMA work done
+            "executed_flop_per_step": flops["conv_executed_fp32"] * B,
+            "executed_tflops": round(flops["conv_executed_fp32"] * B / (ev_s / a.steps) / 1e12, 3),
+            "executed_frac": round(flops["conv_executed_fp32"] * B / (ev_s / a.steps) / 1e12
+                                   / PEAK_FP32_TFLOPS, 4)}
     extra = {"unet_step_tflops_all": round(flops["total"] * B / step_s / 1e12 * world, 2),
              "unet_flop_per_sample_step": flops, "member_steps_per_s": round(value * B, 1)}
     cpu = None
