@@ -404,14 +404,18 @@ static hipError_t launch_g(const ConvArgs& a, int B, hipStream_t s) {
   return launch_gs<KS, MODE, ACT, WCO, WO, TPX, 1>(a, B, s);
 }
 
-// Wave tile 64 co x 32*TPX px.  TPX = 1 (half the pixels per workgroup, twice
-// the workgroups) when the TPX = 2 grid would leave CUs with fewer than 4
-// workgroups (the 16x16 / 32x32 levels at B = 64).
+// Wave tile 64 co x 32*TPX px: TPX = 2 (two 32-px accumulator pairs per wave,
+// each staged weight fragment feeds twice the MFMAs) for the 3x3 stride-1 and
+// sub-pixel convs; TPX = 1 (twice the workgroups, 5 waves/SIMD) for 1x1 and
+// stride 2, whose short K or strided staging cannot feed the larger tile.
 template <int KS, int MODE, int ACT, int WCO, int WO>
 static hipError_t launch_p(const ConvArgs& a, int B, hipStream_t s) {
   const long long wg2 = (long long)(WO * WO / (64 * (4 / WCO))) * ((a.Cout + 64 * WCO - 1) / (64 * WCO)) * B;
   int tpx = conv_tpx_override();
-  if (tpx == 0) tpx = 1;  // measured: TPX=1 (5 waves/SIMD) beats TPX=2 at every U2 layer
+  // measured per layer (U2 B=64, profiles/r01_unet_layers.txt era): TPX=2 wins
+  // for the 3x3 stride-1 and sub-pixel Upsample convs (32x32 level -7..-9 %,
+  // -270 us per step in all), TPX=1 for 1x1 (8x at 64x64) and stride 2
+  if (tpx == 0) tpx = ((KS == 3 && MODE == MODE_S1) || MODE == MODE_UPP) ? 2 : 1;
   (void)wg2;
   if constexpr (32 * (4 / WCO) >= WO) {
     if (tpx == 1) return launch_g<KS, MODE, ACT, WCO, WO, 1>(a, B, s);
