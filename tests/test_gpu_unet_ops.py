@@ -43,6 +43,9 @@ CASES = [  # (Ca, Cb, Cout, H, ks, mode, act)
     (128, 0, 128, 32, 3, "down", "none"),
     (128, 0, 128, 32, 3, "up", "none"),
     (256, 0, 256, 16, 3, "up", "none"),
+    (64, 0, 64, 64, 3, "up", "none"),            # 64 -> 128 (U5's last Upsample), 64-cout tiles
+    (20, 0, 40, 16, 3, "up", "none"),            # partial 8-channel chunk and cout tile
+    (20, 12, 40, 32, 3, "up", "none"),           # concatenated input through the sub-pixel path
     (192, 0, 64, 64, 1, "same", "none"),
     (384, 128, 256, 16, 1, "same", "none"),
     (256, 0, 768, 16, 1, "same", "gn"),          # attention qkv
@@ -72,6 +75,19 @@ def test_conv2d(Ca, Cb, Cout, H, ks, mode, act, precision, cuda_dev):
     ref = _ref_conv(xin, w, b, mode, act, gn, precision == "bf16")
     err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
     assert err < (1e-4 if precision == "bf16" else 1e-5), err
+
+
+def test_conv2d_up_epilogue(cuda_dev):
+    """Sub-pixel Upsample conv (fp32: 4 parity classes of 2x2 taps) with the
+    per-sample channel add and residual scattered to the right parity."""
+    B, C, H = 2, 64, 16
+    x, w, b = _rand((B, C, H, H), 30), _rand((C, C, 3, 3), 31, 0.04), _rand((C,), 32)
+    eb, res = _rand((B, C), 33), _rand((B, C, 2 * H, 2 * H), 34)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), mode="up",
+                 ebias=eb.to(cuda_dev), res=res.to(cuda_dev)).cpu()
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), w, b, padding=1)
+    ref = ref + eb[:, :, None, None] + res
+    assert RN.rel_l2(out.double().numpy(), ref.double().numpy()) < 1e-5
 
 
 def test_conv2d_epilogue(cuda_dev):
