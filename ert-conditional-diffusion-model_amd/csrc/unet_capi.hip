@@ -200,6 +200,11 @@ struct Walk {
   }
 
   float2* gnbuf = nullptr;
+  // plan capture only: a side stream (forked/joined with events) on which a
+  // ResBlock's 1x1 skip conv runs concurrently with its conv1 -- a branch of
+  // the step graph that fills conv1's tail
+  hipStream_t s2 = nullptr;
+  hipEvent_t evf = nullptr, evj = nullptr;
 
   // bf16: the statistics of a 3x3 GN+SiLU conv's input are computed by the
   // fused gn_act_bf16_kernel together with its bf16 image (one read of the
@@ -278,11 +283,23 @@ struct Walk {
     const int HW = Hh * Ww;
     const float* eb = ebias_all ? ebias_all + L->eboff.at(n) : nullptr;
     gn_stats(A, Ca, Bs, Cb, HW, n + ".norm1", true);
+    const bool skip = Ca + Cb != cout;
+    const bool side = skip && s2 && !dry;
+    if (side) {   // fork: the skip conv only needs the block input
+      chk(hipEventRecord(evf, s));
+      chk(hipStreamWaitEvent(s2, evf, 0));
+    }
     float* h1 = conv(n + ".conv1", 3, MODE_S1, ACT_GN_SILU, A, Ca, Bs, Cb, Hh, Ww, eb, nullptr);
     const float* resid = A;
-    if (Ca + Cb != cout) resid = conv(n + ".skip", 1, MODE_S1, ACT_NONE, A, Ca, Bs, Cb, Hh, Ww,
-                                      nullptr, nullptr);
+    if (skip) {
+      const hipStream_t s0 = s;
+      if (side) s = s2;
+      resid = conv(n + ".skip", 1, MODE_S1, ACT_NONE, A, Ca, Bs, Cb, Hh, Ww, nullptr, nullptr);
+      s = s0;
+      if (side) chk(hipEventRecord(evj, s2));
+    }
     gn_stats(h1, cout, nullptr, 0, HW, n + ".norm2", true);
+    if (side) chk(hipStreamWaitEvent(s, evj, 0));   // join before conv2 reads the residual
     return conv(n + ".conv2", 3, MODE_S1, ACT_GN_SILU, h1, cout, nullptr, 0, Hh, Ww, nullptr, resid);
   }
 
@@ -515,9 +532,13 @@ struct SampleCall {
     w.chk(launch_set_word(f.tdev, t_first, s));
     return rcode(w.err);
   }
-  int step(hipStream_t s) const {
+  int step(hipStream_t s, hipStream_t s2 = nullptr, hipEvent_t evf = nullptr,
+           hipEvent_t evj = nullptr) const {
     const Layout Lo = layout_with_freq(c);
     Walk w{c, &Lo, packed, (char*)ws, 0, B, s, false};
+    w.s2 = s2;
+    w.evf = evf;
+    w.evj = evj;
     const Fixed f = fixed(w, L);
     const int P = c->image * c->image;
     embed(w, f, nullptr);
@@ -535,6 +556,8 @@ struct ertd_unet_plan {
   ertd_unet_config cfg{};
   SampleCall call{};
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;            // skip-conv branch of the step graph
+  hipEvent_t evf = nullptr, evj = nullptr;
   hipGraph_t g_head = nullptr, g_step = nullptr;
   hipGraphExec_t x_head = nullptr, x_step = nullptr;
 };
@@ -752,10 +775,17 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
     return r;
   }
   hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+  // ERTD_UNET_SIDE=0 keeps the step graph a single chain (A/B)
+  const char* sv = getenv("ERTD_UNET_SIDE");
+  if (e == hipSuccess && (!sv || atoi(sv) != 0)) {
+    e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evf, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evj, hipEventDisableTiming);
+  }
   for (int k = 0; e == hipSuccess && k < 2; ++k) {
     e = hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal);
     if (e != hipSuccess) break;
-    r = k == 0 ? p->call.head(p->stream) : p->call.step(p->stream);
+    r = k == 0 ? p->call.head(p->stream) : p->call.step(p->stream, p->side, p->evf, p->evj);
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(p->stream, &g);
     (k == 0 ? p->g_head : p->g_step) = g;
@@ -786,6 +816,9 @@ int ertd_unet_plan_destroy(ertd_unet_plan* p) {
   if (p->g_head) (void)hipGraphDestroy(p->g_head);
   if (p->g_step) (void)hipGraphDestroy(p->g_step);
   if (p->stream) (void)hipStreamDestroy(p->stream);
+  if (p->side) (void)hipStreamDestroy(p->side);
+  if (p->evf) (void)hipEventDestroy(p->evf);
+  if (p->evj) (void)hipEventDestroy(p->evj);
   delete p;
   return ERTD_OK;
 }

@@ -56,9 +56,13 @@ def test_unet_sampler_vs_oracle(cuda_dev):
     assert err < 1e-4, err
 
 
-def test_unet_plan_matches_direct_and_deterministic(cuda_dev):
-    name, B, L, T = "U1", 2, 65, 6
-    m, _ = _pair(name, cuda_dev, seed=4)
+@pytest.mark.parametrize("name,precision,T", [("U1", "fp32", 6), ("U2", "fp32", 3),
+                                              ("U3", "bf16", 3)])
+def test_unet_plan_matches_direct_and_deterministic(name, precision, T, cuda_dev):
+    """The captured step graph (skip convs on a forked branch, fused bf16 GN
+    prologue) equals the eagerly launched sampler bit for bit."""
+    B, L = 2, 65
+    m = ertdiff.ConditionalUNet.from_config(name, seed=4, precision=precision).to(cuda_dev).eval()
     cond = torch.from_numpy(synth_uniform((B, 14, L), 105)).to(cuda_dev)
     sched = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
     P = m.param_dim
