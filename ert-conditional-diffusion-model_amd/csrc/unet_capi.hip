@@ -205,6 +205,7 @@ struct Walk {
   // the step graph that fills conv1's tail
   hipStream_t s2 = nullptr;
   hipEvent_t evf = nullptr, evj = nullptr;
+  hipEvent_t emb_join = nullptr;   // embedding branch not yet joined (first conv1 waits)
 
   // bf16: the statistics of a 3x3 GN+SiLU conv's input are computed by the
   // fused gn_act_bf16_kernel together with its bf16 image (one read of the
@@ -288,6 +289,10 @@ struct Walk {
     if (side) {   // fork: the skip conv only needs the block input
       chk(hipEventRecord(evf, s));
       chk(hipStreamWaitEvent(s2, evf, 0));
+    }
+    if (emb_join && !dry) {   // conv1's epilogue adds the embedding bias
+      chk(hipStreamWaitEvent(s, emb_join, 0));
+      emb_join = nullptr;
     }
     float* h1 = conv(n + ".conv1", 3, MODE_S1, ACT_GN_SILU, A, Ca, Bs, Cb, Hh, Ww, eb, nullptr);
     const float* resid = A;
@@ -533,7 +538,7 @@ struct SampleCall {
     return rcode(w.err);
   }
   int step(hipStream_t s, hipStream_t s2 = nullptr, hipEvent_t evf = nullptr,
-           hipEvent_t evj = nullptr) const {
+           hipEvent_t evj = nullptr, hipEvent_t eve = nullptr) const {
     const Layout Lo = layout_with_freq(c);
     Walk w{c, &Lo, packed, (char*)ws, 0, B, s, false};
     w.s2 = s2;
@@ -541,7 +546,18 @@ struct SampleCall {
     w.evj = evj;
     const Fixed f = fixed(w, L);
     const int P = c->image * c->image;
-    embed(w, f, nullptr);
+    if (s2 && eve) {
+      // the embedding dense layers run beside conv_in and the first norm1
+      w.chk(hipEventRecord(evf, s));
+      w.chk(hipStreamWaitEvent(s2, evf, 0));
+      w.s = s2;
+      embed(w, f, nullptr);
+      w.s = s;
+      w.chk(hipEventRecord(eve, s2));
+      w.emb_join = eve;
+    } else {
+      embed(w, f, nullptr);
+    }
     w.unet(x, f.ebias, f.eps);
     UpdateArgs u{x, f.eps, c1, c2, sigma, noise, num_steps, f.tdev, seed, member_offset, P};
     w.chk(launch_unet_update(u, B, s));
@@ -557,7 +573,7 @@ struct ertd_unet_plan {
   SampleCall call{};
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;            // skip-conv branch of the step graph
-  hipEvent_t evf = nullptr, evj = nullptr;
+  hipEvent_t evf = nullptr, evj = nullptr, eve = nullptr;
   hipGraph_t g_head = nullptr, g_step = nullptr;
   hipGraphExec_t x_head = nullptr, x_step = nullptr;
 };
@@ -781,11 +797,12 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
     e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evf, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evj, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->eve, hipEventDisableTiming);
   }
   for (int k = 0; e == hipSuccess && k < 2; ++k) {
     e = hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal);
     if (e != hipSuccess) break;
-    r = k == 0 ? p->call.head(p->stream) : p->call.step(p->stream, p->side, p->evf, p->evj);
+    r = k == 0 ? p->call.head(p->stream) : p->call.step(p->stream, p->side, p->evf, p->evj, p->eve);
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(p->stream, &g);
     (k == 0 ? p->g_head : p->g_step) = g;
@@ -819,6 +836,7 @@ int ertd_unet_plan_destroy(ertd_unet_plan* p) {
   if (p->side) (void)hipStreamDestroy(p->side);
   if (p->evf) (void)hipEventDestroy(p->evf);
   if (p->evj) (void)hipEventDestroy(p->evj);
+  if (p->eve) (void)hipEventDestroy(p->eve);
   delete p;
   return ERTD_OK;
 }
