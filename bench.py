@@ -74,6 +74,12 @@ def parse():
     ap.add_argument("--no-u3", action="store_true",
                     help="skip the configs[2] measurement (U3: + mid attention, B=256, bf16)")
     ap.add_argument("--no-kde", action="store_true", help="skip the KDE-mode measurement")
+    ap.add_argument("--ensemble", type=int, default=1024,
+                    help="members of the fixed configs[3] ensemble (sharded over the ranks)")
+    ap.add_argument("--ensemble-steps", type=int, default=10)
+    ap.add_argument("--no-ensemble", action="store_true", help="skip the configs[3] measurement")
+    ap.add_argument("--no-u5", action="store_true",
+                    help="skip the configs[4] measurement (U5 128x128, bf16, 64 members per GPU)")
     ap.add_argument("--no-reference", action="store_true",
                     help="skip the reference-model (R2) measurement in extra")
     ap.add_argument("--ref-steps", type=int, default=2000)
@@ -96,9 +102,13 @@ def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
     if world > 1:
+        # the RCCL communicator is created first (device_id: eager init on
+        # this rank's GPU), before any other GPU work of this process
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        print(f"[bench] rank {rank}: RCCL world size {dist.get_world_size()}", file=sys.stderr,
+              flush=True)
+    torch.cuda.set_device(local)
     return rank, world, torch.device("cuda", local)
 
 
@@ -263,6 +273,22 @@ def train_bench(dev, steps=200, B=32, T=500):
             "train_ms_per_step": round(el / steps * 1e3, 4), "train_final_loss": round(float(loss), 5)}
 
 
+def _host_cpus():
+    """(CPU model, CPUs this process may run on, threads used = min(OMP_NUM_THREADS, that))."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", aff)), aff))
+    return model, aff, threads
+
+
 def _tune_cpu_allocator():
     """Give the CPU baseline its best case: glibc's default mmap threshold
     makes every fresh multi-MB conv output an mmap + page-fault zero-fill, so
@@ -281,7 +307,7 @@ def _tune_cpu_allocator():
 def cpu_train_baseline(seconds, B=32, T=500):
     from oracle import ref_torch as RT
     _tune_cpu_allocator()
-    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    cpu_model, affinity, threads = _host_cpus()
     torch.set_num_threads(threads)
     torch.manual_seed(42)
     W = {k: v.detach() for k, v in ertdiff.ConditionalDiffusionModel(P, 128).state_dict().items()}
@@ -307,7 +333,7 @@ def cpu_baseline(seconds, B, T, mode):
     bit-identical to ERT_Conditional_Diffusion.py's sample_model), bounded."""
     from oracle import ref_torch as RT
     _tune_cpu_allocator()
-    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    cpu_model, affinity, threads = _host_cpus()
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(1042)
     cond = torch.rand(B, 14, L_MEAS, generator=g)
@@ -324,7 +350,7 @@ def cpu_baseline(seconds, B, T, mode):
     RT.sample(cond, W, T, noise, encoder_every_step=not hoist, max_steps=n)
     el = time.perf_counter() - t0
     return {"value": round(n / el, 3), "unit": "denoising-steps/sec", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model, "affinity_cpus": affinity,
             "sample": f"{n} of {T} steps of the reference sampler ({'hoisted' if hoist else 'faithful'}), "
                       f"B={B}, cond (B,14,{L_MEAS}) fp32, torch {torch.__version__} CPU, {threads} threads",
             "seconds": round(el, 2)}
@@ -397,7 +423,7 @@ def cpu_unet_baseline(name, seconds, B, T):
     """The U-Net spec (oracle/unet_torch.py) on PyTorch-CPU, bounded sample."""
     from oracle import unet_torch as U
     _tune_cpu_allocator()
-    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    cpu_model, affinity, threads = _host_cpus()
     torch.set_num_threads(threads)
     cfg = U.CONFIGS[name]
     W = U.init_weights(cfg, 0)
@@ -419,11 +445,50 @@ def cpu_unet_baseline(name, seconds, B, T):
     U.sample(cond, W, cfg, T, noise, max_steps=n)
     el = time.perf_counter() - t0
     return {"value": round(n / el, 4), "unit": "denoising-steps/sec", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model, "affinity_cpus": affinity,
             "sample": f"{n} of {T} steps of sample_model around the U-Net spec "
                       f"(oracle/unet_torch.py, {name}), B={B}, cond (B,14,{L_MEAS}) fp32, "
                       f"torch {torch.__version__} CPU, {threads} threads",
             "seconds": round(el, 2)}
+
+
+def time_unet(model, cond, B, steps, warmup, T, seed, offset, world, dev, shared=False):
+    """One UNetSamplerPlan of `steps` reverse steps from t = T-1.  Warmup runs
+    `warmup` steps through the SAME plan (so its graphs are uploaded before
+    timing), x is reset to x_T, then the timed replay sits between barrier +
+    synchronize on both sides; HIP events on the launching stream beside the
+    host clock.  Returns (host seconds max over ranks, event seconds, plan)."""
+    sched = ertdiff.get_diffusion_schedule(T, device=dev)
+    x_T = ertdiff.philox_normal(B, model.param_dim, T, 1, seed, offset, dev)
+    plan = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=steps, seed=seed,
+                                   member_offset=offset, B=B, shared_condition=shared)
+    left = max(1, warmup)
+    while left > 0:
+        n = min(left, steps)
+        plan.x.copy_(x_T)
+        plan.launch(n_steps=n)
+        left -= n
+    plan.x.copy_(x_T)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    plan.launch(stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    ev_s = e0.elapsed_time(e1) * 1e-3
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    if not torch.isfinite(plan.x).all():
+        raise RuntimeError("U-Net sampler produced non-finite values")
+    return el, ev_s, plan
 
 
 def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev):
@@ -436,37 +501,51 @@ def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev):
     cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
     if world > 1:
         dist.broadcast(cond, src=0)
-    sched = ertdiff.get_diffusion_schedule(T, device=dev)
-    offset = rank * B
-    x_T = ertdiff.philox_normal(B, model.param_dim, T, 1, 2043, offset, dev)
-    timed = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=steps,
-                                    seed=2043, member_offset=offset)
-    warm = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=max(1, warmup),
-                                   seed=2043, member_offset=offset)
-    warm.x.copy_(x_T)
-    warm.launch()
-    timed.x.copy_(x_T)
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    t0 = time.perf_counter()
-    timed.launch(torch.cuda.current_stream(dev))
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    el = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        el = float(e.item())
-    if not torch.isfinite(timed.x).all():
-        raise RuntimeError(f"{name} sampler produced non-finite values")
+    el, ev_s, plan = time_unet(model, cond, B, steps, warmup, T, 2043, rank * B, world, dev)
+    del plan
     step_s = el / steps
     conv_tf = fl["conv"] * B / step_s / 1e12
     peak = PEAK_FP32_TFLOPS if precision == "fp32" else PEAK_BF16_TFLOPS
-    return {"config": f"{name} B={B} {precision} T={T}", "value": round(world * steps / el, 3),
-            "unit": "denoising-steps/sec", "ms_per_step": round(step_s * 1e3, 4),
+    return {"config": f"{name} B={B} per GPU, {precision}, T={T}", "value": round(world * steps / el, 3),
+            "unit": "denoising-steps/sec", "scaling": "weak", "ms_per_step": round(step_s * 1e3, 4),
             "conv_tflops": round(conv_tf, 2), "conv_peak_tflops": peak,
             "conv_frac": round(conv_tf / peak, 4), "steps": steps, "warmup": warmup,
-            "member_steps_per_s": round(world * steps / el * B, 1)}
+            "member_steps_per_s": round(world * steps / el * B, 1),
+            "gflop_per_sample_step": round(fl["total"] / 1e9, 3)}
+
+
+def bench_ensemble(n_members, name, steps, warmup, T, rank, world, dev):
+    """BASELINE configs[3]: ONE fixed conditioned ensemble of n_members
+    realisations (the reference's realisation loops :394-410 / :1036-1086
+    batched), sharded over the ranks by member_range (strong scaling): rank 0
+    broadcasts the single (1, 14, 4693) condition (the one RCCL collective), every
+    rank samples its member range reading that condition in place (stride 0)
+    with Philox noise keyed by the global member id; nothing is gathered inside
+    the timed region (each rank keeps its shard).  value = reverse
+    steps of the WHOLE ensemble per second (max time over ranks)."""
+    from ertdiff.ensemble import member_range
+    model = ertdiff.ConditionalUNet.from_config(name, seed=0).to(dev).eval()
+    if rank == 0:
+        g = torch.Generator(device=dev).manual_seed(1044)
+        cond = torch.rand(1, 14, L_MEAS, device=dev, generator=g)
+    else:
+        cond = torch.empty(1, 14, L_MEAS, device=dev)
+    if world > 1:
+        dist.broadcast(cond, src=0)
+    lo, hi = member_range(n_members, world, rank)
+    el, ev_s, plan = time_unet(model, cond, hi - lo, steps, warmup, T, 2044, lo, world, dev,
+                               shared=True)
+    del plan
+    value = steps / el
+    return {"config": f"{name} fp32, one condition, {n_members}-member ensemble sharded over "
+                      f"{world} GPU(s), T={T} (BASELINE configs[3])",
+            "value": round(value, 3), "unit": "denoising-steps/sec (whole ensemble)",
+            "scaling": "strong", "member_steps_per_s": round(value * n_members, 1),
+            "ms_per_step": round(el / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "rccl_world_size": world,
+            "member_ranges": [list(member_range(n_members, world, r)) for r in range(world)],
+            "collectives": "1 x broadcast of the (1,14,4693) fp32 condition (262,808 B) before "
+                           "timing; no gather"}
 
 
 def bench_kde(dev, world, rank, n=100, cells=4693 * 14, grid=5000, reps=3, cpu_cells=300,
@@ -521,40 +600,12 @@ def main():
     spec = CONFIGS[a.unet]
     flops = unet_flops(**spec)
     model = ertdiff.ConditionalUNet.from_config(a.unet, seed=0).to(dev).eval()
-    Pu = model.param_dim
     g = torch.Generator(device=dev).manual_seed(1042)
     cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
     if world > 1:
         dist.broadcast(cond, src=0)      # the one collective on the data path
-    sched = ertdiff.get_diffusion_schedule(T, device=dev)
     offset = rank * B
-    x_T = ertdiff.philox_normal(B, Pu, T, 1, 2042, offset, dev)
-    timed = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1, n_run=a.steps,
-                                    seed=2042, member_offset=offset)
-    warm = ertdiff.UNetSamplerPlan(model, cond, T, *sched, t_first=T - 1,
-                                   n_run=max(1, a.warmup), seed=2042, member_offset=offset)
-    warm.x.copy_(x_T)
-    warm.launch()                        # graph upload + warmup steps
-    timed.x.copy_(x_T)
-    stream = torch.cuda.current_stream(dev)
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    timed.launch(stream)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    el = time.perf_counter() - t0
-    ev_s = e0.elapsed_time(e1) * 1e-3
-    if world > 1:
-        e = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        el = float(e.item())
-    if not torch.isfinite(timed.x).all():
-        raise RuntimeError("U-Net sampler produced non-finite values")
+    el, ev_s, timed = time_unet(model, cond, B, a.steps, a.warmup, T, 2042, offset, world, dev)
     value = world * a.steps / el
     step_s = el / a.steps
     conv_flop_step = flops["conv"] * B
@@ -580,9 +631,14 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_unet_baseline(a.unet, a.cpu_unet_seconds, B, T)
         extra["vs_cpu_baseline"] = round(value / cpu["value"], 1)
-    del timed, warm
+    del timed
     if not a.no_u3:
         extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev)
+    if not a.no_ensemble:
+        extra["configs3_ensemble"] = bench_ensemble(a.ensemble, "U2", a.ensemble_steps, 2, T, rank,
+                                                    world, dev)
+    if not a.no_u5:
+        extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev)
     if not a.no_kde:
         extra["kde_mode"] = bench_kde(dev, world, rank, cpu=not a.no_cpu_baseline)
     if not a.no_reference:

@@ -818,12 +818,17 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
   return ERTD_OK;
 }
 
-int ertd_unet_plan_launch(ertd_unet_plan* p, void* stream) {
-  if (!p || !p->x_head || !p->x_step) return ERTD_EINVAL;
+int ertd_unet_plan_launch_steps(ertd_unet_plan* p, int n_steps, void* stream) {
+  if (!p || !p->x_head || !p->x_step || n_steps < 0 || n_steps > p->call.n_run) return ERTD_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipGraphLaunch(p->x_head, s);
-  for (int i = 0; e == hipSuccess && i < p->call.n_run; ++i) e = hipGraphLaunch(p->x_step, s);
+  for (int i = 0; e == hipSuccess && i < n_steps; ++i) e = hipGraphLaunch(p->x_step, s);
   return rcode(e);
+}
+
+int ertd_unet_plan_launch(ertd_unet_plan* p, void* stream) {
+  if (!p) return ERTD_EINVAL;
+  return ertd_unet_plan_launch_steps(p, p->call.n_run, stream);
 }
 
 int ertd_unet_plan_destroy(ertd_unet_plan* p) {

@@ -60,15 +60,17 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(GnArgs a) {
     red[1][tid >> 6] = ss;
   }
   __syncthreads();
-  if (tid < cpg) {
-    const double n = (double)cpg * HW;
-    const double S = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    const double SS = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-    const double mean = S / n;
-    double var = SS / n - mean * mean;
-    var = var > 0.0 ? var : 0.0;
-    const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
-    const int c = g * cpg + tid;
+  const double n = (double)cpg * HW;
+  const double S = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  const double SS = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  const double mean = S / n;
+  double var = SS / n - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
+  // a group may hold more channels than the workgroup has threads (groups=1
+  // at C=512): every channel of the group gets its {scale, shift}
+  for (int cl = tid; cl < cpg; cl += 256) {
+    const int c = g * cpg + cl;
     const float scale = rstd * a.gamma[c];
     const float shift = -scale * (float)mean + a.beta[c];
     a.out[(size_t)b * C + c] = make_float2(scale, shift);

@@ -91,6 +91,7 @@ SIGNATURES = {
                                           _VP, _VP, _VP, _VP, _U64, _U32, _VP, _VP, _SZ,
                                           ctypes.POINTER(_VP)]),
     "ertd_unet_plan_launch": (_I, [_VP, _VP]),
+    "ertd_unet_plan_launch_steps": (_I, [_VP, _I, _VP]),
     "ertd_unet_plan_destroy": (_I, [_VP]),
     "ertd_plan_launch": (_I, [_VP, _VP]),
     "ertd_plan_destroy": (_I, [_VP]),

@@ -11,7 +11,11 @@ so the ensemble shards with no exchange on the data path.  One process per GPU
      reading the shared condition in place (stride 0) with Philox noise keyed
      by the GLOBAL member id, so the ensemble is bitwise identical for any
      world size;
-  3. optionally one all_gather returns the (n_members, P) result to all ranks.
+  3. each rank returns its own shard (hi-lo, P) on its device; the caller
+     copies it to the host (per-device D2H) and concatenates by member_range
+     -- no gather collective.  ``gather=True`` is an opt-in
+     convenience that adds one all_gather AFTER sampling, for callers that
+     want the whole ensemble on every rank.
 """
 from __future__ import annotations
 
@@ -73,13 +77,14 @@ def gather_members(local: torch.Tensor, n_members: int, group=None) -> torch.Ten
 def sample_ensemble(model, condition: Optional[torch.Tensor], n_members: int, T: int, betas,
                     alphas, alpha_bar, *, seed: int, num_steps=None, temperature: float = 1.0,
                     mode: str = "hoisted", L: Optional[int] = None, device=None, group=None,
-                    gather: bool = True,
+                    gather: bool = False,
                     _sampler: Optional[Callable] = None) -> torch.Tensor:
     """n_members realisations x_0 (unconstrained space) for ONE condition.
 
     condition: (14, L) or (1, 14, L) on the source rank (others may pass None
-    and give L).  Returns (n_members, P) on every rank if ``gather`` else this
-    rank's (hi-lo, P) shard.  ``_sampler`` replaces the device sampler in the
+    and give L).  Returns this rank's (hi-lo, P) shard (global members
+    member_range(n_members, world, rank)); with ``gather=True`` (opt-in, one
+    all_gather after sampling) the whole (n_members, P) ensemble on every rank.  ``_sampler`` replaces the device sampler in the
     CPU (gloo) tests of this host logic; the product always uses
     ertdiff.sample_model.
     """

@@ -148,7 +148,8 @@ def sample_model(model, condition, T, betas, alphas, alpha_bar, param_dim, devic
         return sample_unet(model, condition, T, betas, alphas, alpha_bar, param_dim, device,
                            num_steps, temperature, noise=noise, seed=seed,
                            member_offset=member_offset, shared_condition=shared_condition,
-                           n_members=n_members)
+                           n_members=n_members, precision=precision,
+                           mode=None if mode == "hoisted" else mode)
     if mode not in _MODES:
         raise ValueError(f"mode must be one of {list(_MODES)}")
     dev = _lib.require_device(condition)

@@ -274,10 +274,19 @@ class _UPrepared:
 def sample_unet(model: ConditionalUNet, condition, T, betas, alphas, alpha_bar, param_dim, device,
                 num_steps=None, temperature=1.0, *, noise: Union[str, torch.Tensor] = "torch",
                 seed: int = 0, member_offset: int = 0, shared_condition: bool = False,
-                n_members: Optional[int] = None, **_ignored):
+                n_members: Optional[int] = None, precision: Optional[str] = None,
+                mode: Optional[str] = None):
     """sample_model (ERT_Conditional_Diffusion.py:102-119) with the U-Net
-    denoiser: same signature, same noise options as ertdiff.sample_model."""
+    denoiser: same signature, same noise options as ertdiff.sample_model.
+    ``precision`` must be None or the model's own (ConditionalUNet.set_precision
+    changes it); ``mode`` is a reference-model option: the U-Net has a single
+    schedule, so anything but None raises instead of being ignored."""
     from .sampler import draw_reference_noise, philox_normal
+    if precision is not None and precision != model.precision:
+        raise RuntimeError(f"ertdiff: precision={precision!r} but the U-Net runs {model.precision!r}; "
+                           "call model.set_precision() first")
+    if mode is not None:
+        raise RuntimeError(f"ertdiff: mode={mode!r} applies to ConditionalDiffusionModel only")
     if model.param_dim != param_dim:
         raise RuntimeError(f"ertdiff: param_dim={param_dim} but the U-Net predicts {model.param_dim}")
     prep = _UPrepared(model, condition, T, betas, alphas, alpha_bar, num_steps, temperature,
@@ -328,7 +337,13 @@ class UNetSamplerPlan:
         self.B = B if B is not None else self.prep.cond.shape[0]
         self.noise = None if noise is None else _lib.f32c(noise, "noise")
         self.x = torch.zeros(self.B, model.param_dim, dtype=torch.float32, device=dev)
-        self.ws = model.workspace(dev, self.B, self.prep.L)
+        # a workspace of its own (step counter, eps, embedding biases, every
+        # activation): a plan launched on another stream never races the
+        # model's eager calls or another plan
+        nbytes = _lib.lib().ertd_unet_workspace_bytes(ctypes.byref(model.cfg), self.B, self.prep.L)
+        if nbytes == 0:
+            raise RuntimeError("ertdiff: unsupported U-Net configuration")
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         self._plan = ctypes.c_void_p()
         with torch.cuda.device(dev):
             _lib.check(_lib.lib().ertd_unet_sample_plan_create(
@@ -336,10 +351,15 @@ class UNetSamplerPlan:
                                 self.n_run, self.ws), ctypes.byref(self._plan)),
                 "unet_sample_plan_create")
 
-    def launch(self, stream: Optional[torch.cuda.Stream] = None):
+    def launch(self, stream: Optional[torch.cuda.Stream] = None, n_steps: Optional[int] = None):
+        """Replays the head graph and n_run steps (or only the first n_steps)."""
         s = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
         with torch.cuda.device(self.dev):
-            _lib.check(_lib.lib().ertd_unet_plan_launch(self._plan, s), "unet_plan_launch")
+            if n_steps is None:
+                _lib.check(_lib.lib().ertd_unet_plan_launch(self._plan, s), "unet_plan_launch")
+            else:
+                _lib.check(_lib.lib().ertd_unet_plan_launch_steps(self._plan, int(n_steps), s),
+                           "unet_plan_launch_steps")
 
     def close(self):
         if self._plan:

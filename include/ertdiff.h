@@ -310,6 +310,9 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* cfg, const float* packe
                                  const float* noise, uint64_t seed, uint32_t member_offset,
                                  float* x_inout, void* ws, size_t ws_bytes, ertd_unet_plan** plan);
 int ertd_unet_plan_launch(ertd_unet_plan* plan, void* stream);
+/* head + the first n_steps (0 <= n_steps <= n_run) steps only: warms both
+ * graphs (first-launch upload) without running the whole plan.            */
+int ertd_unet_plan_launch_steps(ertd_unet_plan* plan, int n_steps, void* stream);
 int ertd_unet_plan_destroy(ertd_unet_plan* plan);
 
 /* ---- Ensemble KDE mode (csrc/kde.hip) -------------

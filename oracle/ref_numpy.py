@@ -201,9 +201,11 @@ def train_steps(W0: Weights, x0, cond, T, ts, noises, lr=1e-4):
     return losses, grads0, params
 
 
-def sample(cond, W: Weights, T: int, noise, num_steps=None, temperature=1.0, alphas32=True):
+def sample(cond, W: Weights, T: int, noise, num_steps=None, temperature=1.0, alphas32=True,
+           max_steps=None):
     """sample_model :102-119 with injected noise in float64.  ``alphas32`` uses
-    the reference's float32 schedule values (so only arithmetic differs)."""
+    the reference's float32 schedule values (so only arithmetic differs);
+    ``max_steps`` stops after that many reverse steps (first steps of a chain)."""
     if alphas32:
         betas = np.linspace(1e-4, 0.02, T, dtype=np.float32).astype(np.float64)
         betas32 = np.linspace(1e-4, 0.02, T, dtype=np.float32)
@@ -216,7 +218,9 @@ def sample(cond, W: Weights, T: int, noise, num_steps=None, temperature=1.0, alp
     cond = np.asarray(cond, np.float64)
     B = cond.shape[0]
     x = noise[0].copy()
-    for t_ in reversed(range(n)):
+    for i, t_ in enumerate(reversed(range(n))):
+        if max_steps is not None and i >= max_steps:
+            break
         pred = forward_full(x, np.full(B, t_), cond, W)["out"]
         coef = (1 - alphas[t_]) / (math.sqrt(1 - alpha_bar[t_]) + 1e-8)
         x = (1.0 / math.sqrt(alphas[t_])) * (x - coef * pred)

@@ -221,11 +221,14 @@ def forward(x, t, cond, W: Weights, cfg: UNetConfig, return_emb: bool = False, b
 
 @torch.no_grad()
 def sample(cond, W: Weights, cfg: UNetConfig, T: int, noise, num_steps=None, temperature=1.0,
-           max_steps=None):
+           max_steps=None, bf16: bool = False, record=()):
     """sample_model (ERT_Conditional_Diffusion.py:102-119) around this U-Net, with
     injected noise (noise[0] = x_T, noise[k] = z for t = n-k) and the same
     float64-scalar update expressions.  ``max_steps`` stops early (bounded
-    CPU-baseline samples)."""
+    CPU-baseline samples); ``bf16`` = the bf16-operand convs of the HIP
+    path's bf16 precision; ``record`` = step counts after which x is kept
+    (returns (x, {count: x})).  noise[k] may also be a callable's product:
+    anything indexable by k."""
     betas = torch.linspace(1e-4, 0.02, T)
     alphas = 1.0 - betas
     alpha_bar = torch.cumprod(alphas, dim=0)
@@ -233,17 +236,20 @@ def sample(cond, W: Weights, cfg: UNetConfig, T: int, noise, num_steps=None, tem
     B = cond.shape[0] if noise is None else noise.shape[1]
     x = noise[0].clone()
     done = 0
+    kept = {}
     for t_ in reversed(range(n)):
         if max_steps is not None and done >= max_steps:
             break
         done += 1
         tt = torch.full((B,), t_, dtype=torch.long)
-        pred = forward(x, tt, cond, W, cfg)
+        pred = forward(x, tt, cond, W, cfg, bf16=bf16)
         coef = (1 - alphas[t_]) / (math.sqrt(1 - alpha_bar[t_]) + 1e-8)
         x = (1.0 / math.sqrt(alphas[t_])) * (x - coef * pred)
         if t_ > 0:
             x = x + math.sqrt(betas[t_]) * temperature * noise[n - t_]
-    return x
+        if done in record:
+            kept[done] = x.clone()
+    return (x, kept) if record else x
 
 
 def init_weights(cfg: UNetConfig, seed: int = 0) -> Weights:

@@ -76,3 +76,21 @@ def gpu_model(golden_weights, cuda_dev):
 @pytest.fixture(scope="session")
 def kde_kat():
     return load_golden("kde_kat.npz")
+
+
+@pytest.fixture(scope="session")
+def unet_sampler_kat():
+    return load_golden("unet_sampler_kat.npz")
+
+
+def record_error(name: str, value: float) -> None:
+    """Append a measured parity error to gpurun_out/parity_errors.jsonl (the
+    numbers DESIGN.md quotes next to each gate); never fails a test."""
+    import json
+    try:
+        d = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "parity_errors.jsonl"), "a") as f:
+            f.write(json.dumps({"test": name, "value": float(value)}) + "\n")
+    except OSError:
+        pass

@@ -6,6 +6,7 @@ broadcast and the gather -- not numerics (those are in test_gpu_parity)."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -45,28 +46,38 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, n_members, q):
+class _UNetLike:
+    """Stand-in with the U-Net's (B, image^2) state shape."""
+    image = 4
+    param_dim = 16
+
+
+def _worker(rank, world, port, n_members, q, model_kind="mlp"):
+    model = _UNetLike() if model_kind == "unet" else _Model()
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         L = 37
         cond = torch.arange(14 * L, dtype=torch.float32).reshape(14, L) / 100 if rank == 0 else None
-        out = sample_ensemble(_Model(), cond, n_members, 10, None, None, None, seed=3, L=L,
-                              device=torch.device("cpu"), _sampler=fake_sampler)
-        shard = sample_ensemble(_Model(), cond, n_members, 10, None, None, None, seed=3, L=L,
-                                device=torch.device("cpu"), gather=False, _sampler=fake_sampler)
-        q.put((rank, out.numpy(), shard.shape[0]))
+        out = sample_ensemble(model, cond, n_members, 10, None, None, None, seed=3, L=L,
+                              device=torch.device("cpu"), gather=True, _sampler=fake_sampler)
+        # default: no gather collective, each rank returns its own shard
+        shard = sample_ensemble(model, cond, n_members, 10, None, None, None, seed=3, L=L,
+                                device=torch.device("cpu"), _sampler=fake_sampler)
+        q.put((rank, out.numpy(), shard.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_members", [(2, 16), (2, 7), (3, 10)])
-def test_sharded_ensemble_gloo(world, n_members):
+@pytest.mark.parametrize("world,n_members,kind", [(2, 16, "mlp"), (2, 7, "mlp"), (3, 10, "mlp"),
+                                                 (2, 1024, "unet")])
+def test_sharded_ensemble_gloo(world, n_members, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_members, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_members, q, kind))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -75,10 +86,15 @@ def test_sharded_ensemble_gloo(world, n_members):
         assert p.exitcode == 0
     L = 37
     cond = torch.arange(14 * L, dtype=torch.float32).reshape(1, 14, L) / 100
-    expect = fake_sampler(_Model(), cond, 10, None, None, None, 5, None, num_steps=None,
+    P = (_UNetLike if kind == "unet" else _Model).param_dim
+    expect = fake_sampler(_Model(), cond, 10, None, None, None, P, None, num_steps=None,
                           temperature=1.0, mode="hoisted", noise="philox", seed=3,
                           member_offset=0, shared_condition=True, n_members=n_members).numpy()
-    for rank, out, nloc in sorted(res, key=lambda r: r[0]):
+    shards = []
+    for rank, out, shard in sorted(res, key=lambda r: r[0]):
         assert (out == expect).all(), f"rank {rank} gathered ensemble differs from the unsharded one"
         lo, hi = member_range(n_members, world, rank)
-        assert nloc == hi - lo
+        assert shard.shape == (hi - lo, P)
+        shards.append(shard)
+    # host concatenation of the per-rank shards (the default, collective-free return)
+    assert (np.concatenate(shards) == expect).all()

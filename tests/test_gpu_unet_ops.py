@@ -111,9 +111,12 @@ def test_conv2d_out_epilogue(cuda_dev):
     assert RN.rel_l2(out.double().numpy(), ref.double().numpy()) < 1e-5
 
 
-@pytest.mark.parametrize("Ca,Cb,H", [(64, 0, 64), (256, 128, 16), (128, 64, 32)])
-def test_group_norm_stats(Ca, Cb, H, cuda_dev):
-    B, G = 3, 32
+@pytest.mark.parametrize("Ca,Cb,H,G", [(64, 0, 64, 32), (256, 128, 16, 32), (128, 64, 32, 32),
+                                        (512, 0, 16, 1), (256, 256, 16, 1), (384, 0, 16, 2)])
+def test_group_norm_stats(Ca, Cb, H, G, cuda_dev):
+    """G = 1 / 2: groups wider than the 256-thread workgroup (every channel of
+    the group still gets its {scale, shift})."""
+    B = 3
     x = _rand((B, Ca, H, H), 12, 2.0) + 0.5
     x2 = _rand((B, Cb, H, H), 13) if Cb else None
     gamma, beta = _rand((Ca + Cb,), 14) + 1, _rand((Ca + Cb,), 15)

@@ -198,3 +198,29 @@ def test_unet_flop_count_matches_torch(name):
     enc_97 = 2 * 14 * 3 * 32 * 49 + 2 * 32 * 3 * 64 * 25 + 2 * 64 * 128  # encoder at L=97
     f = unet_flops(**CONFIGS[name])
     assert f["total"] - f["condition_encoder"] + enc_97 == fc.get_total_flops()
+
+
+def test_unet_sampler_rejects_conflicting_options():
+    """sample_model on a ConditionalUNet raises (before any device work) when
+    asked for a precision the model does not run or a reference-model mode,
+    instead of silently ignoring them."""
+    m = ertdiff.ConditionalUNet.from_config("U1", seed=0)
+    sched = ertdiff.get_diffusion_schedule(4)
+    cond = torch.zeros(1, 14, 9)
+    with pytest.raises(RuntimeError, match="precision"):
+        ertdiff.sample_model(m, cond, 4, *sched, 1024, "cpu", precision="bf16")
+    with pytest.raises(RuntimeError, match="mode"):
+        ertdiff.sample_model(m, cond, 4, *sched, 1024, "cpu", mode="faithful")
+
+
+def test_unet_sampler_golden_fixture_shape(unet_sampler_kat):
+    """tests/golden/unet_sampler_kat.npz (make_unet_golden.py): the full T = 1000
+    chains the GPU tests replay; the bf16-operand spec stays within 2e-3 of the
+    fp32 spec at every recorded step (the budget's basis)."""
+    kat = unet_sampler_kat
+    assert int(kat["T"]) == 1000 and list(kat["record"]) == [1, 10, 100, 500, 1000]
+    for r in kat["record"]:
+        a = kat[f"u3_bf16_x{r}"].astype(np.float64)
+        b = kat[f"u3_fp32_x{r}"].astype(np.float64)
+        assert np.isfinite(a).all() and np.isfinite(b).all()
+        assert np.linalg.norm(a - b) / np.linalg.norm(b) < 2e-3
