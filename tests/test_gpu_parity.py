@@ -246,9 +246,9 @@ def encoder_bf16_oracle(cond, W):
     weights and the conv1 activation rounded to bf16, everything else exact."""
     w = {k: np.asarray(v, np.float64) for k, v in W.items()}
     h = np.maximum(RN.conv1d_s2(_bf16(cond), _bf16(w["condition_encoder.0.weight"]),
-                                w["condition_encoder.0.bias"]), 0)
+                                w["condition_encoder.0.bias"])[0], 0)
     h = np.maximum(RN.conv1d_s2(_bf16(h), _bf16(w["condition_encoder.2.weight"]),
-                                w["condition_encoder.2.bias"]), 0)
+                                w["condition_encoder.2.bias"])[0], 0)
     m = h.mean(axis=2)
     return np.maximum(m @ w["condition_encoder.6.weight"].T + w["condition_encoder.6.bias"], 0)
 

@@ -53,7 +53,10 @@ SAMPLER_TOL = 1e-4
 # operand rounding, another fp32 summation order: flips of single bf16
 # roundings cascade through ~40 convs per step and 1000 steps) and against the
 # fp32 spec (the price of bf16 operands itself).
-BF16_SAMPLER_TOL = {"bf16_spec": 5e-3, "fp32_spec": 5e-3}
+# measured: 1.5e-4 vs the bf16 spec and 1.5e-3 vs the fp32 spec
+# at step 1000 -- the latter is the spec-vs-spec gap itself (1.5e-3,
+# test_host.test_unet_sampler_golden_fixture_shape)
+BF16_SAMPLER_TOL = {"bf16_spec": 1e-3, "fp32_spec": 3e-3}
 
 
 def _run_golden_chain(kat, key, dev):
@@ -192,5 +195,6 @@ def test_unet_bf16_forward(name, B, L, ts, cuda_dev):
     # only in order still drift apart by a fraction of the bf16-vs-fp32 gap
     # (rounding flips cascade); per-operator tightness is tested in
     # test_gpu_unet_ops.py.
-    assert e16 < 2e-2, e16
-    assert e32 < 3e-2, e32
+    # measured 4.6e-3..6.0e-3 vs the bf16 spec, 6.4e-3..8.5e-3 vs fp32 (U1/U3/U5)
+    assert e16 < 1.2e-2, e16
+    assert e32 < 1.6e-2, e32
