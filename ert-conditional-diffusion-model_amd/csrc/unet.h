@@ -41,6 +41,8 @@ struct ConvArgs {
   void* bimg;            // bf16 3x3 GN / Upsample convs: scratch for the pre-transformed
                          // input, conv_bf16_image_bytes(Cin, B, Ho, Wo) bytes (null: stage fp32)
   int bimg_ready;        // 1: bimg already holds the transformed input (launch_gn_act_bf16)
+  const float* wpk_wino; // fp32 3x3 stride-1: Winograd-transformed weights (launch_pack_conv_wino)
+                         // or null (direct implicit GEMM)
 };
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
@@ -54,6 +56,13 @@ hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, floa
 // Cout = 1, 3x3 stride 1 (conv_out; unet_conv_out.hip): per-pixel fp32 fma
 // chains, weights read from either packing (bf16: staged input rounded too)
 hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStream_t s);
+// fp32 3x3 stride-1 convs by Winograd F(2x2,3x3) (unet_conv_wino.hip): eligible
+// shapes (Cin, Ca multiples of 8, Cout of 64, W in 16..128; ERTD_UNET_WINO=0
+// disables), the U = G g G^T packing (0 floats: shape not eligible), launch
+hipError_t launch_conv_wino(int act, const ConvArgs& a, int B, hipStream_t s);
+bool conv_wino_ok(int cin, int ca, int cout, int wo);
+size_t conv_packed_floats_wino(int cin, int cout);
+hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s);
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s);

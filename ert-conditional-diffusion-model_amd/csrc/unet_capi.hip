@@ -8,6 +8,7 @@
 // the caller's ws), so a whole step can be captured into a hipGraph.
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <map>
 #include <string>
@@ -137,6 +138,7 @@ constexpr size_t DUMMY_FLOATS = (size_t)H * H + H + (size_t)H * (1 + 2 * H) + H 
 struct Layout {
   std::vector<Param> params;
   std::map<std::string, size_t> off;  // packed offset per parameter name
+  std::map<std::string, size_t> offw; // fp32: Winograd-packed copy of eligible 3x3 weights
   std::map<std::string, int> eboff;   // ResBlock name -> column offset in Wall
   size_t enc = 0, dummy = 0, wall = 0, ball = 0, total = 0;
   int ebtotal = 0;
@@ -172,6 +174,14 @@ Layout layout(const ertd_unet_config* c) {
                           ? conv_packed_floats_up(p.shape[1], p.shape[0])
                           : conv_packed_floats(p.shape[1], p.shape[0], p.shape[2])));
     else o += a64(p.numel());
+    // fp32 ResBlock 3x3 convs also get the Winograd F(2x2,3x3) packing
+    // (dispatch picks it when conv_wino_ok; ERTD_UNET_WINO=0 keeps the direct one)
+    if (c->precision == ERTD_PREC_FP32 && p.shape.size() == 4 && p.shape[2] == 3 &&
+        (ends_with(p.name, ".conv1.weight") || ends_with(p.name, ".conv2.weight")) &&
+        conv_packed_floats_wino(p.shape[1], p.shape[0]) > 0) {
+      L.offw[p.name] = o;
+      o += a64(conv_packed_floats_wino(p.shape[1], p.shape[0]));
+    }
   }
   L.total = o;
   return L;
@@ -259,6 +269,10 @@ struct Walk {
     a.srcA = A; a.srcB = Bs; a.Ca = Ca; a.Cb = Cb;
     a.gn = act != ACT_NONE ? gnbuf : nullptr;
     a.wpk = P(n + ".weight");
+    {
+      const auto it = L->offw.find(n + ".weight");
+      a.wpk_wino = it != L->offw.end() ? pk + it->second : nullptr;
+    }
     a.bias = P(n + ".bias");
     a.ebias = ebias; a.eb_stride = L->ebtotal;
     a.res = res; a.out = out;
@@ -590,6 +604,8 @@ size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision) {
   // fp32 3x3 convs may be Upsample convs (sub-pixel packing)
   if (precision != ERTD_PREC_BF16 && ks == 3 && conv_packed_floats_up(cin, cout) > f)
     f = conv_packed_floats_up(cin, cout);
+  // ... and stride-1 ones carry the Winograd packing behind the direct one
+  if (precision != ERTD_PREC_BF16 && ks == 3) f = a64(f) + conv_packed_floats_wino(cin, cout);
   return f * sizeof(float);
 }
 
@@ -617,6 +633,12 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   a.Cin = Cin; a.Cout = Cout; a.Hs = H; a.Ws = H;
   a.Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   a.Wo = a.Ho;
+  if (precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 &&
+      conv_packed_floats_wino(Cin, Cout) > 0) {
+    float* pw = pk + a64(std::max(conv_packed_floats(Cin, Cout, ks), conv_packed_floats_up(Cin, Cout)));
+    if ((e = launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess) return (int)e;
+    a.wpk_wino = pw;
+  }
   void* bimg = nullptr;
   if (precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
       ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE))) {
@@ -722,6 +744,9 @@ int ertd_unet_pack(const ertd_unet_config* c, const float* const* params, const 
                      ? launch_pack_conv_up(src, p.shape[1], p.shape[0], packed + L.off.at(p.name), s)
                      : launch_pack_conv(src, p.shape[1], p.shape[0], p.shape[2],
                                         packed + L.off.at(p.name), s));
+      const auto itw = L.offw.find(p.name);
+      if (e == hipSuccess && itw != L.offw.end())
+        e = launch_pack_conv_wino(src, p.shape[1], p.shape[0], packed + itw->second, s);
     } else if (p.shape.size() == 2) {
       e = launch_transpose(src, p.shape[0], p.shape[1], packed + L.off.at(p.name), p.shape[0], s);
     } else {

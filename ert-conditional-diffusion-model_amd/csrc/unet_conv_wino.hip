@@ -1,0 +1,485 @@
+// 3x3 stride-1 convolution of the U-Net ResBlocks by Winograd F(2x2, 3x3) on
+// fp32 MFMA (v_mfma_f32_32x32x2_f32), GroupNorm + SiLU fused into the input
+// transform, bias / embedding / residual into the output transform.
+//
+// Per 2x2 output tile and input channel c (d = the 4x4 input window at
+// rows 2ty-1.., cols 2tx-1.., zero outside the image, AFTER the activation):
+//   V = B^T d B        B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
+//   U = G g G^T        G   = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]
+//   M[xi] = sum_c U[xi][co][c] V[xi][c][tile]          (16 GEMMs, xi = 4i + j)
+//   Y = A^T M A        A^T = [1 1 1 0; 0 1 -1 -1]
+// 16 multiplies per 4 outputs instead of 36: 2.25x less MFMA work than the
+// direct implicit GEMM (unet_conv.hip), all of it fp32 (products exact, sums
+// rounded in fp32; the transforms add a few roundings per value -- the
+// forward stays within 1e-5 of the spec, tests/test_gpu_unet*.py).
+//
+// Work item = (64 output channels, 64 tiles = 256 output pixels, sample), all
+// 16 xi, K walked in chunks of 8 input channels.  The kernel is PERSISTENT:
+// one 768-thread workgroup per CU walks items bid, bid + grid, ... as one
+// continuous chunk pipeline, so the next item's first chunks are staged
+// while the current one finishes and its epilogue (stores) overlaps the
+// next item's loads.  12 waves with fixed roles:
+//   * 8 MFMA waves on v_mfma_f32_16x16x4_f32: wave w = (16-co block w & 3,
+//     32-tile pair w >> 2) keeps ALL 16 xi of its 16 co x 32 tiles (2 x 16
+//     accumulators of 4 VGPRs = 128), so the output transform needs no data
+//     of any other wave; inside the K loop it only reads LDS (per xi and
+//     4-channel k-step: one ds_read_b32 of U, two of V, 2 MFMAs);
+//     They also LDS-DMA the weights U (pre-transformed at pack time in
+//     fragment order: [xi 16][k-step 2][co block 4][k 4][co 16] = 32 KB per
+//     chunk) two chunks ahead into a 3-slot ring;
+//   * 4 producer waves: the input transform -- lane = tile, 2 channels per
+//     wave: the two middle columns of the tile's 4x4 window are loaded three
+//     chunks ahead into two register sets (one float2 per row, with the
+//     channels' GroupNorm scale/shift), GroupNorm+SiLU applied, the outer
+//     columns taken from the neighbouring lanes (DPP wave shifts), transformed
+//     and written as V [xi][k-step 2][tile block 4][k 4][tile 16] (32 KB,
+//     double-buffered).
+//   With 3 waves per SIMD (2 MFMA + 1 producer) the hardware interleaves the
+//   producer's VALU / memory work with the MFMA waves' matrix-pipe time; one
+//   barrier per chunk.
+//   * Output transform (MFMA waves, in registers, right after an item's last
+//     chunk): Y = A^T M A per (co, tile), + bias (+ emb) (+ residual), two
+//     float2 stores per (co, tile); the next item's chunks are already staged.
+// LDS 160 KB: one workgroup per CU.
+#include <cstdlib>
+
+#include "unet.h"
+
+namespace ertd {
+namespace unet {
+
+namespace {
+
+constexpr int NMW = 8;                        // MFMA waves
+constexpr int NPW = 4;                        // producer waves
+constexpr int WT = 64 * (NMW + NPW);          // threads per workgroup (768)
+constexpr int WKC = 8;                        // input channels per K chunk
+constexpr int WSP = WKC / 4;                  // MFMA step pairs per chunk
+constexpr int U_FL = 16 * 2 * WSP * 128;      // U floats per chunk buffer (8192)
+constexpr int V_FL = 16 * WSP * 2 * 128;      // V floats per chunk buffer (8192)
+constexpr int NUB = 3;                        // U ring depth (DMA two chunks ahead)
+constexpr size_t WLDS = (size_t)(NUB * U_FL + 2 * V_FL) * sizeof(float);   // 160 KB
+constexpr int XIF = WKC * 64;                 // U / V floats per xi (512)
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ unsigned wlds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+int wino_env() {
+  static int v = [] {
+    const char* e = getenv("ERTD_UNET_WINO");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// item it -> (co block, tile block, sample): co block fastest, so the
+// workgroups running at one time share few weight slices
+struct Item {
+  int cog, tblk, b;
+};
+__device__ __forceinline__ Item item_of(int it, int ncog, int ntblk) {
+  Item r;
+  r.cog = it % ncog;
+  const int t = it / ncog;
+  r.tblk = t % ntblk;
+  r.b = t / ntblk;
+  return r;
+}
+
+// DBG (diagnostics only, ERTD_WINO_DBG): bit 0 skips the activation VALU,
+// bit 1 the input loads, bit 2 the weight DMA, bit 3 the MFMAs, bit 4 the
+// producers' transform, bit 5 the MFMA waves' LDS reads -- the results are
+// wrong, the timings show where a chunk's time goes
+template <int WO, int ACT, int DBG = 0>
+__global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* ubuf = smem;                 // [3][U_FL] ring
+  float* vbuf = smem + NUB * U_FL;    // [2][V_FL]
+
+  constexpr int TPR = WO / 2;         // tiles per tile row
+  constexpr int HW = WO * WO;
+  constexpr int NTBLK = TPR * TPR / 64;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int Cin = a.Cin, Ca = a.Ca;
+  const int nchunk = Cin / WKC;
+  const int ncog = a.Cout / 64;
+  const int bid = blockIdx.x, G = gridDim.x;
+  const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;   // items of this workgroup
+  const int gtot = nloc * nchunk;                                    // chunks of this workgroup
+
+  if (wave >= NMW) {
+    // =================== producer waves ===================
+    const int q = wave - NMW;          // channels 2q, 2q+1 of every chunk
+    // V offset of (channel c = 2q + hv, tile t = lane): [xi][c >> 2][t >> 4][c & 3][t & 15]
+    const int vwoff = (q >> 1) * 256 + (lane >> 4) * 64 + (2 * (q & 1)) * 16 + (lane & 15);
+    // registers of the chunk in flight: the two middle columns of the 4x4
+    // window (one float2 per row) of both channels, their GroupNorm
+    // {scale, shift}, and the window's padding masks.  Each lane loads its
+    // tile's middle columns; the outer columns are the neighbouring tiles'
+    // (lanes t-1 / t+1) by DPP wave shifts -- across a tile-row boundary they
+    // are padding (masked), so the shifted-in neighbour never matters there.
+    float2 raw[2][2][4];   // [register set][channel][row]
+    float2 gnv[2][2];
+    unsigned msk[2] = {0u, 0u};   // bits 0-3: row r valid, bit 4: left column, bit 5: right column
+    auto load_chunk = [&](const int set, int g) {
+      const int il = g / nchunk, k = g - il * nchunk;
+      const Item itm = item_of(bid + il * G, ncog, NTBLK);
+      const int tg = itm.tblk * 64 + lane;
+      const int ty = tg / TPR, tx = tg - ty * TPR;
+      unsigned m = (tx > 0 ? 16u : 0u) | (tx < TPR - 1 ? 32u : 0u);
+      int roff[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int iy = 2 * ty - 1 + r;
+        const bool ok = iy >= 0 && iy < WO;
+        m |= ok ? (1u << r) : 0u;
+        roff[r] = (ok ? iy : 0) * WO + 2 * tx;
+      }
+      msk[set] = m;
+#pragma unroll
+      for (int hv = 0; hv < 2; ++hv) {
+        const int cg = k * WKC + 2 * q + hv;    // wave-uniform
+        if constexpr (ACT != ACT_NONE) gnv[set][hv] = a.gn[(size_t)itm.b * Cin + cg];
+        if constexpr (DBG & 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) raw[set][hv][r] = make_float2((float)(r + k), (float)hv);
+        } else {
+          const float* p = cg < Ca ? a.srcA + ((size_t)itm.b * Ca + cg) * HW
+                                   : a.srcB + ((size_t)itm.b * a.Cb + (cg - Ca)) * HW;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) raw[set][hv][r] = *reinterpret_cast<const float2*>(p + roff[r]);
+        }
+      }
+    };
+    auto transform_chunk = [&](const int set, float* vb) {
+      if constexpr (DBG & 16) return;
+      const unsigned m = msk[set];
+#pragma unroll
+      for (int hv = 0; hv < 2; ++hv) {
+        float d[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float m0 = raw[set][hv][r].x, m1 = raw[set][hv][r].y;
+          if constexpr (ACT != ACT_NONE && !(DBG & 1)) {
+            m0 = fmaf(m0, gnv[set][hv].x, gnv[set][hv].y);   // ATen's folded GroupNorm
+            m1 = fmaf(m1, gnv[set][hv].x, gnv[set][hv].y);
+            if constexpr (ACT == ACT_GN_SILU) {
+              m0 = m0 * __builtin_amdgcn_rcpf(1.0f + __expf(-m0));
+              m1 = m1 * __builtin_amdgcn_rcpf(1.0f + __expf(-m1));
+            }
+          }
+          // left neighbour's column 2tx-1 (lane t-1's m1), right's 2tx+2 (lane t+1's m0)
+          const float lf = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m1), 0x138, 0xf, 0xf, false));
+          const float rt = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m0), 0x130, 0xf, 0xf, false));
+          // the padding pads the activated tensor
+          const bool rok = (m >> r) & 1u;
+          d[r][0] = (rok && (m & 16u)) ? lf : 0.f;
+          d[r][1] = rok ? m0 : 0.f;
+          d[r][2] = rok ? m1 : 0.f;
+          d[r][3] = (rok && (m & 32u)) ? rt : 0.f;
+        }
+        float tm[4][4];   // B^T d
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          tm[0][s] = d[0][s] - d[2][s];
+          tm[1][s] = d[1][s] + d[2][s];
+          tm[2][s] = d[2][s] - d[1][s];
+          tm[3][s] = d[1][s] - d[3][s];
+        }
+        float* o = vb + vwoff + hv * 16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {   // (B^T d) B
+          o[(4 * i + 0) * XIF] = tm[i][0] - tm[i][2];
+          o[(4 * i + 1) * XIF] = tm[i][1] + tm[i][2];
+          o[(4 * i + 2) * XIF] = tm[i][2] - tm[i][1];
+          o[(4 * i + 3) * XIF] = tm[i][1] - tm[i][3];
+        }
+      }
+    };
+
+    // Two register sets (chunk c in set c & 1), loads three chunks ahead of
+    // the MFMAs: in the slot of chunk g the producers transform chunk g+1
+    // (loaded two slots earlier -- the compiler's own vmcnt waits, which count
+    // only these loads) into V[(g+1) & 1] and issue chunk g+3's loads.
+    if (gtot > 0) load_chunk(0, 0);
+    if (gtot > 1) load_chunk(1, 1);
+    if (gtot > 0) transform_chunk(0, vbuf);
+    if (gtot > 2) load_chunk(0, 2);
+    __syncthreads();   // (A) chunk 0 staged
+    for (int g = 0; g < gtot; g += 2) {
+      if (g + 1 < gtot) transform_chunk(1, vbuf + V_FL);
+      if (g + 3 < gtot) load_chunk(1, g + 3);
+      __syncthreads();   // (B) end of slot g
+      if (g + 1 < gtot) {
+        if (g + 2 < gtot) transform_chunk(0, vbuf);
+        if (g + 4 < gtot) load_chunk(0, g + 4);
+        __syncthreads();   // (B) end of slot g+1
+      }
+    }
+    return;
+  }
+
+  // =================== MFMA waves ===================
+  const int cb = wave & 3, tbp = wave >> 2;
+  const int aoff = cb * 64 + lane;                  // + xi*XIF + s*256
+  const int boff = (2 * tbp) * 64 + lane;           // + xi*XIF + s*256 (+64: second tile block)
+  f32x4 acc[16][2];
+
+  // U slice DMA of chunk g into ring slot g % 3, issued two slots ahead by the
+  // MFMA waves themselves (4 x 1 KB per wave): they issue no other vector
+  // memory operation in the K loop, so "all but this slot's 4 DMAs done"
+  // (vmcnt(4)) is exactly "chunk g+1's slice has landed"
+  auto dma_u = [&](int g) {
+    if constexpr (DBG & 4) return;
+    const int il = g / nchunk, k = g - il * nchunk;
+    const int cog = (bid + il * G) % ncog;
+    const float* usrc = a.wpk_wino + ((size_t)cog * nchunk + k) * U_FL;
+    float* dst = ubuf + (g % NUB) * U_FL;
+#pragma unroll
+    for (int j = 0; j < U_FL / (NMW * 256); ++j) {
+      const int ins = wave * (U_FL / (NMW * 256)) + j;   // wave-uniform, 1 KB each
+      const float* src = usrc + ins * 256 + lane * 4;
+      const unsigned ldst = __builtin_amdgcn_readfirstlane(wlds_addr(dst + ins * 256));
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(src), "s"(ldst)
+          : "memory");
+    }
+  };
+  static_assert(U_FL / (NMW * 256) == 4, "vmcnt(4) below counts the DMAs of one slot");
+  if (gtot > 0) dma_u(0);
+  if (gtot > 1) dma_u(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // (A)
+  for (int il = 0; il < nloc; ++il) {
+#pragma unroll
+    for (int x = 0; x < 16; ++x) acc[x][0] = acc[x][1] = f32x4{};
+    for (int k = 0; k < nchunk; ++k) {
+      const int g = il * nchunk + k;
+      const bool dma = g + 2 < gtot;
+      if (dma) dma_u(g + 2);
+      const float* ub = ubuf + (g % NUB) * U_FL + aoff;
+      const float* vb = vbuf + (g & 1) * V_FL + boff;
+#pragma unroll
+      for (int st = 0; st < WKC / 4; ++st) {   // k-step of 4 channels
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+          float av, b0, b1;
+          if constexpr (DBG & 32) {
+            av = (float)(lane + x + st);
+            b0 = (float)(lane - x + k);
+            b1 = b0 + 1.f;
+          } else {
+            av = ub[x * XIF + st * 256];
+            b0 = vb[x * XIF + st * 256];
+            b1 = vb[x * XIF + st * 256 + 64];
+          }
+          if constexpr (DBG & 8) {
+            acc[x][0][0] += av * b0;
+            acc[x][1][0] += av * b1;
+          } else {
+            acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[x][0], 0, 0, 0);
+            acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[x][1], 0, 0, 0);
+          }
+        }
+      }
+      // keep the chunk's MFMAs ahead of the barrier (hipcc would sink them:
+      // they touch no memory)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) asm volatile("" : "+v"(acc[x][0]), "+v"(acc[x][1]));
+      if (dma) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // (B)
+    }
+
+    // ---- output transform of this wave's 16 co x 32 tiles, in registers:
+    // lane l holds M[xi] of co = 16 cb + 4 (l >> 4) + i (acc element i) and
+    // tile 16 j + (l & 15) of its tile pair (accumulator j)
+    const Item itm = item_of(bid + il * G, ncog, NTBLK);
+    const float* ebp = a.ebias ? a.ebias + (size_t)itm.b * a.eb_stride : nullptr;
+    float bias[4], eb[4];
+    int co[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      co[i] = itm.cog * 64 + cb * 16 + 4 * (lane >> 4) + i;
+      bias[i] = a.bias[co[i]];
+      eb[i] = ebp ? ebp[co[i]] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int tg = itm.tblk * 64 + (2 * tbp + j) * 16 + (lane & 15);
+      const int ty = tg / TPR, tx = tg - ty * TPR;
+      const size_t pix = (size_t)(2 * ty) * WO + 2 * tx;
+      float* outb = a.out + (size_t)itm.b * a.Cout * HW + pix;
+      const float* resb = a.res ? a.res + (size_t)itm.b * a.Cout * HW + pix : nullptr;
+      float2 rv[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          rv[i][y] = resb ? *reinterpret_cast<const float2*>(resb + (size_t)co[i] * HW + y * WO)
+                          : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float Pm[4][2];   // P = M A, per row of M
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float m0 = acc[4 * r + 0][j][i], m1 = acc[4 * r + 1][j][i];
+          const float m2 = acc[4 * r + 2][j][i], m3 = acc[4 * r + 3][j][i];
+          Pm[r][0] = (m0 + m1) + m2;
+          Pm[r][1] = (m1 - m2) - m3;
+        }
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          float v[2];
+#pragma unroll
+          for (int x = 0; x < 2; ++x) {
+            // Y = A^T P, then the spec's op order: conv + bias, + emb, + residual
+            float t = y == 0 ? (Pm[0][x] + Pm[1][x]) + Pm[2][x] : (Pm[1][x] - Pm[2][x]) - Pm[3][x];
+            t = t + bias[i];
+            if (ebp) t = t + eb[i];
+            if (resb) t = t + (x == 0 ? rv[i][y].x : rv[i][y].y);
+            v[x] = t;
+          }
+          *reinterpret_cast<float2*>(outb + (size_t)co[i] * HW + y * WO) = make_float2(v[0], v[1]);
+        }
+      }
+    }
+  }
+}
+
+int wino_dbg() {
+  static int v = [] {
+    const char* e = getenv("ERTD_WINO_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+int cu_count() {
+  static int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    return n;
+  }();
+  return v;
+}
+
+template <int WO, int ACT, int DBG>
+hipError_t launch_wod(const ConvArgs& a, int B, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_wino_kernel<WO, ACT, DBG>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)WLDS);
+    attr = true;
+  }
+  const int nitems = (WO / 2) * (WO / 2) / 64 * (a.Cout / 64) * B;
+  const int grid = nitems < cu_count() ? nitems : cu_count();
+  conv_wino_kernel<WO, ACT, DBG><<<grid, WT, WLDS, s>>>(a, nitems);
+  return hipGetLastError();
+}
+
+template <int WO, int ACT>
+hipError_t launch_wo(const ConvArgs& a, int B, hipStream_t s) {
+  if constexpr (WO == 64 && ACT == ACT_GN_SILU) {
+    switch (wino_dbg()) {
+      case 1: return launch_wod<WO, ACT, 1>(a, B, s);
+      case 2: return launch_wod<WO, ACT, 2>(a, B, s);
+      case 4: return launch_wod<WO, ACT, 4>(a, B, s);
+      case 8: return launch_wod<WO, ACT, 8>(a, B, s);
+      case 7: return launch_wod<WO, ACT, 7>(a, B, s);
+      case 23: return launch_wod<WO, ACT, 23>(a, B, s);
+      case 55: return launch_wod<WO, ACT, 55>(a, B, s);
+      default: break;
+    }
+  }
+  return launch_wod<WO, ACT, 0>(a, B, s);
+}
+
+template <int ACT>
+hipError_t launch_act(const ConvArgs& a, int B, hipStream_t s) {
+  switch (a.Wo) {
+    case 16: return launch_wo<16, ACT>(a, B, s);
+    case 32: return launch_wo<32, ACT>(a, B, s);
+    case 64: return launch_wo<64, ACT>(a, B, s);
+    case 128: return launch_wo<128, ACT>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// ---- packing: W (Cout, Cin, 3, 3) -> U = G g G^T in [cog][chunk][xi][st][cb][kk][c16]
+// (computed in float64, rounded once): the A-operand fragment of
+// v_mfma_f32_16x16x4_f32 for co block cb (16 co) and k-step st, lane l =
+// 16 kk + c16 -> co = 16 cb + c16, channel 4 st + kk of the chunk
+__global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int nchunk, size_t total,
+                                 float* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c16 = (int)(i & 15);
+  const int kk = (int)((i >> 4) & 3);
+  const int cb = (int)((i >> 6) & 3);
+  const int st = (int)((i >> 8) & 1);
+  size_t rest = i >> 9;
+  const int xi = (int)(rest % 16);
+  rest /= 16;
+  const int k = (int)(rest % nchunk);
+  const int cog = (int)(rest / nchunk);
+  const int co = cog * 64 + cb * 16 + c16;
+  const int ci = k * WKC + 4 * st + kk;
+  const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  const int ri = xi >> 2, rj = xi & 3;
+  const float* g = w + ((size_t)co * cin + ci) * 9;
+  double u = 0.0;
+#pragma unroll
+  for (int y = 0; y < 3; ++y) {
+    double row = 0.0;
+#pragma unroll
+    for (int x = 0; x < 3; ++x) row += (double)g[y * 3 + x] * G[rj][x];
+    u += G[ri][y] * row;
+  }
+  dst[i] = (float)u;
+}
+
+}  // namespace
+
+bool conv_wino_ok(int cin, int ca, int cout, int wo) {
+  return wino_env() != 0 && cin % WKC == 0 && ca % WKC == 0 && cout % 64 == 0 &&
+         (wo == 16 || wo == 32 || wo == 64 || wo == 128);
+}
+
+size_t conv_packed_floats_wino(int cin, int cout) {
+  if (cin % WKC || cout % 64) return 0;
+  return (size_t)16 * cout * cin;
+}
+
+hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s) {
+  const size_t total = conv_packed_floats_wino(cin, cout);
+  if (!total) return hipErrorInvalidValue;
+  pack_wino_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cin / WKC, total, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_wino(int act, const ConvArgs& a, int B, hipStream_t s) {
+  if (!a.wpk_wino || !conv_wino_ok(a.Cin, a.Ca, a.Cout, a.Wo) || a.Ho != a.Wo || a.Hs != a.Ho ||
+      a.Ws != a.Wo)
+    return hipErrorInvalidValue;
+  switch (act) {
+    case ACT_NONE: return launch_act<ACT_NONE>(a, B, s);
+    case ACT_GN_SILU: return launch_act<ACT_GN_SILU>(a, B, s);
+    case ACT_GN: return launch_act<ACT_GN>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace unet
+}  // namespace ertd

@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from ertdiff.unet import attention, conv2d, group_norm_act_bf16, group_norm_stats
 from oracle import ref_numpy as RN
+from conftest import record_error
 
 pytestmark = pytest.mark.gpu
 
@@ -54,6 +55,15 @@ CASES = [  # (Ca, Cb, Cout, H, ks, mode, act)
     (32, 24, 1, 32, 3, "same", "gn_silu"),       # Cout 1, concat, partial 16-ch chunk
     (20, 0, 1, 16, 3, "same", "none"),           # Cout 1, whole image in one workgroup
     (128, 0, 1, 128, 3, "same", "gn_silu"),      # Cout 1 at U5's resolution
+    # fp32 Winograd F(2x2,3x3) path (Cin, Ca % 8 == 0, Cout % 64 == 0) at every width
+    (128, 0, 128, 128, 3, "same", "gn_silu"),    # U5's 128x128 level
+    (32, 32, 64, 32, 3, "same", "none"),         # no activation, concatenated input
+    (256, 0, 128, 16, 3, "same", "gn"),          # GroupNorm without SiLU
+    (384, 128, 256, 16, 3, "same", "gn_silu"),   # U2's widest concat (K = 512)
+    # ... and shapes it does not take (direct implicit GEMM)
+    (20, 0, 64, 32, 3, "same", "gn_silu"),       # Cin % 8 != 0
+    (64, 0, 96, 32, 3, "same", "gn_silu"),       # Cout % 64 != 0
+    (60, 4, 64, 16, 3, "same", "gn_silu"),       # concat split inside an 8-channel chunk
 ]
 
 
@@ -74,6 +84,7 @@ def test_conv2d(Ca, Cb, Cout, H, ks, mode, act, precision, cuda_dev):
     xin = x if x2 is None else torch.cat([x, x2], 1)
     ref = _ref_conv(xin, w, b, mode, act, gn, precision == "bf16")
     err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
+    record_error(f"conv2d_{Ca}_{Cb}_{Cout}_{H}_k{ks}_{mode}_{act}_{precision}", err)
     assert err < (1e-4 if precision == "bf16" else 1e-5), err
 
 

@@ -57,20 +57,26 @@ def walk():
 
 
 layers = walk()
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_kernel<" in r["Kernel_Name"] or "conv_out_kernel<" in r["Kernel_Name"]]
+KEYS = ("conv_kernel<", "conv_out_kernel<", "conv_wino_kernel<", "conv_bf16_kernel<")
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if any(k in r["Kernel_Name"] for k in KEYS)]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 last = rows[-len(layers):]
 tot_t = tot_f = 0
 for (n, cin, cout, ks, wo), r in zip(layers, last):
     us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
     fl = 2 * cin * cout * ks * ks * wo * wo * B
+    alg = fl
     if "conv_kernel<2, 3," in r["Kernel_Name"]:   # fp32 sub-pixel Upsample: 4 of 9 taps executed
         fl = fl * 4 // 9
         n = n + "*"
+    if "conv_wino_kernel<" in r["Kernel_Name"]:   # Winograd F(2x2,3x3): 16 of 36 multiplies
+        fl = fl * 4 // 9
+        n = n + "w"
     tot_t += us
     tot_f += fl
     tmpl = r["Kernel_Name"][r["Kernel_Name"].find("<"):r["Kernel_Name"].find(">") + 1]
-    wgs = int(r["Grid_Size_X"]) // 256 * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+    wgs = int(r["Grid_Size_X"]) // int(r.get("Workgroup_Size_X", 256) or 256) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
     print(f"{n:14s} {cin:4d}->{cout:4d} k{ks} {wo:3d}  {tmpl:22s} wg {wgs:5d}  {us:8.1f} us  "
-          f"{fl / us / 1e6:7.1f} TF  {fl / us / 1e6 / 157.3 * 100:5.1f}%")
-print(f"total {tot_t:.0f} us, {tot_f / tot_t / 1e6:.1f} TF (executed FLOP; * = sub-pixel Upsample, 4 of 9 taps)")
+          f"{fl / us / 1e6:7.1f} TF  {fl / us / 1e6 / 157.3 * 100:5.1f}%  (alg {alg / us / 1e6:6.1f} TF)")
+print(f"total {tot_t:.0f} us, {tot_f / tot_t / 1e6:.1f} TF (executed FLOP; * = sub-pixel Upsample, "
+      f"4 of 9 taps; w = Winograd F(2x2,3x3), 16 of 36 multiplies)")
