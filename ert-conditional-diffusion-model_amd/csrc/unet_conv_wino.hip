@@ -268,28 +268,40 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
       if (dma) dma_u(g + 2);
       const float* ub = ubuf + (g % NUB) * U_FL + aoff;
       const float* vb = vbuf + (g & 1) * V_FL + boff;
-#pragma unroll
-      for (int st = 0; st < WKC / 4; ++st) {   // k-step of 4 channels
-#pragma unroll
-        for (int x = 0; x < 16; ++x) {
-          float av, b0, b1;
-          if constexpr (DBG & 32) {
-            av = (float)(lane + x + st);
-            b0 = (float)(lane - x + k);
-            b1 = b0 + 1.f;
-          } else {
-            av = ub[x * XIF + st * 256];
-            b0 = vb[x * XIF + st * 256];
-            b1 = vb[x * XIF + st * 256 + 64];
-          }
-          if constexpr (DBG & 8) {
-            acc[x][0][0] += av * b0;
-            acc[x][1][0] += av * b1;
-          } else {
-            acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[x][0], 0, 0, 0);
-            acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[x][1], 0, 0, 0);
-          }
+      // 32 steps (k-step st = s >> 4 of 4 channels, xi = s & 15): operands
+      // read 3 steps ahead into a 4-deep register ring, each step's three
+      // ds_reads grouped with the two MFMAs of an earlier step (the compiler
+      // otherwise spends the few free registers on A operands and waits a
+      // full LDS latency before every MFMA pair)
+      constexpr int NS = 2 * 16, PD = 3;
+      float ra[4], rb0[4], rb1[4];
+      auto ld = [&](const int s2) {
+        const int st = s2 >> 4, x = s2 & 15, r = s2 & 3;
+        if constexpr (DBG & 32) {
+          ra[r] = (float)(lane + x + st);
+          rb0[r] = (float)(lane - x + k);
+          rb1[r] = rb0[r] + 1.f;
+        } else {
+          ra[r] = ub[x * XIF + st * 256];
+          rb0[r] = vb[x * XIF + st * 256];
+          rb1[r] = vb[x * XIF + st * 256 + 64];
         }
+      };
+#pragma unroll
+      for (int s2 = 0; s2 < PD; ++s2) ld(s2);
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) {
+        if (s2 + PD < NS) ld(s2 + PD);
+        const int x = s2 & 15, r = s2 & 3;
+        if constexpr (DBG & 8) {
+          acc[x][0][0] += ra[r] * rb0[r];
+          acc[x][1][0] += ra[r] * rb1[r];
+        } else {
+          acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[r], rb0[r], acc[x][0], 0, 0, 0);
+          acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[r], rb1[r], acc[x][1], 0, 0, 0);
+        }
+        if (s2 + PD < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                      // MFMAs
       }
       // keep the chunk's MFMAs ahead of the barrier (hipcc would sink them:
       // they touch no memory)
@@ -398,6 +410,8 @@ hipError_t launch_wo(const ConvArgs& a, int B, hipStream_t s) {
       case 4: return launch_wod<WO, ACT, 4>(a, B, s);
       case 8: return launch_wod<WO, ACT, 8>(a, B, s);
       case 7: return launch_wod<WO, ACT, 7>(a, B, s);
+      case 16: return launch_wod<WO, ACT, 16>(a, B, s);
+      case 18: return launch_wod<WO, ACT, 18>(a, B, s);
       case 23: return launch_wod<WO, ACT, 23>(a, B, s);
       case 55: return launch_wod<WO, ACT, 55>(a, B, s);
       default: break;
