@@ -90,7 +90,8 @@ __device__ __forceinline__ Item item_of(int it, int ncog, int ntblk) {
 
 // DBG (diagnostics only, ERTD_WINO_DBG): bit 0 skips the activation VALU,
 // bit 1 the input loads, bit 2 the weight DMA, bit 3 the MFMAs, bit 4 the
-// producers' transform, bit 5 the MFMA waves' LDS reads -- the results are
+// producers' transform, bit 5 the MFMA waves' LDS reads, bits 6/7/8 the
+// producers' DPP / padding selects / V stores -- the results are
 // wrong, the timings show where a chunk's time goes
 template <int WO, int ACT, int DBG = 0>
 __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
@@ -174,14 +175,24 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
             }
           }
           // left neighbour's column 2tx-1 (lane t-1's m1), right's 2tx+2 (lane t+1's m0)
-          const float lf = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m1), 0x138, 0xf, 0xf, false));
-          const float rt = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m0), 0x130, 0xf, 0xf, false));
+          float lf, rt;
+          if constexpr (DBG & 64) {
+            lf = m1;
+            rt = m0;
+          } else {
+            lf = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m1), 0x138, 0xf, 0xf, false));
+            rt = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m0), 0x130, 0xf, 0xf, false));
+          }
           // the padding pads the activated tensor
-          const bool rok = (m >> r) & 1u;
-          d[r][0] = (rok && (m & 16u)) ? lf : 0.f;
-          d[r][1] = rok ? m0 : 0.f;
-          d[r][2] = rok ? m1 : 0.f;
-          d[r][3] = (rok && (m & 32u)) ? rt : 0.f;
+          if constexpr (DBG & 128) {
+            d[r][0] = lf; d[r][1] = m0; d[r][2] = m1; d[r][3] = rt;
+          } else {
+            const bool rok = (m >> r) & 1u;
+            d[r][0] = (rok && (m & 16u)) ? lf : 0.f;
+            d[r][1] = rok ? m0 : 0.f;
+            d[r][2] = rok ? m1 : 0.f;
+            d[r][3] = (rok && (m & 32u)) ? rt : 0.f;
+          }
         }
         float tm[4][4];   // B^T d
 #pragma unroll
@@ -192,12 +203,20 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
           tm[3][s] = d[1][s] - d[3][s];
         }
         float* o = vb + vwoff + hv * 16;
+        if constexpr (DBG & 256) {
+          float t = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {   // (B^T d) B
-          o[(4 * i + 0) * XIF] = tm[i][0] - tm[i][2];
-          o[(4 * i + 1) * XIF] = tm[i][1] + tm[i][2];
-          o[(4 * i + 2) * XIF] = tm[i][2] - tm[i][1];
-          o[(4 * i + 3) * XIF] = tm[i][1] - tm[i][3];
+          for (int i = 0; i < 4; ++i)
+            t += (tm[i][0] - tm[i][2]) + (tm[i][1] + tm[i][2]) + (tm[i][2] - tm[i][1]) + (tm[i][1] - tm[i][3]);
+          o[0] = t;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {   // (B^T d) B
+            o[(4 * i + 0) * XIF] = tm[i][0] - tm[i][2];
+            o[(4 * i + 1) * XIF] = tm[i][1] + tm[i][2];
+            o[(4 * i + 2) * XIF] = tm[i][2] - tm[i][1];
+            o[(4 * i + 3) * XIF] = tm[i][1] - tm[i][3];
+          }
         }
       }
     };
@@ -206,21 +225,29 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
     // the MFMAs: in the slot of chunk g the producers transform chunk g+1
     // (loaded two slots earlier -- the compiler's own vmcnt waits, which count
     // only these loads) into V[(g+1) & 1] and issue chunk g+3's loads.
-    if (gtot > 0) load_chunk(0, 0);
-    if (gtot > 1) load_chunk(1, 1);
-    if (gtot > 0) transform_chunk(0, vbuf);
-    if (gtot > 2) load_chunk(0, 2);
-    __syncthreads();   // (A) chunk 0 staged
-    for (int g = 0; g < gtot; g += 2) {
-      if (g + 1 < gtot) transform_chunk(1, vbuf + V_FL);
-      if (g + 3 < gtot) load_chunk(1, g + 3);
-      __syncthreads();   // (B) end of slot g
-      if (g + 1 < gtot) {
-        if (g + 2 < gtot) transform_chunk(0, vbuf);
-        if (g + 4 < gtot) load_chunk(0, g + 4);
-        __syncthreads();   // (B) end of slot g+1
-      }
+    // Loads past the last chunk re-load the last one (clamped, unused): the
+    // steady-state loop then has no conditional loads, and the compiler's
+    // vmcnt bookkeeping across its back edge stays exact (a transform waits
+    // only for its own set, not for the loads issued one slot earlier).
+    const int glast = gtot - 1;
+    auto clampg = [&](int g) { return g < glast ? g : glast; };
+    if (gtot > 0) {
+      load_chunk(0, 0);
+      load_chunk(1, clampg(1));
+      transform_chunk(0, vbuf);
+      load_chunk(0, clampg(2));
     }
+    __syncthreads();   // (A) chunk 0 staged
+    int g = 0;
+    for (; g + 1 < gtot; g += 2) {
+      transform_chunk(1, vbuf + V_FL);          // chunk g+1
+      load_chunk(1, clampg(g + 3));
+      __syncthreads();   // (B) end of slot g
+      transform_chunk(0, vbuf);                 // chunk g+2 (unused past the end)
+      load_chunk(0, clampg(g + 4));
+      __syncthreads();   // (B) end of slot g+1
+    }
+    if (g < gtot) __syncthreads();   // (B) end of the last slot (odd chunk count)
     return;
   }
 
@@ -411,7 +438,10 @@ hipError_t launch_wo(const ConvArgs& a, int B, hipStream_t s) {
       case 8: return launch_wod<WO, ACT, 8>(a, B, s);
       case 7: return launch_wod<WO, ACT, 7>(a, B, s);
       case 16: return launch_wod<WO, ACT, 16>(a, B, s);
-      case 18: return launch_wod<WO, ACT, 18>(a, B, s);
+      case 64: return launch_wod<WO, ACT, 64>(a, B, s);
+      case 128: return launch_wod<WO, ACT, 128>(a, B, s);
+      case 256: return launch_wod<WO, ACT, 256>(a, B, s);
+      case 448: return launch_wod<WO, ACT, 448>(a, B, s);
       case 23: return launch_wod<WO, ACT, 23>(a, B, s);
       case 55: return launch_wod<WO, ACT, 55>(a, B, s);
       default: break;
