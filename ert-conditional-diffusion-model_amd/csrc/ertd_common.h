@@ -172,6 +172,13 @@ hipError_t launch_encoder_train(const float* packed, const float* b1, const floa
 hipError_t launch_encoder_strips(const float* packed, const float* b1, const float* b2,
                                  const float* cond, long long cstride, int B, int L,
                                  int precision, float* partial, hipStream_t s);
+// conv part of the encoder backward given g = dL/d(pool mean) / L2 (B, 64)
+// (train.hip; the U-Net train step)
+size_t encoder_bwd_ws_floats(int B, int L);
+hipError_t launch_encoder_conv_backward(const float* packed, const float* cond, const float* a1,
+                                        const unsigned char* m2, const float* g, int B, int L,
+                                        float* ws, float* dw1, float* db1, float* dw2, float* db2,
+                                        hipStream_t s);
 // Same, plus one extra block computing the time row v(t) = W0t.relu(Wt.e(t)+bt)
 // into V[t] (faithful sampler: the row the next head_step launch consumes).
 struct TimeRowArgs {

@@ -477,6 +477,38 @@ hipError_t launch_train_backward(const ertd_weights& w, const float* packed, con
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Encoder backward for another head (the U-Net's cond_proj): the conv part of
+// the reference encoder's backward given g = dL/d(pool mean) / L2 per member
+// (B, 64) -- the same conv_bwd / reduce kernels as the reference train step.
+// ws: encoder_bwd_ws_floats(B, L) floats.
+// ---------------------------------------------------------------------------
+__global__ void put_g_kernel(const float* __restrict__ g, int B, float* __restrict__ vec) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C2) return;
+  const int b = i / C2, c = i - b * C2;
+  vec[(size_t)b * TV + TV_G + c] = g[i];
+}
+
+size_t encoder_bwd_ws_floats(int B, int L) {
+  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
+  return ((size_t)B * TV + 63) / 64 * 64 + (size_t)B * S * NG;
+}
+
+hipError_t launch_encoder_conv_backward(const float* packed, const float* cond, const float* a1,
+                                        const unsigned char* m2, const float* g, int B, int L,
+                                        float* ws, float* dw1, float* db1, float* dw2, float* db2,
+                                        hipStream_t s) {
+  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
+  float* vec = ws;
+  float* gpart = ws + ((size_t)B * TV + 63) / 64 * 64;
+  put_g_kernel<<<(B * C2 + 255) / 256, 256, 0, s>>>(g, B, vec);
+  conv_bwd_kernel<<<dim3((unsigned)(B * S)), 256, 0, s>>>(packed, cond, a1, m2, vec, L, L1, L2, S,
+                                                          gpart);
+  conv_grad_reduce_kernel<<<(NG + 31) / 32, 256, 0, s>>>(gpart, B * S, dw1, dw2, db1, db2);
+  return hipGetLastError();
+}
+
 hipError_t launch_adam(const ertd_weights& w, float* const* grads, float* const* exp_avg,
                        float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
                        float eps, hipStream_t s) {

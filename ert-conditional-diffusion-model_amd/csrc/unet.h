@@ -75,6 +75,7 @@ struct GnArgs {
   int HW, groups;
   const float* gamma; const float* beta;
   float2* out;           // (B, Ca+Cb) {gamma*rstd, beta - mean*gamma*rstd}
+  float2* mr;            // optional (B, groups) {mean, rstd} (training: GroupNorm backward)
 };
 hipError_t launch_gn_stats(const GnArgs& a, int B, hipStream_t s);
 // GroupNorm statistics + apply (+ SiLU) + bf16 image of a 3x3 stride-1 bf16

@@ -67,6 +67,7 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(GnArgs a) {
   double var = SS / n - mean * mean;
   var = var > 0.0 ? var : 0.0;
   const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
+  if (a.mr && tid == 0) a.mr[(size_t)b * a.groups + g] = make_float2((float)mean, rstd);
   // a group may hold more channels than the workgroup has threads (groups=1
   // at C=512): every channel of the group gets its {scale, shift}
   for (int cl = tid; cl < cpg; cl += 256) {

@@ -1,0 +1,678 @@
+// Training (backward) operators of the build-defined U-Net (SURVEY.md 8a';
+// north_star "sampler/trainer", the reference train step
+// ERT_Conditional_Diffusion.py:305-320 around the U-Net).  PARITY UNPINNED vs
+// the reference (no U-Net there): checked against torch autograd on
+// oracle/unet_torch.py (tests/test_gpu_unet_train.py).
+//
+// The host walk (ertdiff/unet_train.py) composes these with the forward
+// operators (ertd_conv2d, ertd_group_norm_stats):
+//   ertd_gn_stats_mr          GroupNorm statistics + (mean, rstd) per group
+//   ertd_gn_act_apply         act(GroupNorm(cat(x, x2))) materialized (the conv input a wgrad needs)
+//   ertd_gn_act_backward      dL/dx of act(GroupNorm(x)) (+ per-sample dgamma / dbeta partials)
+//   ertd_im2col               the (C*k*k, Ho*Wo) patch matrix of a conv input (stride 1 / 2 /
+//                             nearest-x2 upsample modes)
+//   ertd_wgrad_gemm           dW = sum_b dY_b . Xcol_b^T on fp32 MFMA, split over samples,
+//                             fixed-order reduction
+//   ertd_conv_weight_flip     W'[ci][co] = W[co][ci] flipped: dX of a conv is a conv of dY
+//   ertd_zero_insert / ertd_sum_pool2   stride-2 / upsample dX plumbing
+//   ertd_channel_sums         per (sample, channel) and per channel sums (bias / emb grads)
+//   ertd_reduce_rows          fixed-order sum over rows (per-sample partials -> grads)
+//   ertd_gemm_small           strided batched fp32 GEMM (+ bias / accumulate): dense layers,
+//                             attention forward / backward
+//   ertd_softmax_rows / ertd_softmax_backward   attention softmax and its backward
+//   ertd_eltwise              silu / silu-backward / relu-backward / add / scale / pool-mean
+//   ertd_mse_loss             MSELoss(mean) and dL/deps
+//   ertd_encoder_train_fwd / ertd_encoder_train_bwd   the reference condition encoder
+//                             (conv strips with saved activations; backward reused from
+//                             the reference train step, train.hip)
+//   ertd_adam_multi           torch.optim.Adam over any number of tensors
+// Every reduction has a fixed order: results are bitwise reproducible.
+#include <cmath>
+#include <cstring>
+
+#include "unet.h"
+
+using namespace ertd;
+using namespace ertd::unet;
+
+namespace {
+
+inline int rcode(hipError_t e) { return e == hipSuccess ? ERTD_OK : (int)e; }
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+__device__ __forceinline__ float silu_grad(float x) {
+  const float s = 1.0f / (1.0f + expf(-x));
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// ---- GroupNorm (+SiLU) apply ------------------------------------------------------
+__global__ void gn_act_apply_kernel(const float* __restrict__ xa, int Ca, const float* __restrict__ xb,
+                                    int Cb, int HW, const float2* __restrict__ ss, int act, size_t n,
+                                    float* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int C = Ca + Cb;
+  const size_t bc = i / HW;
+  const int p = (int)(i - bc * HW);
+  const int b = (int)(bc / C), c = (int)(bc - (size_t)b * C);
+  const float x = c < Ca ? xa[((size_t)b * Ca + c) * HW + p] : xb[((size_t)b * Cb + c - Ca) * HW + p];
+  const float2 g = ss[bc];
+  float v = fmaf(x, g.x, g.y);
+  if (act == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+  out[i] = v;
+}
+
+// ---- GroupNorm (+SiLU) backward: one 256-thread workgroup per (group, sample).
+// xhat = (x - mean) rstd, xn = gamma xhat + beta, y = act(xn):
+//   dxn = dy act'(xn); dgamma_c += sum dxn xhat, dbeta_c += sum dxn (per sample)
+//   dx = rstd (dxhat - mean_g(dxhat) - xhat mean_g(dxhat xhat)),  dxhat = gamma dxn
+__device__ __forceinline__ double wg_sum(double v, double* red, int tid) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void gn_act_bwd_kernel(
+    const float* __restrict__ xa, int Ca, const float* __restrict__ xb, int Cb, int HW, int groups,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float2* __restrict__ mr,
+    int act, const float* __restrict__ dy, float* __restrict__ dxa, float* __restrict__ dxb,
+    int accumulate, float* __restrict__ dgb) {
+  __shared__ double red[4];
+  const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int C = Ca + Cb, cpg = C / groups;
+  const float2 m = mr[(size_t)b * groups + g];
+  const float mean = m.x, rstd = m.y;
+  double A = 0.0, Bs = 0.0;
+  for (int cl = 0; cl < cpg; ++cl) {
+    const int c = g * cpg + cl;
+    const float* x = c < Ca ? xa + ((size_t)b * Ca + c) * HW : xb + ((size_t)b * Cb + c - Ca) * HW;
+    const float* d = dy + ((size_t)b * C + c) * HW;
+    const float ga = gamma[c], be = beta[c];
+    double sg = 0.0, sb = 0.0;
+    for (int p = tid; p < HW; p += 256) {
+      const float xh = (x[p] - mean) * rstd;
+      float dxn = d[p];
+      if (act == ACT_GN_SILU) dxn = dxn * silu_grad(fmaf(ga, xh, be));
+      sg += (double)dxn * xh;
+      sb += (double)dxn;
+    }
+    sg = wg_sum(sg, red, tid);
+    sb = wg_sum(sb, red, tid);
+    if (tid == 0) {
+      dgb[(size_t)b * C + c] = (float)sg;                        // plane 0: dgamma partial
+      dgb[(size_t)(gridDim.y + b) * C + c] = (float)sb;         // plane 1: dbeta partial
+    }
+    A += (double)ga * sb;     // sum dxhat
+    Bs += (double)ga * sg;    // sum dxhat xhat
+  }
+  const double n = (double)cpg * HW;
+  const float mA = (float)(A / n), mB = (float)(Bs / n);
+  for (int cl = 0; cl < cpg; ++cl) {
+    const int c = g * cpg + cl;
+    const float* x = c < Ca ? xa + ((size_t)b * Ca + c) * HW : xb + ((size_t)b * Cb + c - Ca) * HW;
+    float* dx = c < Ca ? dxa + ((size_t)b * Ca + c) * HW : dxb + ((size_t)b * Cb + c - Ca) * HW;
+    const float* d = dy + ((size_t)b * C + c) * HW;
+    const float ga = gamma[c], be = beta[c];
+    for (int p = tid; p < HW; p += 256) {
+      const float xh = (x[p] - mean) * rstd;
+      float dxn = d[p];
+      if (act == ACT_GN_SILU) dxn = dxn * silu_grad(fmaf(ga, xh, be));
+      const float v = rstd * ((ga * dxn - mA) - xh * mB);
+      dx[p] = accumulate ? dx[p] + v : v;
+    }
+  }
+}
+
+// ---- im2col: out[b][c*kk + tap][q] for output pixel q of the conv --------------------
+__global__ void im2col_kernel(const float* __restrict__ x, int C, int H, int ks, int mode, int Ho,
+                              size_t n, float* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int HWo = Ho * Ho, kk = ks * ks;
+  const size_t row = i / HWo;
+  const int q = (int)(i - row * HWo);
+  const int b = (int)(row / ((size_t)C * kk));
+  const int r = (int)(row - (size_t)b * C * kk);
+  const int c = r / kk, tap = r - c * kk;
+  const int ky = tap / ks, kx = tap - ky * ks;
+  const int oy = q / Ho, ox = q - oy * Ho;
+  int iy, ix, lim = H;
+  if (ks == 1) { iy = oy; ix = ox; }
+  else if (mode == MODE_S2) { iy = 2 * oy - 1 + ky; ix = 2 * ox - 1 + kx; }
+  else if (mode == MODE_UP) { iy = oy - 1 + ky; ix = ox - 1 + kx; lim = 2 * H; }
+  else { iy = oy - 1 + ky; ix = ox - 1 + kx; }
+  float v = 0.f;
+  if (iy >= 0 && iy < lim && ix >= 0 && ix < lim) {
+    if (mode == MODE_UP && ks == 3) { iy >>= 1; ix >>= 1; }
+    v = x[((size_t)b * C + c) * H * H + (size_t)iy * H + ix];
+  }
+  out[i] = v;
+}
+
+// ---- dW partial of one sample: C[m][n] = sum_p A[m][p] B[n][p] on fp32 MFMA.
+// WG = 4 waves, 64 (m) x 64 (n) tile, K chunks of 32 pixels staged in LDS.
+__global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
+                                                    int M, int N, int P, size_t bsA, size_t bsB,
+                                                    float* __restrict__ part, int split_len,
+                                                    int nsplit_per_b) {
+  __shared__ float As[32][65];
+  __shared__ float Bs[32][65];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const int split = blockIdx.z;
+  const int b = split / nsplit_per_b, sp = split - b * nsplit_per_b;
+  const int p_lo = sp * split_len, p_hi = min(P, p_lo + split_len);
+  const float* Ab = A + (size_t)b * bsA;
+  const float* Bb = Bm + (size_t)b * bsB;
+  const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
+  f32x16 acc = {};
+  for (int p0 = p_lo; p0 < p_hi; p0 += 32) {
+    for (int idx = tid; idx < 64 * 32; idx += 256) {
+      const int r = idx >> 5, k = idx & 31;
+      const int p = p0 + k;
+      As[k][r] = (m0 + r < M && p < p_hi) ? Ab[(size_t)(m0 + r) * P + p] : 0.f;
+      Bs[k][r] = (n0 + r < N && p < p_hi) ? Bb[(size_t)(n0 + r) * P + p] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+      const float a = As[2 * s + h][wm + l32];
+      const float bb = Bs[2 * s + h][wn + l32];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* Cp = part + (size_t)split * M * N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h, n = n0 + wn + l32;
+    if (m < M && n < N) Cp[(size_t)m * N + n] = acc[r];
+  }
+}
+
+__global__ void reduce_rows_kernel(const float* __restrict__ part, int rows, size_t cols,
+                                   float* __restrict__ out, int accumulate) {
+  const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += part[(size_t)r * cols + j];
+  out[j] = accumulate ? out[j] + s : s;
+}
+
+__global__ void weight_flip_kernel(const float* __restrict__ w, int Cout, int Cin, int ks,
+                                   float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int kk = ks * ks;
+  if (i >= Cout * Cin * kk) return;
+  const int tap = i % kk, r = i / kk;
+  const int co = r % Cout, ci = r / Cout;   // out is (Cin, Cout, ks, ks)
+  const int ky = tap / ks, kx = tap % ks;
+  out[i] = w[((size_t)co * Cin + ci) * kk + (ks - 1 - ky) * ks + (ks - 1 - kx)];
+}
+
+__global__ void zero_insert_kernel(const float* __restrict__ x, int Ho, size_t n, float* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // over the 2Ho x 2Ho output
+  if (i >= n) return;
+  const int W2 = 2 * Ho;
+  const size_t bc = i / ((size_t)W2 * W2);
+  const int q = (int)(i - bc * W2 * W2);
+  const int y = q / W2, xx = q - y * W2;
+  out[i] = ((y | xx) & 1) ? 0.f : x[bc * Ho * Ho + (size_t)(y >> 1) * Ho + (xx >> 1)];
+}
+
+__global__ void sum_pool2_kernel(const float* __restrict__ x, int H, size_t n, float* __restrict__ out,
+                                 int accumulate) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // over the H x H output
+  if (i >= n) return;
+  const size_t bc = i / ((size_t)H * H);
+  const int q = (int)(i - bc * H * H);
+  const int y = q / H, xx = q - y * H;
+  const float* s = x + bc * 4 * H * H;
+  const int W2 = 2 * H;
+  const float v = (s[(size_t)(2 * y) * W2 + 2 * xx] + s[(size_t)(2 * y) * W2 + 2 * xx + 1]) +
+                  (s[(size_t)(2 * y + 1) * W2 + 2 * xx] + s[(size_t)(2 * y + 1) * W2 + 2 * xx + 1]);
+  out[i] = accumulate ? out[i] + v : v;
+}
+
+// per (sample, channel) sum over HW (one workgroup each, fixed order)
+__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ x, int HW,
+                                                       float* __restrict__ out) {
+  __shared__ double red[4];
+  const size_t bc = blockIdx.x;
+  const float* s = x + bc * HW;
+  double acc = 0.0;
+  for (int p = threadIdx.x; p < HW; p += 256) acc += (double)s[p];
+  acc = wg_sum(acc, red, threadIdx.x);
+  if (threadIdx.x == 0) out[bc] = (float)acc;
+}
+
+// ---- small strided batched GEMM (fp32 FMA, 32x32 tile per workgroup)
+struct SmallGemm {
+  const float* A; long long a_i, a_k, a_b;
+  const float* Bm; long long b_k, b_j, b_b;
+  float* C; long long c_i, c_j, c_b;
+  const float* bias;   // per column j, or null
+  int I, J, K;
+  float alpha;
+  int accumulate;
+};
+
+__global__ __launch_bounds__(256) void gemm_small_kernel(SmallGemm g) {
+  __shared__ float As[32][33];
+  __shared__ float Bs[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32, bt = blockIdx.z;
+  const float* A = g.A + bt * g.a_b;
+  const float* Bm = g.Bm + bt * g.b_b;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < g.K; k0 += 32) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = ty + 8 * r;
+      As[ii][tx] = (i0 + ii < g.I && k0 + tx < g.K) ? A[(i0 + ii) * g.a_i + (k0 + tx) * g.a_k] : 0.f;
+      Bs[ii][tx] = (k0 + ii < g.K && j0 + tx < g.J) ? Bm[(k0 + ii) * g.b_k + (j0 + tx) * g.b_j] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const float bv = Bs[k][tx];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = fmaf(As[ty + 8 * r][k], bv, acc[r]);
+    }
+    __syncthreads();
+  }
+  float* C = g.C + bt * g.c_b;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + ty + 8 * r, j = j0 + tx;
+    if (i < g.I && j < g.J) {
+      float v = g.alpha * acc[r];
+      if (g.bias) v = v + g.bias[j];
+      float* cp = C + i * g.c_i + j * g.c_j;
+      *cp = g.accumulate ? *cp + v : v;
+    }
+  }
+}
+
+// softmax over rows of length N (one workgroup per row), P = softmax(scale * S)
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ S, int N, float scale,
+                                                           float* __restrict__ P) {
+  __shared__ float red[4];
+  const size_t row = blockIdx.x;
+  const float* s = S + row * N;
+  float m = -INFINITY;
+  for (int j = threadIdx.x; j < N; j += 256) m = fmaxf(m, s[j] * scale);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = threadIdx.x; j < N; j += 256) sum += expf(s[j] * scale - m);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  sum = (red[0] + red[1]) + (red[2] + red[3]);
+  for (int j = threadIdx.x; j < N; j += 256) P[row * N + j] = expf(s[j] * scale - m) / sum;
+}
+
+// dS = scale * P (dP - rowsum(dP P))
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restrict__ P,
+                                                          const float* __restrict__ dP, int N,
+                                                          float scale, float* __restrict__ dS) {
+  __shared__ float red[4];
+  const size_t row = blockIdx.x;
+  const float* p = P + row * N;
+  const float* d = dP + row * N;
+  float acc = 0.f;
+  for (int j = threadIdx.x; j < N; j += 256) acc = fmaf(p[j], d[j], acc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float dot = (red[0] + red[1]) + (red[2] + red[3]);
+  for (int j = threadIdx.x; j < N; j += 256) dS[row * N + j] = scale * (p[j] * (d[j] - dot));
+}
+
+// elementwise ops (ertd_eltwise)
+enum Elt { ELT_SILU = 0, ELT_SILU_BWD = 1, ELT_RELU = 2, ELT_RELU_BWD = 3, ELT_ADD = 4,
+           ELT_SCALE = 5, ELT_COPY_STRIDED = 6 };
+__global__ void eltwise_kernel(int op, const float* __restrict__ x, const float* __restrict__ y,
+                               float* __restrict__ out, size_t n, float alpha, int accumulate) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float v;
+  switch (op) {
+    case ELT_SILU: v = silu_f(x[i]); break;
+    case ELT_SILU_BWD: v = y[i] * silu_grad(x[i]); break;   // x = pre-activation, y = dL/dout
+    case ELT_RELU: v = fmaxf(x[i], 0.f); break;
+    case ELT_RELU_BWD: v = x[i] > 0.f ? y[i] : 0.f; break;
+    case ELT_ADD: v = x[i] + y[i]; break;
+    default: v = alpha * x[i]; break;
+  }
+  out[i] = accumulate ? out[i] + v : v;
+}
+
+// dst[b][d0 + c][p] (+)= src[b][c0 + c][p] for c < Cd: channel slices of (B, C, HW) tensors
+__global__ void chan_slice_kernel(const float* __restrict__ src, int Cs, int c0, int Cd, int HW,
+                                  size_t n, float* __restrict__ dst, int Cdst, int d0,
+                                  int accumulate) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const size_t bc = i / HW;
+  const int p = (int)(i - bc * HW);
+  const int b = (int)(bc / Cd), c = (int)(bc - (size_t)b * Cd);
+  const float v = src[((size_t)b * Cs + c0 + c) * HW + p];
+  float* d = dst + ((size_t)b * Cdst + d0 + c) * HW + p;
+  *d = accumulate ? *d + v : v;
+}
+
+// MSELoss(mean): loss = sum (e - z)^2 / n (fixed order: one workgroup), dout = 2 (e - z) / n
+__global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ e, const float* __restrict__ z,
+                                                  size_t n, float* __restrict__ loss,
+                                                  float* __restrict__ dout) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  const float two_n = (float)(2.0 / (double)n);
+  for (size_t i = threadIdx.x; i < n; i += 256) {
+    const float d = e[i] - z[i];
+    acc += (double)d * d;
+    if (dout) dout[i] = two_n * d;
+  }
+  acc = wg_sum(acc, red, threadIdx.x);
+  if (threadIdx.x == 0) *loss = (float)(acc / (double)n);
+}
+
+// pool mean of the encoder strips' partial sums: m[b][c] = sum_s partial[b][s][c] / L2
+__global__ void pool_mean_kernel(const float* __restrict__ partial, int S, int L2, int B,
+                                 float* __restrict__ m) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C2) return;
+  const int b = i / C2, c = i - b * C2;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += partial[((size_t)b * S + k) * C2 + c];
+  m[i] = s / (float)L2;
+}
+
+// torch.optim.Adam over up to 32 tensors per launch
+constexpr int ADAM_T = 32;
+struct AdamMulti {
+  float* p[ADAM_T];
+  const float* g[ADAM_T];
+  float* m[ADAM_T];
+  float* v[ADAM_T];
+  long long off[ADAM_T + 1];
+  int nt;
+  float one_minus_b1, b2, one_minus_b2, step_size_neg, bc2_sqrt, eps;
+};
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.off[a.nt]) return;
+  int k = 0;
+  while (k + 1 < a.nt && i >= a.off[k + 1]) ++k;
+  const long long e = i - a.off[k];
+  const float g = a.g[k][e];
+  float m = a.m[k][e];
+  m = m + a.one_minus_b1 * (g - m);                 // exp_avg.lerp_(grad, 1 - beta1)
+  float v = a.v[k][e] * a.b2;                       // exp_avg_sq.mul_(beta2)
+  v = v + a.one_minus_b2 * g * g;                   //   .addcmul_(grad, grad, 1 - beta2)
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  a.p[k][e] = a.p[k][e] + a.step_size_neg * (m / denom);
+  a.m[k][e] = m;
+  a.v[k][e] = v;
+}
+
+inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+extern "C" {
+
+int ertd_gn_stats_mr(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                     const float* gamma, const float* beta, float* ss_out, float* mr_out,
+                     void* stream) {
+  const int C = Ca + Cb;
+  if (!x || !gamma || !beta || !ss_out || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
+      groups < 1 || C % groups || HW < 4 || HW % 4)
+    return ERTD_EINVAL;
+  GnArgs g{x, x2, Ca, Cb, HW, groups, gamma, beta, (float2*)ss_out, (float2*)mr_out};
+  return rcode(launch_gn_stats(g, B, (hipStream_t)stream));
+}
+
+int ertd_gn_act_apply(const float* x, int Ca, const float* x2, int Cb, int B, int HW,
+                      const float* ss, int act, float* out, void* stream) {
+  if (!x || !ss || !out || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) || HW < 1 ||
+      (act != ACT_GN_SILU && act != ACT_GN))
+    return ERTD_EINVAL;
+  const size_t n = (size_t)B * (Ca + Cb) * HW;
+  gn_act_apply_kernel<<<nblk(n), 256, 0, (hipStream_t)stream>>>(x, Ca, x2, Cb, HW, (const float2*)ss,
+                                                                 act, n, out);
+  return rcode(hipGetLastError());
+}
+
+int ertd_gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                         const float* gamma, const float* beta, const float* mr, int act,
+                         const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
+                         void* stream) {
+  const int C = Ca + Cb;
+  if (!x || !gamma || !beta || !mr || !dy || !dx || !dgb_part || B < 1 || Ca < 1 || Cb < 0 ||
+      (Cb > 0 && (!x2 || !dx2)) || groups < 1 || C % groups || HW < 1 ||
+      (act != ACT_GN_SILU && act != ACT_GN))
+    return ERTD_EINVAL;
+  gn_act_bwd_kernel<<<dim3(groups, B), 256, 0, (hipStream_t)stream>>>(
+      x, Ca, x2, Cb, HW, groups, gamma, beta, (const float2*)mr, act, dy, dx, dx2, accumulate,
+      dgb_part);
+  return rcode(hipGetLastError());
+}
+
+int ertd_im2col(const float* x, int C, int B, int H, int ks, int mode, float* out, void* stream) {
+  if (!x || !out || C < 1 || B < 1 || H < 1 || (ks != 1 && ks != 3) || mode < MODE_S1 ||
+      mode > MODE_UP || (ks == 1 && mode != MODE_S1))
+    return ERTD_EINVAL;
+  const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  const size_t n = (size_t)B * C * ks * ks * Ho * Ho;
+  im2col_kernel<<<nblk(n), 256, 0, (hipStream_t)stream>>>(x, C, H, ks, mode, Ho, n, out);
+  return rcode(hipGetLastError());
+}
+
+size_t ertd_wgrad_ws_bytes(int M, int N, int P, int B) {
+  if (M < 1 || N < 1 || P < 1 || B < 1) return 0;
+  const int nsp = (P + 4095) / 4096;
+  return (size_t)B * nsp * M * N * sizeof(float);
+}
+
+int ertd_wgrad_gemm(const float* dY, const float* X, int M, int N, int P, int B, long long bsA,
+                    long long bsB, float* dW, int accumulate, void* ws, size_t ws_bytes,
+                    void* stream) {
+  if (!dY || !X || !dW || !ws || M < 1 || N < 1 || P < 1 || B < 1) return ERTD_EINVAL;
+  if (ertd_wgrad_ws_bytes(M, N, P, B) > ws_bytes) return ERTD_ENOSPC;
+  const int split_len = 4096, nsp = (P + split_len - 1) / split_len;
+  hipStream_t s = (hipStream_t)stream;
+  wgrad_kernel<<<dim3((N + 63) / 64, (M + 63) / 64, B * nsp), 256, 0, s>>>(
+      dY, X, M, N, P, (size_t)bsA, (size_t)bsB, (float*)ws, split_len, nsp);
+  const size_t cols = (size_t)M * N;
+  reduce_rows_kernel<<<nblk(cols), 256, 0, s>>>((const float*)ws, B * nsp, cols, dW, accumulate);
+  return rcode(hipGetLastError());
+}
+
+int ertd_reduce_rows(const float* part, int rows, long long cols, float* out, int accumulate,
+                     void* stream) {
+  if (!part || !out || rows < 1 || cols < 1) return ERTD_EINVAL;
+  reduce_rows_kernel<<<nblk((size_t)cols), 256, 0, (hipStream_t)stream>>>(part, rows, (size_t)cols,
+                                                                         out, accumulate);
+  return rcode(hipGetLastError());
+}
+
+int ertd_conv_weight_flip(const float* w, int Cout, int Cin, int ks, float* out, void* stream) {
+  if (!w || !out || Cout < 1 || Cin < 1 || (ks != 1 && ks != 3)) return ERTD_EINVAL;
+  weight_flip_kernel<<<nblk((size_t)Cout * Cin * ks * ks), 256, 0, (hipStream_t)stream>>>(w, Cout, Cin,
+                                                                                          ks, out);
+  return rcode(hipGetLastError());
+}
+
+int ertd_zero_insert(const float* x, int B, int C, int Ho, float* out, void* stream) {
+  if (!x || !out || B < 1 || C < 1 || Ho < 1) return ERTD_EINVAL;
+  const size_t n = (size_t)B * C * 4 * Ho * Ho;
+  zero_insert_kernel<<<nblk(n), 256, 0, (hipStream_t)stream>>>(x, Ho, n, out);
+  return rcode(hipGetLastError());
+}
+
+int ertd_sum_pool2(const float* x, int B, int C, int H, float* out, int accumulate, void* stream) {
+  if (!x || !out || B < 1 || C < 1 || H < 1) return ERTD_EINVAL;
+  const size_t n = (size_t)B * C * H * H;
+  sum_pool2_kernel<<<nblk(n), 256, 0, (hipStream_t)stream>>>(x, H, n, out, accumulate);
+  return rcode(hipGetLastError());
+}
+
+int ertd_channel_sums(const float* x, int B, int C, int HW, float* out_bc, float* out_c,
+                      int accumulate_c, void* stream) {
+  if (!x || !out_bc || B < 1 || C < 1 || HW < 1) return ERTD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  chan_sum_kernel<<<(unsigned)((size_t)B * C), 256, 0, s>>>(x, HW, out_bc);
+  if (out_c) reduce_rows_kernel<<<nblk((size_t)C), 256, 0, s>>>(out_bc, B, (size_t)C, out_c, accumulate_c);
+  return rcode(hipGetLastError());
+}
+
+int ertd_gemm_small(const float* A, long long a_i, long long a_k, long long a_b, const float* Bm,
+                    long long b_k, long long b_j, long long b_b, float* C, long long c_i,
+                    long long c_j, long long c_b, const float* bias, int I, int J, int K, int batch,
+                    float alpha, int accumulate, void* stream) {
+  if (!A || !Bm || !C || I < 1 || J < 1 || K < 1 || batch < 1) return ERTD_EINVAL;
+  SmallGemm g{A, a_i, a_k, a_b, Bm, b_k, b_j, b_b, C, c_i, c_j, c_b, bias, I, J, K, alpha, accumulate};
+  gemm_small_kernel<<<dim3((J + 31) / 32, (I + 31) / 32, batch), 256, 0, (hipStream_t)stream>>>(g);
+  return rcode(hipGetLastError());
+}
+
+int ertd_softmax_rows(const float* S, long long rows, int N, float scale, float* P, void* stream) {
+  if (!S || !P || rows < 1 || N < 1) return ERTD_EINVAL;
+  softmax_rows_kernel<<<(unsigned)rows, 256, 0, (hipStream_t)stream>>>(S, N, scale, P);
+  return rcode(hipGetLastError());
+}
+
+int ertd_softmax_backward(const float* P, const float* dP, long long rows, int N, float scale,
+                          float* dS, void* stream) {
+  if (!P || !dP || !dS || rows < 1 || N < 1) return ERTD_EINVAL;
+  softmax_bwd_kernel<<<(unsigned)rows, 256, 0, (hipStream_t)stream>>>(P, dP, N, scale, dS);
+  return rcode(hipGetLastError());
+}
+
+int ertd_eltwise(int op, const float* x, const float* y, float* out, long long n, float alpha,
+                 int accumulate, void* stream) {
+  if (!x || !out || n < 1 || op < ELT_SILU || op > ELT_SCALE ||
+      ((op == ELT_SILU_BWD || op == ELT_RELU_BWD || op == ELT_ADD) && !y))
+    return ERTD_EINVAL;
+  eltwise_kernel<<<nblk((size_t)n), 256, 0, (hipStream_t)stream>>>(op, x, y, out, (size_t)n, alpha,
+                                                                   accumulate);
+  return rcode(hipGetLastError());
+}
+
+int ertd_channel_slice(const float* src, int B, int Cs, int c0, int Cd, int HW, float* dst,
+                       int Cdst, int d0, int accumulate, void* stream) {
+  if (!src || !dst || B < 1 || Cd < 1 || c0 < 0 || c0 + Cd > Cs || d0 < 0 || d0 + Cd > Cdst ||
+      HW < 1)
+    return ERTD_EINVAL;
+  const size_t n = (size_t)B * Cd * HW;
+  chan_slice_kernel<<<nblk(n), 256, 0, (hipStream_t)stream>>>(src, Cs, c0, Cd, HW, n, dst, Cdst, d0,
+                                                              accumulate);
+  return rcode(hipGetLastError());
+}
+
+int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss, float* dout,
+                  void* stream) {
+  if (!eps || !noise || !loss || n < 1) return ERTD_EINVAL;
+  mse_kernel<<<1, 256, 0, (hipStream_t)stream>>>(eps, noise, (size_t)n, loss, dout);
+  return rcode(hipGetLastError());
+}
+
+// the reference condition encoder with saved activations: partial (B,S,64),
+// a1 (B,32,L1), relu mask m2 (B,64,L2) bytes, pool mean m (B,64); packed =
+// the reference-layout packing (ertd_pack_weights) of the current encoder weights
+size_t ertd_encoder_train_ws_bytes(int B, int L) {
+  if (B < 1 || L < 1) return 0;
+  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
+  size_t f = (size_t)B * S * C2 + (size_t)B * C1 * L1 + ((size_t)B * C2 * L2 + 3) / 4 + 64 * 4 +
+             encoder_bwd_ws_floats(B, L);
+  return f * sizeof(float);
+}
+
+static void enc_layout(int B, int L, float* ws, float** partial, float** a1, unsigned char** m2,
+                       float** bw) {
+  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
+  size_t o = 0;
+  *partial = ws + o; o += ((size_t)B * S * C2 + 63) / 64 * 64;
+  *a1 = ws + o; o += ((size_t)B * C1 * L1 + 63) / 64 * 64;
+  *m2 = (unsigned char*)(ws + o); o += (((size_t)B * C2 * L2 + 3) / 4 + 63) / 64 * 64;
+  *bw = ws + o;
+}
+
+int ertd_encoder_train_fwd(const float* packed, const float* b1, const float* b2, const float* cond,
+                           int B, int L, float* m_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!packed || !b1 || !b2 || !cond || !m_out || !ws || B < 1 || L < 1) return ERTD_EINVAL;
+  if (ertd_encoder_train_ws_bytes(B, L) > ws_bytes) return ERTD_ENOSPC;
+  float *partial, *a1, *bw;
+  unsigned char* m2;
+  enc_layout(B, L, (float*)ws, &partial, &a1, &m2, &bw);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = launch_encoder_train(packed, b1, b2, cond, B, L, partial, a1, m2, s);
+  if (e != hipSuccess) return (int)e;
+  const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
+  pool_mean_kernel<<<nblk((size_t)B * C2), 256, 0, s>>>(partial, S, L2, B, m_out);
+  return rcode(hipGetLastError());
+}
+
+// g = dL/dm / L2 (B, 64) -> conv weight / bias grads of the encoder (after ertd_encoder_train_fwd on ws)
+int ertd_encoder_train_bwd(const float* packed, const float* cond, const float* g, int B, int L,
+                           float* dw1, float* db1, float* dw2, float* db2, void* ws,
+                           size_t ws_bytes, void* stream) {
+  if (!packed || !cond || !g || !dw1 || !db1 || !dw2 || !db2 || !ws || B < 1 || L < 1)
+    return ERTD_EINVAL;
+  if (ertd_encoder_train_ws_bytes(B, L) > ws_bytes) return ERTD_ENOSPC;
+  float *partial, *a1, *bw;
+  unsigned char* m2;
+  enc_layout(B, L, (float*)ws, &partial, &a1, &m2, &bw);
+  return rcode(launch_encoder_conv_backward(packed, cond, a1, m2, g, B, L, bw, dw1, db1, dw2, db2,
+                                            (hipStream_t)stream));
+}
+
+int ertd_adam_multi(float* const* params, const float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, const long long* sizes, int ntensors, int step,
+                    float lr, float beta1, float beta2, float eps, void* stream) {
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !sizes || ntensors < 1 || step < 1)
+    return ERTD_EINVAL;
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  hipStream_t s = (hipStream_t)stream;
+  for (int t0 = 0; t0 < ntensors; t0 += ADAM_T) {
+    AdamMulti a{};
+    a.nt = ntensors - t0 < ADAM_T ? ntensors - t0 : ADAM_T;
+    long long off = 0;
+    for (int k = 0; k < a.nt; ++k) {
+      a.p[k] = params[t0 + k];
+      a.g[k] = grads[t0 + k];
+      a.m[k] = exp_avg[t0 + k];
+      a.v[k] = exp_avg_sq[t0 + k];
+      a.off[k] = off;
+      off += sizes[t0 + k];
+    }
+    a.off[a.nt] = off;
+    // scalars formed as torch does: Python floats (double), rounded when applied to fp32
+    a.one_minus_b1 = (float)(1.0 - (double)beta1);
+    a.b2 = beta2;
+    a.one_minus_b2 = (float)(1.0 - (double)beta2);
+    a.step_size_neg = (float)(-((double)lr / bc1));
+    a.bc2_sqrt = (float)std::sqrt(bc2);
+    a.eps = eps;
+    adam_multi_kernel<<<nblk((size_t)off), 256, 0, s>>>(a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return ERTD_OK;
+}
+
+}  // extern "C"

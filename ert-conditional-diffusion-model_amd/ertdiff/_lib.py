@@ -44,6 +44,7 @@ class ErtdWeights(ctypes.Structure):
 # Exported symbol -> (restype, argtypes).  Every name declared in include/ertdiff.h.
 _VP, _I, _U32, _U64, _SZ, _F = (ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32,
                                 ctypes.c_uint64, ctypes.c_size_t, ctypes.c_float)
+_LL = ctypes.c_longlong
 _W = ctypes.POINTER(ErtdWeights)
 SIGNATURES = {
     "ertd_version": (_I, []),
@@ -90,6 +91,29 @@ SIGNATURES = {
     "ertd_unet_sample_plan_create": (_I, [_VP, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I,
                                           _VP, _VP, _VP, _VP, _U64, _U32, _VP, _VP, _SZ,
                                           ctypes.POINTER(_VP)]),
+    "ertd_gn_stats_mr": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP]),
+    "ertd_gn_act_apply": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _I, _VP, _VP]),
+    "ertd_gn_act_backward": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _I, _VP, _VP, _VP,
+                                  _I, _VP, _VP]),
+    "ertd_im2col": (_I, [_VP, _I, _I, _I, _I, _I, _VP, _VP]),
+    "ertd_wgrad_ws_bytes": (_SZ, [_I, _I, _I, _I]),
+    "ertd_wgrad_gemm": (_I, [_VP, _VP, _I, _I, _I, _I, _LL, _LL, _VP, _I, _VP, _SZ, _VP]),
+    "ertd_reduce_rows": (_I, [_VP, _I, _LL, _VP, _I, _VP]),
+    "ertd_conv_weight_flip": (_I, [_VP, _I, _I, _I, _VP, _VP]),
+    "ertd_zero_insert": (_I, [_VP, _I, _I, _I, _VP, _VP]),
+    "ertd_sum_pool2": (_I, [_VP, _I, _I, _I, _VP, _I, _VP]),
+    "ertd_channel_sums": (_I, [_VP, _I, _I, _I, _VP, _VP, _I, _VP]),
+    "ertd_gemm_small": (_I, [_VP, _LL, _LL, _LL, _VP, _LL, _LL, _LL, _VP, _LL, _LL, _LL, _VP, _I, _I,
+                             _I, _I, _F, _I, _VP]),
+    "ertd_softmax_rows": (_I, [_VP, _LL, _I, _F, _VP, _VP]),
+    "ertd_softmax_backward": (_I, [_VP, _VP, _LL, _I, _F, _VP, _VP]),
+    "ertd_eltwise": (_I, [_I, _VP, _VP, _VP, _LL, _F, _I, _VP]),
+    "ertd_channel_slice": (_I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I, _VP]),
+    "ertd_mse_loss": (_I, [_VP, _VP, _LL, _VP, _VP, _VP]),
+    "ertd_encoder_train_ws_bytes": (_SZ, [_I, _I]),
+    "ertd_encoder_train_fwd": (_I, [_VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _SZ, _VP]),
+    "ertd_encoder_train_bwd": (_I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "ertd_adam_multi": (_I, [_VP, _VP, _VP, _VP, _VP, _I, _I, _F, _F, _F, _F, _VP]),
     "ertd_unet_plan_launch": (_I, [_VP, _VP]),
     "ertd_unet_plan_launch_steps": (_I, [_VP, _I, _VP]),
     "ertd_unet_plan_destroy": (_I, [_VP]),

@@ -90,6 +90,11 @@ def train_step(model, optimizer, x0, cond, T, alpha_bar, *, t=None, noise=None,
     """One reference train step (:309-320); returns loss.item() (or the device
     scalar if ``return_tensor``).  t / noise default to the reference's draws
     (torch.randint then torch.randn_like, :312-313)."""
+    from .unet import ConditionalUNet
+    if isinstance(model, ConditionalUNet):   # the same call surface over the U-Net denoiser
+        from .unet_train import unet_train_step
+        return unet_train_step(model, optimizer, x0, cond, T, alpha_bar, t=t, noise=noise,
+                               return_tensor=return_tensor)
     model._check_supported()
     params = model._params()
     dev = _lib.require_device(x0, cond, alpha_bar, params[0])

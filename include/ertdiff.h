@@ -315,6 +315,76 @@ int ertd_unet_plan_launch(ertd_unet_plan* plan, void* stream);
 int ertd_unet_plan_launch_steps(ertd_unet_plan* plan, int n_steps, void* stream);
 int ertd_unet_plan_destroy(ertd_unet_plan* plan);
 
+/* ---- U-Net training operators (csrc/unet_train.hip; the reference train step
+ * ERT_Conditional_Diffusion.py:305-320 around the build-defined U-Net, walked
+ * by ertdiff/unet_train.py).  PARITY UNPINNED vs the reference (no U-Net
+ * there): checked against torch autograd on oracle/unet_torch.py.  All device
+ * pointers, enqueued on `stream`; `accumulate` = add into the output.
+ * ertd_gn_stats_mr: ertd_group_norm_stats + mr_out (B, groups) {mean, rstd}.
+ * ertd_gn_act_apply: out (B, Ca+Cb, HW) = act(cat(x, x2) * ss.x + ss.y), act 1 GN+SiLU / 2 GN.
+ * ertd_gn_act_backward: dx / dx2 of act(GroupNorm(cat(x, x2))) given dy (B, C, HW);
+ *   dgb_part (2, B, C): per-sample sum dxn*xhat (plane 0) and sum dxn (plane 1) ->
+ *   dgamma / dbeta by ertd_reduce_rows.
+ * ertd_im2col: out (B, C*ks*ks, Ho*Ho) patches of x (B, C, H, H), mode 0 s1 / 1 s2 / 2 upsample.
+ * ertd_wgrad_gemm: dW (M, N) = sum_b dY_b (M, P) . X_b (N, P)^T (batch strides bsA, bsB),
+ *   fp32 MFMA, split per sample + fixed-order reduction; ws >= ertd_wgrad_ws_bytes.
+ * ertd_conv_weight_flip: out (Cin, Cout, ks, ks) = w (Cout, Cin, ks, ks) spatially flipped.
+ * ertd_zero_insert: out (B, C, 2Ho, 2Ho) with x at even positions; ertd_sum_pool2: 2x2 sums.
+ * ertd_channel_sums: out_bc (B, C) sums over HW; out_c (C) = sum over b (optional).
+ * ertd_gemm_small: C[b][i][j] = alpha sum_k A[b][i][k] B[b][k][j] (+ bias[j]) with element
+ *   strides (a_i, a_k, a_b, b_k, b_j, b_b, c_i, c_j, c_b).
+ * ertd_softmax_rows: P = softmax(scale S) per row; ertd_softmax_backward: dS = scale P (dP - <dP, P>).
+ * ertd_eltwise: op 0 silu(x), 1 y silu'(x), 2 relu(x), 3 y [x > 0], 4 x + y, 5 alpha x.
+ * ertd_channel_slice: dst (B, Cdst, HW) channels [d0, d0+Cd) (+)= src (B, Cs, HW) channels
+ *   [c0, c0+Cd).
+ * ertd_mse_loss: loss (1) = mean (eps - noise)^2, dout = 2 (eps - noise) / n (optional).
+ * ertd_encoder_train_fwd / _bwd: the reference condition encoder (:133-142) with saved
+ *   activations in ws (pool mean m (B, 64) out) / conv-parameter grads from g = dL/dm / L.
+ * ertd_adam_multi: torch.optim.Adam step (no weight decay) over ntensors tensors.        */
+int ertd_gn_stats_mr(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                     const float* gamma, const float* beta, float* ss_out, float* mr_out,
+                     void* stream);
+int ertd_gn_act_apply(const float* x, int Ca, const float* x2, int Cb, int B, int HW,
+                      const float* ss, int act, float* out, void* stream);
+int ertd_gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                         const float* gamma, const float* beta, const float* mr, int act,
+                         const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
+                         void* stream);
+int ertd_im2col(const float* x, int C, int B, int H, int ks, int mode, float* out, void* stream);
+size_t ertd_wgrad_ws_bytes(int M, int N, int P, int B);
+int ertd_wgrad_gemm(const float* dY, const float* X, int M, int N, int P, int B, long long bsA,
+                    long long bsB, float* dW, int accumulate, void* ws, size_t ws_bytes,
+                    void* stream);
+int ertd_reduce_rows(const float* part, int rows, long long cols, float* out, int accumulate,
+                     void* stream);
+int ertd_conv_weight_flip(const float* w, int Cout, int Cin, int ks, float* out, void* stream);
+int ertd_zero_insert(const float* x, int B, int C, int Ho, float* out, void* stream);
+int ertd_sum_pool2(const float* x, int B, int C, int H, float* out, int accumulate, void* stream);
+int ertd_channel_sums(const float* x, int B, int C, int HW, float* out_bc, float* out_c,
+                      int accumulate_c, void* stream);
+int ertd_gemm_small(const float* A, long long a_i, long long a_k, long long a_b, const float* Bm,
+                    long long b_k, long long b_j, long long b_b, float* C, long long c_i,
+                    long long c_j, long long c_b, const float* bias, int I, int J, int K, int batch,
+                    float alpha, int accumulate, void* stream);
+int ertd_softmax_rows(const float* S, long long rows, int N, float scale, float* P, void* stream);
+int ertd_softmax_backward(const float* P, const float* dP, long long rows, int N, float scale,
+                          float* dS, void* stream);
+int ertd_eltwise(int op, const float* x, const float* y, float* out, long long n, float alpha,
+                 int accumulate, void* stream);
+int ertd_channel_slice(const float* src, int B, int Cs, int c0, int Cd, int HW, float* dst,
+                       int Cdst, int d0, int accumulate, void* stream);
+int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss, float* dout,
+                  void* stream);
+size_t ertd_encoder_train_ws_bytes(int B, int L);
+int ertd_encoder_train_fwd(const float* packed, const float* b1, const float* b2, const float* cond,
+                           int B, int L, float* m_out, void* ws, size_t ws_bytes, void* stream);
+int ertd_encoder_train_bwd(const float* packed, const float* cond, const float* g, int B, int L,
+                           float* dw1, float* db1, float* dw2, float* db2, void* ws,
+                           size_t ws_bytes, void* stream);
+int ertd_adam_multi(float* const* params, const float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, const long long* sizes, int ntensors, int step,
+                    float lr, float beta1, float beta2, float eps, void* stream);
+
 /* ---- Ensemble KDE mode (csrc/kde.hip) -------------
  * Replaces the reference's per-cell loop ERT_Conditional_Diffusion.py:747-762
  * (scipy.stats.gaussian_kde per cell of sim_data, evaluated on

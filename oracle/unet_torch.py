@@ -180,7 +180,9 @@ def condition_embedding(cond, W):
 
 
 def embedding(t, cond, W, cfg: UNetConfig):
-    e = F.linear(sinusoid(t, cfg.ch), W["time_embed.0.weight"], W["time_embed.0.bias"])
+    # the sinusoid is fp32 (the reference's); a float64 weight dict runs the rest in float64
+    s = sinusoid(t, cfg.ch).to(W["time_embed.0.weight"].dtype)
+    e = F.linear(s, W["time_embed.0.weight"], W["time_embed.0.bias"])
     e = F.linear(F.silu(e), W["time_embed.2.weight"], W["time_embed.2.bias"])
     return e + F.linear(condition_embedding(cond, W), W["cond_proj.weight"], W["cond_proj.bias"])
 
