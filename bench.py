@@ -91,6 +91,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hoisted", action="store_true", help="skip the secondary hoisted timing")
     ap.add_argument("--no-train", action="store_true", help="skip the secondary train-step timing")
+    ap.add_argument("--no-unet-train", action="store_true", help="skip the U-Net train-step timing")
+    ap.add_argument("--unet-train-steps", type=int, default=5)
     ap.add_argument("--no-strip-roofline", action="store_true")
     ap.add_argument("--no-steps-schedule", action="store_true",
                     help="skip the secondary per-step-schedule timing")
@@ -271,6 +273,35 @@ def train_bench(dev, steps=200, B=32, T=500):
     el = time.perf_counter() - t0
     return {"train_steps_per_s": round(steps / el, 1), "train_batch": B,
             "train_ms_per_step": round(el / steps * 1e3, 4), "train_final_loss": round(float(loss), 5)}
+
+
+def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000):
+    """The reference train step (:309-320) on the U-Net denoiser: q_sample, the
+    HIP forward with saved activations, the hand-written HIP backward, MSE and
+    the multi-tensor Adam kernel (ertdiff.unet_train_step), fp32, batch B."""
+    from ertdiff.unet_train import unet_train_step
+    model = ertdiff.ConditionalUNet.from_config(name, seed=0).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    g = torch.Generator(device=dev).manual_seed(11)
+    P_ = model.param_dim
+    x0 = torch.randn(B, P_, device=dev, generator=g)
+    cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=dev)
+    ts = torch.randint(0, T, (steps + warmup, B), device=dev, generator=g)
+    ns = torch.randn(steps + warmup, B, P_, device=dev, generator=g)
+    for i in range(warmup):
+        unet_train_step(model, opt, x0, cond, T, ab, t=ts[i], noise=ns[i], return_tensor=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = unet_train_step(model, opt, x0, cond, T, ab, t=ts[warmup + i], noise=ns[warmup + i],
+                               return_tensor=True)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    return {"unet_train_steps_per_s": round(steps / el, 3), "model": name, "batch": B,
+            "ms_per_step": round(el / steps * 1e3, 2), "steps": steps, "warmup": warmup,
+            "final_loss": round(float(loss), 5), "dtype": "f32",
+            "note": "one process, wall clock around the steps (host walk + HIP kernels)"}
 
 
 def _host_cpus():
@@ -642,6 +673,8 @@ def main():
                                                     world, dev)
     if not a.no_u5:
         extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev)
+    if not a.no_unet_train and world == 1:
+        extra["unet_train"] = bench_unet_train(dev, steps=a.unet_train_steps)
     if not a.no_kde:
         extra["kde_mode"] = bench_kde(dev, world, rank, cpu=not a.no_cpu_baseline)
     if not a.no_reference:

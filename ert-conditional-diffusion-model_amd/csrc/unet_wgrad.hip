@@ -1,0 +1,306 @@
+// Convolution weight gradient of the U-Net train step as an implicit GEMM on
+// fp32 MFMA (SURVEY.md 8a' trainer; checked against torch autograd on
+// oracle/unet_torch.py by tests/test_gpu_unet_train.py).
+//
+//   dW[co][ci][tap] = sum_{b, output pixel p} dY[b][co][p] * Xv[b][ci][p + off(tap)]
+//
+// Xv is the conv's (virtual) input: X itself (stride 1), the nearest-x2
+// upsampled X (mode UP, never materialized), or X read at stride 2 (mode S2).
+// GEMM view: M = Cout, N = Cin * taps, K = B * Ho * Wo (huge).  A workgroup
+// owns a 64 (co) x 32 (ci) x taps output tile and a contiguous range of
+// K-chunks (128 output pixels of one sample each); the per-range partials are
+// summed in a fixed order by reduce_rows (bitwise reproducible, no atomics).
+//
+// Per chunk, dY (64 x 128) and the input rows the chunk's taps touch (32 ci x
+// (R + 2) rows, zero halo; S2: even / odd columns de-interleaved) are staged
+// in LDS.  The K order inside an MFMA is permuted so that lane group g feeds
+// pixels 4g .. 4g+3 of a 16-pixel group over 4 consecutive MFMAs: every
+// operand fetch is one ds_read_b128 (+ one b32 for a tap's left / right
+// neighbour), and the 3 taps of a kernel row share one fetch.  Wave tile:
+// 32 co x 16 ci x taps (2 x taps v_mfma_f32_16x16x4_f32 accumulators).
+#include "unet.h"
+
+using namespace ertd;
+using namespace ertd::unet;
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int TCO = 64, TCI = 32, PXC = 128, DYS = PXC + 4;
+
+struct WgArgs {
+  const float* dy;
+  const float* xa;
+  const float* xb;
+  int Ca, Cb, Cout, H, Ho, R;
+  int ntiles, nco, nsplit, cps, nchunks;
+  float* part;   // (nsplit, Cout, Cin * KK)
+};
+
+__host__ __device__ constexpr int round_cis(int n) { return n + ((4 - n) % 64 + 64) % 64; }
+
+// LDS geometry per mode: rows of the staged input, row width, per-channel stride
+struct Geo {
+  int nr, roww, cis;
+};
+__host__ __device__ inline Geo geo(int mode, int ks, int Ho) {
+  const int R = PXC / Ho;
+  Geo g{};
+  if (ks == 1) {
+    g.nr = R; g.roww = Ho; g.cis = PXC + 4;
+  } else if (mode == MODE_S2) {
+    g.nr = 2 * R + 1; g.roww = 2 * Ho + 8; g.cis = round_cis(g.nr * g.roww);
+  } else {
+    g.nr = R + 2; g.roww = Ho + 8; g.cis = round_cis(g.nr * g.roww);
+  }
+  return g;
+}
+
+__device__ __forceinline__ const float* chan_ptr(const WgArgs& a, int b, int ci) {
+  const size_t hw = (size_t)a.H * a.H;
+  return ci < a.Ca ? a.xa + ((size_t)b * a.Ca + ci) * hw : a.xb + ((size_t)b * a.Cb + ci - a.Ca) * hw;
+}
+
+template <int MODE, int KS>
+__global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int KK = KS * KS;
+  const int Ho = a.Ho, R = a.R, Cin = a.Ca + a.Cb;
+  const Geo G = geo(MODE, KS, Ho);
+  float* dyL = smem;
+  float* xL = smem + TCO * DYS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.x % a.ntiles, split = blockIdx.x / a.ntiles;
+  const int co0 = (tile % a.nco) * TCO, ci0 = (tile / a.nco) * TCI;
+  const int cb0 = 2 * (w & 1), cib = w >> 1;
+  // zero the staged input once: halo columns are never written by the loads
+  for (int i = tid; i < TCI * G.cis; i += 256) xL[i] = 0.f;
+
+  f32x4 acc[2][KK];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < KK; ++t) acc[i][t] = f32x4{};
+
+  const int rows_per_b = Ho / R;
+  const int c_lo = split * a.cps, c_hi = min(a.nchunks, c_lo + a.cps);
+  for (int c = c_lo; c < c_hi; ++c) {
+    const int b = c / rows_per_b, y0 = (c - b * rows_per_b) * R;
+    __syncthreads();
+    // ---- stage dY (64 co x 128 pixels): rows y0 .. y0+R-1 are contiguous
+    for (int i = tid; i < TCO * PXC / 4; i += 256) {
+      const int r = i / (PXC / 4), c4 = i - r * (PXC / 4);
+      const int co = co0 + r;
+      f32x4 v = f32x4{};
+      if (co < a.Cout)
+        v = *(const f32x4*)(a.dy + ((size_t)b * a.Cout + co) * Ho * Ho + (size_t)y0 * Ho + 4 * c4);
+      *(f32x4*)(dyL + r * DYS + 4 * c4) = v;
+    }
+    // ---- stage the input rows
+    if constexpr (KS == 1) {
+      for (int i = tid; i < TCI * PXC / 4; i += 256) {
+        const int r = i / (PXC / 4), c4 = i - r * (PXC / 4);
+        const int ci = ci0 + r;
+        f32x4 v = f32x4{};
+        if (ci < Cin) v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)y0 * Ho + 4 * c4);
+        *(f32x4*)(xL + r * G.cis + 4 * c4) = v;
+      }
+    } else if constexpr (MODE == MODE_S2) {
+      // input rows 2 y0 - 1 .. 2 (y0 + R - 1) + 1, width H = 2 Ho; E at col 4, O at col Ho + 8
+      const int W = a.H, q = W / 4;
+      for (int i = tid; i < TCI * G.nr * q; i += 256) {
+        const int r = i / q, c4 = i - r * q;
+        const int cl = r / G.nr, rr = r - cl * G.nr;
+        const int ci = ci0 + cl, iy = 2 * y0 - 1 + rr;
+        f32x4 v = f32x4{};
+        if (ci < Cin && iy >= 0 && iy < W) v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)iy * W + 4 * c4);
+        float* row = xL + cl * G.cis + rr * G.roww;
+        *(float2*)(row + 4 + 2 * c4) = float2{v.x, v.z};
+        *(float2*)(row + Ho + 8 + 2 * c4) = float2{v.y, v.w};
+      }
+    } else {
+      // virtual input rows y0 - 1 .. y0 + R (UP: source row / col halved)
+      const int q = Ho / 4;
+      for (int i = tid; i < TCI * G.nr * q; i += 256) {
+        const int r = i / q, c4 = i - r * q;
+        const int cl = r / G.nr, rr = r - cl * G.nr;
+        const int ci = ci0 + cl, vy = y0 - 1 + rr;
+        f32x4 v = f32x4{};
+        if (ci < Cin && vy >= 0 && vy < Ho) {
+          if constexpr (MODE == MODE_UP) {
+            const float2 s = *(const float2*)(chan_ptr(a, b, ci) + (size_t)(vy >> 1) * a.H + 2 * c4);
+            v = f32x4{s.x, s.x, s.y, s.y};
+          } else {
+            v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)vy * Ho + 4 * c4);
+          }
+        }
+        *(f32x4*)(xL + cl * G.cis + rr * G.roww + 4 + 4 * c4) = v;
+      }
+    }
+    __syncthreads();
+    // ---- MFMAs over the chunk's 128 pixels, 16 at a time
+    const float* xw = xL + (cib * 16 + l16) * G.cis;
+    const float* a0p = dyL + ((cb0 + 0) * 16 + l16) * DYS + 4 * g;
+    const float* a1p = dyL + ((cb0 + 1) * 16 + l16) * DYS + 4 * g;
+    for (int p16 = 0; p16 < PXC; p16 += 16) {
+      const f32x4 A0 = *(const f32x4*)(a0p + p16);
+      const f32x4 A1 = *(const f32x4*)(a1p + p16);
+      if constexpr (KS == 1) {
+        const f32x4 Bv = *(const f32x4*)(xw + p16 + 4 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[s], Bv[s], acc[0][0], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[s], Bv[s], acc[1][0], 0, 0, 0);
+        }
+      } else {
+        const int yl = p16 / Ho, x0 = p16 - yl * Ho + 4 * g;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          f32x4 B0, B1, B2;
+          if constexpr (MODE == MODE_S2) {
+            const float* row = xw + (2 * yl + ky) * G.roww;
+            const f32x4 E = *(const f32x4*)(row + 4 + x0);
+            const f32x4 O = *(const f32x4*)(row + Ho + 8 + x0);
+            const float ol = row[Ho + 7 + x0];
+            B0 = f32x4{ol, O.x, O.y, O.z};
+            B1 = E;
+            B2 = O;
+          } else {
+            const float* row = xw + (yl + ky) * G.roww + 4 + x0;
+            const f32x4 C = *(const f32x4*)row;
+            const float lf = row[-1], rt = row[4];
+            B0 = f32x4{lf, C.x, C.y, C.z};
+            B1 = C;
+            B2 = f32x4{C.y, C.z, C.w, rt};
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            acc[0][3 * ky + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[s], B0[s], acc[0][3 * ky + 0], 0, 0, 0);
+            acc[1][3 * ky + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[s], B0[s], acc[1][3 * ky + 0], 0, 0, 0);
+            acc[0][3 * ky + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[s], B1[s], acc[0][3 * ky + 1], 0, 0, 0);
+            acc[1][3 * ky + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[s], B1[s], acc[1][3 * ky + 1], 0, 0, 0);
+            acc[0][3 * ky + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[s], B2[s], acc[0][3 * ky + 2], 0, 0, 0);
+            acc[1][3 * ky + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[s], B2[s], acc[1][3 * ky + 2], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  // ---- partial tile out: D row 4 (lane / 16) + r of the 16-row block, column lane % 16
+  const size_t ncol = (size_t)Cin * KK;
+  const int ci = ci0 + cib * 16 + l16;
+  if (ci >= Cin) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + (cb0 + i) * 16 + 4 * g + r;
+      if (co >= a.Cout) continue;
+      float* dst = a.part + ((size_t)split * a.Cout + co) * ncol + (size_t)ci * KK;
+#pragma unroll
+      for (int t = 0; t < KK; ++t) dst[t] = acc[i][t][r];
+    }
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int rows, size_t cols,
+                                    float* __restrict__ out, int accumulate) {
+  const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += part[(size_t)r * cols + j];
+  out[j] = accumulate ? out[j] + s : s;
+}
+
+int n_cu() {
+  static int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    return n;
+  }();
+  return v;
+}
+
+struct Plan {
+  int Ho, R, nco, nci, ntiles, nchunks, cps, nsplit;
+  size_t lds, part_floats;
+};
+
+bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
+  if (Cin < 1 || Cout < 1 || B < 1 || H < 1 || (ks != 1 && ks != 3) || mode < MODE_S1 ||
+      mode > MODE_UP || (ks == 1 && mode != MODE_S1))
+    return false;
+  const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  if (Ho > PXC || PXC % Ho || (mode == MODE_S2 && H != 2 * Ho)) return false;
+  if (ks == 3 && Ho < 16) return false;    // a 16-pixel group stays inside one row
+  if (ks == 1 && Ho * Ho < 16) return false;
+  const Geo G = geo(mode, ks, Ho);
+  p->Ho = Ho;
+  p->R = PXC / Ho;
+  p->nco = (Cout + TCO - 1) / TCO;
+  p->nci = (Cin + TCI - 1) / TCI;
+  p->ntiles = p->nco * p->nci;
+  p->nchunks = B * (Ho / p->R);
+  if (ks == 1 && Ho * Ho < PXC) return false;
+  // >= 4 chunks per range (keeps the partial traffic well below the operand
+  // traffic), about 4 workgroups per CU
+  const int want = (4 * n_cu() + p->ntiles - 1) / p->ntiles;
+  int cps = (p->nchunks + want - 1) / want;
+  if (cps < 4) cps = 4;
+  if (cps > p->nchunks) cps = p->nchunks;
+  p->cps = cps;
+  p->nsplit = (p->nchunks + cps - 1) / cps;
+  p->lds = ((size_t)TCO * DYS + (size_t)TCI * G.cis) * sizeof(float);
+  p->part_floats = (size_t)p->nsplit * Cout * Cin * ks * ks;
+  return true;
+}
+
+template <int MODE, int KS>
+hipError_t launch_t(const WgArgs& a, size_t lds, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)wgrad_conv_kernel<MODE, KS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  wgrad_conv_kernel<MODE, KS><<<(unsigned)(a.ntiles * a.nsplit), 256, lds, s>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mode) {
+  Plan p;
+  if (!plan_of(Cin, Cout, B, H, ks, mode, &p)) return 0;
+  return p.part_floats * sizeof(float);
+}
+
+int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
+                    int Cout, int ks, int mode, float* dw, int accumulate, void* ws,
+                    size_t ws_bytes, void* stream) {
+  if (!dy || !x || !dw || !ws || Ca < 1 || Cb < 0 || (Cb > 0 && !x2)) return ERTD_EINVAL;
+  Plan p;
+  if (!plan_of(Ca + Cb, Cout, B, H, ks, mode, &p)) return ERTD_EINVAL;
+  if (p.part_floats * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+  WgArgs a{dy, x, x2, Ca, Cb, Cout, H, p.Ho, p.R, p.ntiles, p.nco, p.nsplit, p.cps, p.nchunks,
+           (float*)ws};
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (ks == 1) e = launch_t<MODE_S1, 1>(a, p.lds, s);
+  else if (mode == MODE_S2) e = launch_t<MODE_S2, 3>(a, p.lds, s);
+  else if (mode == MODE_UP) e = launch_t<MODE_UP, 3>(a, p.lds, s);
+  else e = launch_t<MODE_S1, 3>(a, p.lds, s);
+  if (e != hipSuccess) return (int)e;
+  const size_t cols = (size_t)Cout * (Ca + Cb) * ks * ks;
+  wgrad_reduce_kernel<<<(unsigned)((cols + 255) / 256), 256, 0, s>>>((const float*)ws, p.nsplit, cols,
+                                                                    dw, accumulate);
+  e = hipGetLastError();
+  return e == hipSuccess ? ERTD_OK : (int)e;
+}
+
+}  // extern "C"

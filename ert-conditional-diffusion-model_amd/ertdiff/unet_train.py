@@ -118,6 +118,21 @@ class _K:
                                             out.data_ptr(), int(accumulate), ws.data_ptr(), n,
                                             _s(self.dev)), "wgrad_gemm")
 
+    def conv_wgrad(self, dy, xa, xb, ks, mode, out):
+        """out (Cout, Cin, ks, ks) = dL/dW of conv(cat(xa, xb)) on the implicit-GEMM
+        kernel; False when the geometry is outside it (caller falls back)."""
+        B, Ca, H, _ = xa.shape
+        Cb = 0 if xb is None else xb.shape[1]
+        Cout = dy.shape[1]
+        n = self.lib.ertd_conv_wgrad_ws_bytes(Ca + Cb, Cout, B, H, ks, mode)
+        if n == 0:
+            return False
+        ws = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        _lib.check(self.lib.ertd_conv_wgrad(dy.data_ptr(), xa.data_ptr(), Ca, _p(xb), Cb, B, H, Cout,
+                                            ks, mode, out.data_ptr(), 0, ws.data_ptr(), n,
+                                            _s(self.dev)), "conv_wgrad")
+        return True
+
     def flip(self, w):
         Cout, Cin, ks, _ = w.shape
         out = self.empty(Cin, Cout, ks, ks)
@@ -212,25 +227,22 @@ class _Grads:
         return self.g.get(id(t))
 
 
-def _conv_backward(k: _K, G: _Grads, grads, name, w, xa, xb, dy, mode, x_needs_grad=True,
-                   act_input=None):
+def _conv_backward(k: _K, G: _Grads, grads, name, w, xa, xb, dy, mode, x_needs_grad=True):
     """Gradients of y = conv(cat(xa, xb)) (+ bias): weight and bias grads into
-    grads[name.weight/.bias]; dx accumulated into G (xa / xb).  act_input: the
-    tensor the conv actually read (materialized activation) when given."""
+    grads[name.weight/.bias]; returns dL/d cat(xa, xb) (or None)."""
     Cout, Cin, ks, _ = w.shape
-    x_conv = act_input
-    if x_conv is None:
-        if xb is None:
-            x_conv = xa
-        else:   # materialize the concatenation for the patch matrix
+    # weight / bias
+    dW = k.empty(Cout, Cin * ks * ks)
+    if not k.conv_wgrad(dy, xa, xb, ks, mode, dW):
+        # outside the implicit-GEMM kernel's geometry: patch matrix + GEMM
+        x_conv = xa
+        if xb is not None:
             B, Ca, H, W = xa.shape
             x_conv = k.empty(B, Cin, H, W)
             k.chan_copy(xa, 0, Ca, x_conv, 0)
             k.chan_copy(xb, 0, xb.shape[1], x_conv, Ca)
-    # weight / bias
-    dW = k.empty(Cout, Cin * ks * ks)
-    col = x_conv if ks == 1 else k.im2col(x_conv, ks, mode)
-    k.wgrad(dy, col.view(col.shape[0], col.shape[1], -1), dW)
+        col = x_conv if ks == 1 else k.im2col(x_conv, ks, mode)
+        k.wgrad(dy, col.view(col.shape[0], col.shape[1], -1), dW)
     grads[name + ".weight"] = dW.view(Cout, Cin, ks, ks)
     db = k.empty(Cout)
     k.chan_sums(dy, db)

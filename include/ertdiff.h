@@ -375,6 +375,15 @@ int ertd_channel_slice(const float* src, int B, int Cs, int c0, int Cd, int HW, 
                        int Cdst, int d0, int accumulate, void* stream);
 int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss, float* dout,
                   void* stream);
+/* ertd_conv_wgrad: dW (Cout, Ca+Cb, ks, ks) (+)= the weight gradient of
+ *   y = conv(cat(x, x2)) (mode 0 stride 1 / 1 stride 2 / 2 nearest-x2 upsample,
+ *   as ertd_conv2d) given dy (B, Cout, Ho, Ho): implicit GEMM on fp32 MFMA,
+ *   fixed-order split reduction; ws >= ertd_conv_wgrad_ws_bytes (0 = unsupported
+ *   geometry: output side not a power of two in [16, 128]).  csrc/unet_wgrad.hip. */
+size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mode);
+int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
+                    int Cout, int ks, int mode, float* dw, int accumulate, void* ws,
+                    size_t ws_bytes, void* stream);
 size_t ertd_encoder_train_ws_bytes(int B, int L);
 int ertd_encoder_train_fwd(const float* packed, const float* b1, const float* b2, const float* cond,
                            int B, int L, float* m_out, void* ws, size_t ws_bytes, void* stream);

@@ -127,3 +127,54 @@ def test_unet_train_rejects_bf16(cuda_dev):
     cond = torch.zeros(2, 14, 33, device=cuda_dev)
     with pytest.raises(RuntimeError, match="fp32"):
         unet_train_step(m, opt, x0, cond, 1000, ab)
+
+
+@pytest.mark.parametrize("Ca,Cb,Cout,H,ks,mode,B", [
+    (64, 0, 64, 64, 3, 0, 3),      # ResBlock conv, 64x64
+    (128, 64, 64, 32, 3, 0, 2),    # concat input, Cout < Cin
+    (256, 0, 256, 16, 3, 0, 2),
+    (1, 0, 32, 32, 3, 0, 2),       # conv_in: Cin = 1 (masked ci tile)
+    (32, 0, 1, 32, 3, 0, 2),       # conv_out: Cout = 1 (masked co tile)
+    (48, 0, 40, 128, 3, 0, 1),     # ragged channel tiles, 128x128 rows
+    (64, 0, 64, 64, 3, 1, 2),      # Downsample (stride 2): 64 -> 32
+    (128, 0, 128, 32, 3, 1, 2),    # 32 -> 16
+    (128, 0, 128, 16, 3, 2, 2),    # Upsample 16 -> 32
+    (64, 0, 64, 64, 3, 2, 1),      # Upsample 64 -> 128
+    (96, 32, 64, 32, 1, 0, 2),     # 1x1 skip on a concat
+    (256, 0, 768, 16, 1, 0, 2),    # attention qkv
+])
+def test_conv_wgrad_vs_autograd(Ca, Cb, Cout, H, ks, mode, B, cuda_dev):
+    from ertdiff import _lib
+    g = torch.Generator().manual_seed(Ca * 7 + Cout + H + mode)
+    Cin = Ca + Cb
+    x = torch.randn(B, Cin, H, H, generator=g)
+    Ho = H // 2 if mode == 1 else (2 * H if mode == 2 else H)
+    dy = torch.randn(B, Cout, Ho, Ho, generator=g)
+    xin = F.interpolate(x.double(), scale_factor=2, mode="nearest") if mode == 2 else x.double()
+    ref = torch.nn.grad.conv2d_weight(xin, (Cout, Cin, ks, ks), dy.double(),
+                                      stride=2 if mode == 1 else 1, padding=ks // 2)
+    lib = _lib.lib()
+    n = lib.ertd_conv_wgrad_ws_bytes(Cin, Cout, B, H, ks, mode)
+    assert n > 0
+    ws = torch.empty(n, dtype=torch.uint8, device=cuda_dev)
+    xa = x[:, :Ca].contiguous().to(cuda_dev)
+    xb = x[:, Ca:].contiguous().to(cuda_dev) if Cb else None
+    dyd = dy.to(cuda_dev)
+    out = torch.full((Cout, Cin, ks, ks), 0.5, device=cuda_dev)
+    for acc in (0, 1):
+        rc = lib.ertd_conv_wgrad(dyd.data_ptr(), xa.data_ptr(), Ca,
+                                 None if xb is None else xb.data_ptr(), Cb, B, H, Cout, ks, mode,
+                                 out.data_ptr(), acc, ws.data_ptr(), n, _lib.stream_of(cuda_dev))
+        assert rc == 0
+    err = _rel(out, 2 * ref)                    # written, then accumulated once more
+    record_error(f"conv_wgrad_{Cin}_{Cout}_{H}_k{ks}_m{mode}", err)
+    assert err < 1e-5, err
+
+
+def test_conv_wgrad_rejects_bad_geometry(cuda_dev):
+    from ertdiff import _lib
+    lib = _lib.lib()
+    assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 8, 3, 0) == 0       # 8x8 rows: outside
+    assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 48, 3, 0) == 0      # not a power of two
+    assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 32, 1, 1) == 0      # 1x1 stride 2
+    assert lib.ertd_conv_wgrad(None, None, 1, None, 0, 1, 16, 1, 3, 0, None, 0, None, 0, None) != 0
