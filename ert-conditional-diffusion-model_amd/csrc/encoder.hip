@@ -109,6 +109,17 @@ __global__ __launch_bounds__(256) void pack_w2b_kernel(ertd_weights w, float* __
   packed[PACK_W2B + idx] = w.enc2_w[(o * C1 + c) * 3 + kk];
 }
 
+// only the encoder conv regions (fp32 + bf16 fragments, W2B): what the encoder's
+// train-mode forward / backward read (the U-Net train step's condition encoder)
+hipError_t launch_pack_encoder_convs(const float* w0, const float* w2, float* packed, hipStream_t s) {
+  ertd_weights w{};
+  w.enc0_w = w0;
+  w.enc2_w = w2;
+  pack_kernel<<<(PACK_TOTAL + 255) / 256, 256, 0, s>>>(w, packed);
+  pack_w2b_kernel<<<W2B_FLOATS / 256, 256, 0, s>>>(w, packed);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s) {
   pack_kernel<<<(PACK_TOTAL + 255) / 256, 256, 0, s>>>(w, packed);
   const int n = C2 * H + H * H + (w.param_dim + 2 * H) * H;

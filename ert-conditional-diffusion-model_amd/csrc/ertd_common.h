@@ -166,6 +166,7 @@ constexpr int W2L_FLOATS = 64 * W2L_PITCH;
 constexpr int PACKED_FLOATS_ALL = PACK_W2L + W2L_FLOATS;
 
 hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s);
+hipError_t launch_pack_encoder_convs(const float* w0, const float* w2, float* packed, hipStream_t s);
 hipError_t launch_encoder_train(const float* packed, const float* b1, const float* b2,
                                 const float* cond, int B, int L, float* partial, float* a1,
                                 unsigned char* m2, hipStream_t s);

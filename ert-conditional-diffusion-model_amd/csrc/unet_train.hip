@@ -102,8 +102,8 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
     sg = wg_sum(sg, red, tid);
     sb = wg_sum(sb, red, tid);
     if (tid == 0) {
-      dgb[(size_t)b * C + c] = (float)sg;                        // plane 0: dgamma partial
-      dgb[(size_t)(gridDim.y + b) * C + c] = (float)sb;         // plane 1: dbeta partial
+      dgb[(size_t)(2 * b) * C + c] = (float)sg;        // [b][0][c]: dgamma partial
+      dgb[(size_t)(2 * b + 1) * C + c] = (float)sb;    // [b][1][c]: dbeta partial
     }
     A += (double)ga * sb;     // sum dxhat
     Bs += (double)ga * sg;    // sum dxhat xhat
@@ -194,13 +194,29 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
   }
 }
 
-__global__ void reduce_rows_kernel(const float* __restrict__ part, int rows, size_t cols,
-                                   float* __restrict__ out, int accumulate) {
-  const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= cols) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += part[(size_t)r * cols + j];
-  out[j] = accumulate ? out[j] + s : s;
+// out[j] (+)= sum_r part[r][j]: 64 columns x 4 row-interleaved partial sums
+// per workgroup (loads in flight), combined in a fixed order (reproducible)
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int rows,
+                                                          size_t cols, float* __restrict__ out,
+                                                          int accumulate) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const size_t j = (size_t)blockIdx.x * 64 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (j < cols) {
+    int r = ty;
+    for (; r + 4 < rows; r += 8) {
+      s0 += part[(size_t)r * cols + j];
+      s1 += part[(size_t)(r + 4) * cols + j];
+    }
+    if (r < rows) s0 += part[(size_t)r * cols + j];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && j < cols) {
+    const float s = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    out[j] = accumulate ? out[j] + s : s;
+  }
 }
 
 __global__ void weight_flip_kernel(const float* __restrict__ w, int Cout, int Cin, int ks,
@@ -239,15 +255,15 @@ __global__ void sum_pool2_kernel(const float* __restrict__ x, int H, size_t n, f
 }
 
 // per (sample, channel) sum over HW (one workgroup each, fixed order)
-__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ x, int HW,
-                                                       float* __restrict__ out) {
+__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ x, int HW, int C,
+                                                       int ldo, float* __restrict__ out) {
   __shared__ double red[4];
   const size_t bc = blockIdx.x;
   const float* s = x + bc * HW;
   double acc = 0.0;
   for (int p = threadIdx.x; p < HW; p += 256) acc += (double)s[p];
   acc = wg_sum(acc, red, threadIdx.x);
-  if (threadIdx.x == 0) out[bc] = (float)acc;
+  if (threadIdx.x == 0) out[(bc / C) * ldo + bc % C] = (float)acc;
 }
 
 // ---- small strided batched GEMM (fp32 FMA, 32x32 tile per workgroup)
@@ -373,18 +389,28 @@ __global__ void chan_slice_kernel(const float* __restrict__ src, int Cs, int c0,
   *d = accumulate ? *d + v : v;
 }
 
-// MSELoss(mean): loss = sum (e - z)^2 / n (fixed order: one workgroup), dout = 2 (e - z) / n
-__global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ e, const float* __restrict__ z,
-                                                  size_t n, float* __restrict__ loss,
-                                                  float* __restrict__ dout) {
+// MSELoss(mean): per-workgroup double partial sums of (e - z)^2 (fixed
+// ranges), then one workgroup adds them in order; dout = 2 (e - z) / n
+constexpr int MSE_WG = 256;
+__global__ __launch_bounds__(256) void mse_part_kernel(const float* __restrict__ e, const float* __restrict__ z,
+                                                       size_t n, size_t per, double* __restrict__ part,
+                                                       float* __restrict__ dout) {
   __shared__ double red[4];
   double acc = 0.0;
   const float two_n = (float)(2.0 / (double)n);
-  for (size_t i = threadIdx.x; i < n; i += 256) {
+  const size_t lo = (size_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  for (size_t i = lo + threadIdx.x; i < hi; i += 256) {
     const float d = e[i] - z[i];
     acc += (double)d * d;
     if (dout) dout[i] = two_n * d;
   }
+  acc = wg_sum(acc, red, threadIdx.x);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+__global__ __launch_bounds__(256) void mse_final_kernel(const double* __restrict__ part, int np, size_t n,
+                                                        float* __restrict__ loss) {
+  __shared__ double red[4];
+  double acc = threadIdx.x < np ? part[threadIdx.x] : 0.0;
   acc = wg_sum(acc, red, threadIdx.x);
   if (threadIdx.x == 0) *loss = (float)(acc / (double)n);
 }
@@ -426,6 +452,21 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
   a.p[k][e] = a.p[k][e] + a.step_size_neg * (m / denom);
   a.m[k][e] = m;
   a.v[k][e] = v;
+}
+
+// dst = cat(src[0], src[1], ...) over up to 64 contiguous tensors per launch
+constexpr int CAT_T = 64;
+struct CatMulti {
+  const float* src[CAT_T];
+  long long off[CAT_T + 1];
+  int nt;
+};
+__global__ __launch_bounds__(256) void concat_kernel(CatMulti c, float* __restrict__ dst) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= c.off[c.nt]) return;
+  int k = 0;
+  while (k + 1 < c.nt && i >= c.off[k + 1]) ++k;
+  dst[i] = c.src[k][i - c.off[k]];
 }
 
 inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
@@ -497,15 +538,16 @@ int ertd_wgrad_gemm(const float* dY, const float* X, int M, int N, int P, int B,
   wgrad_kernel<<<dim3((N + 63) / 64, (M + 63) / 64, B * nsp), 256, 0, s>>>(
       dY, X, M, N, P, (size_t)bsA, (size_t)bsB, (float*)ws, split_len, nsp);
   const size_t cols = (size_t)M * N;
-  reduce_rows_kernel<<<nblk(cols), 256, 0, s>>>((const float*)ws, B * nsp, cols, dW, accumulate);
+  reduce_rows_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>((const float*)ws, B * nsp, cols, dW,
+                                                                   accumulate);
   return rcode(hipGetLastError());
 }
 
 int ertd_reduce_rows(const float* part, int rows, long long cols, float* out, int accumulate,
                      void* stream) {
   if (!part || !out || rows < 1 || cols < 1) return ERTD_EINVAL;
-  reduce_rows_kernel<<<nblk((size_t)cols), 256, 0, (hipStream_t)stream>>>(part, rows, (size_t)cols,
-                                                                         out, accumulate);
+  reduce_rows_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, (hipStream_t)stream>>>(part, rows, (size_t)cols,
+                                                                                   out, accumulate);
   return rcode(hipGetLastError());
 }
 
@@ -530,12 +572,14 @@ int ertd_sum_pool2(const float* x, int B, int C, int H, float* out, int accumula
   return rcode(hipGetLastError());
 }
 
-int ertd_channel_sums(const float* x, int B, int C, int HW, float* out_bc, float* out_c,
+int ertd_channel_sums(const float* x, int B, int C, int HW, float* out_bc, int ldo, float* out_c,
                       int accumulate_c, void* stream) {
-  if (!x || !out_bc || B < 1 || C < 1 || HW < 1) return ERTD_EINVAL;
+  if (ldo == 0) ldo = C;
+  if (!x || !out_bc || B < 1 || C < 1 || HW < 1 || ldo < C || (out_c && ldo != C)) return ERTD_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  chan_sum_kernel<<<(unsigned)((size_t)B * C), 256, 0, s>>>(x, HW, out_bc);
-  if (out_c) reduce_rows_kernel<<<nblk((size_t)C), 256, 0, s>>>(out_bc, B, (size_t)C, out_c, accumulate_c);
+  chan_sum_kernel<<<(unsigned)((size_t)B * C), 256, 0, s>>>(x, HW, C, ldo, out_bc);
+  if (out_c)
+    reduce_rows_kernel<<<(unsigned)((C + 63) / 64), 256, 0, s>>>(out_bc, B, (size_t)C, out_c, accumulate_c);
   return rcode(hipGetLastError());
 }
 
@@ -586,8 +630,17 @@ int ertd_channel_slice(const float* src, int B, int Cs, int c0, int Cd, int HW, 
 int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss, float* dout,
                   void* stream) {
   if (!eps || !noise || !loss || n < 1) return ERTD_EINVAL;
-  mse_kernel<<<1, 256, 0, (hipStream_t)stream>>>(eps, noise, (size_t)n, loss, dout);
-  return rcode(hipGetLastError());
+  hipStream_t s = (hipStream_t)stream;
+  const size_t per = (((size_t)n + MSE_WG - 1) / MSE_WG + 255) / 256 * 256;
+  const int np = (int)(((size_t)n + per - 1) / per);
+  double* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, MSE_WG * sizeof(double), s);
+  if (e != hipSuccess) return (int)e;
+  mse_part_kernel<<<np, 256, 0, s>>>(eps, noise, (size_t)n, per, part, dout);
+  mse_final_kernel<<<1, 256, 0, s>>>(part, np, (size_t)n, loss);
+  e = hipGetLastError();
+  hipFreeAsync(part, s);
+  return rcode(e);
 }
 
 // the reference condition encoder with saved activations: partial (B,S,64),
@@ -609,6 +662,11 @@ static void enc_layout(int B, int L, float* ws, float** partial, float** a1, uns
   *a1 = ws + o; o += ((size_t)B * C1 * L1 + 63) / 64 * 64;
   *m2 = (unsigned char*)(ws + o); o += (((size_t)B * C2 * L2 + 3) / 4 + 63) / 64 * 64;
   *bw = ws + o;
+}
+
+int ertd_encoder_train_pack(const float* w0, const float* w2, float* packed, void* stream) {
+  if (!w0 || !w2 || !packed) return ERTD_EINVAL;
+  return rcode(launch_pack_encoder_convs(w0, w2, packed, (hipStream_t)stream));
 }
 
 int ertd_encoder_train_fwd(const float* packed, const float* b1, const float* b2, const float* cond,
@@ -638,6 +696,29 @@ int ertd_encoder_train_bwd(const float* packed, const float* cond, const float* 
   enc_layout(B, L, (float*)ws, &partial, &a1, &m2, &bw);
   return rcode(launch_encoder_conv_backward(packed, cond, a1, m2, g, B, L, bw, dw1, db1, dw2, db2,
                                             (hipStream_t)stream));
+}
+
+int ertd_concat(const float* const* srcs, const long long* sizes, int n, float* dst, void* stream) {
+  if (!srcs || !sizes || !dst || n < 1) return ERTD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  long long base = 0;
+  for (int t0 = 0; t0 < n; t0 += CAT_T) {
+    CatMulti c{};
+    c.nt = n - t0 < CAT_T ? n - t0 : CAT_T;
+    long long off = 0;
+    for (int k = 0; k < c.nt; ++k) {
+      if (!srcs[t0 + k] || sizes[t0 + k] < 0) return ERTD_EINVAL;
+      c.src[k] = srcs[t0 + k];
+      c.off[k] = off;
+      off += sizes[t0 + k];
+    }
+    c.off[c.nt] = off;
+    if (off > 0) concat_kernel<<<nblk((size_t)off), 256, 0, s>>>(c, dst + base);
+    base += off;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return ERTD_OK;
 }
 
 int ertd_adam_multi(float* const* params, const float* const* grads, float* const* exp_avg,

@@ -18,6 +18,8 @@
 // operand fetch is one ds_read_b128 (+ one b32 for a tap's left / right
 // neighbour), and the 3 taps of a kernel row share one fetch.  Wave tile:
 // 32 co x 16 ci x taps (2 x taps v_mfma_f32_16x16x4_f32 accumulators).
+#include <cstdlib>
+
 #include "unet.h"
 
 using namespace ertd;
@@ -204,13 +206,28 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
     }
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int rows, size_t cols,
-                                    float* __restrict__ out, int accumulate) {
-  const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= cols) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += part[(size_t)r * cols + j];
-  out[j] = accumulate ? out[j] + s : s;
+// dW[j] (+)= sum over ranges of part[r][j] (as reduce_rows_kernel in unet_train.hip)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rows,
+                                                           size_t cols, float* __restrict__ out,
+                                                           int accumulate) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const size_t j = (size_t)blockIdx.x * 64 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (j < cols) {
+    int r = ty;
+    for (; r + 4 < rows; r += 8) {
+      s0 += part[(size_t)r * cols + j];
+      s1 += part[(size_t)(r + 4) * cols + j];
+    }
+    if (r < rows) s0 += part[(size_t)r * cols + j];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && j < cols) {
+    const float s = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    out[j] = accumulate ? out[j] + s : s;
+  }
 }
 
 int n_cu() {
@@ -222,6 +239,11 @@ int n_cu() {
     return n;
   }();
   return v;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
 
 struct Plan {
@@ -245,11 +267,12 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
   p->ntiles = p->nco * p->nci;
   p->nchunks = B * (Ho / p->R);
   if (ks == 1 && Ho * Ho < PXC) return false;
-  // >= 4 chunks per range (keeps the partial traffic well below the operand
-  // traffic), about 4 workgroups per CU
-  const int want = (4 * n_cu() + p->ntiles - 1) / p->ntiles;
+  // about 2 workgroups per CU, >= 8 chunks per range (keeps the partial
+  // write + reduce traffic well below the operand traffic)
+  static const int wpc = env_int("ERTD_WGRAD_WPC", 2), min_cps = env_int("ERTD_WGRAD_CPS", 8);
+  const int want = (wpc * n_cu() + p->ntiles - 1) / p->ntiles;
   int cps = (p->nchunks + want - 1) / want;
-  if (cps < 4) cps = 4;
+  if (cps < min_cps) cps = min_cps;
   if (cps > p->nchunks) cps = p->nchunks;
   p->cps = cps;
   p->nsplit = (p->nchunks + cps - 1) / cps;
@@ -297,7 +320,7 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
   else e = launch_t<MODE_S1, 3>(a, p.lds, s);
   if (e != hipSuccess) return (int)e;
   const size_t cols = (size_t)Cout * (Ca + Cb) * ks * ks;
-  wgrad_reduce_kernel<<<(unsigned)((cols + 255) / 256), 256, 0, s>>>((const float*)ws, p.nsplit, cols,
+  wgrad_reduce_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>((const float*)ws, p.nsplit, cols,
                                                                     dw, accumulate);
   e = hipGetLastError();
   return e == hipSuccess ? ERTD_OK : (int)e;

@@ -102,7 +102,9 @@ SIGNATURES = {
     "ertd_conv_weight_flip": (_I, [_VP, _I, _I, _I, _VP, _VP]),
     "ertd_zero_insert": (_I, [_VP, _I, _I, _I, _VP, _VP]),
     "ertd_sum_pool2": (_I, [_VP, _I, _I, _I, _VP, _I, _VP]),
-    "ertd_channel_sums": (_I, [_VP, _I, _I, _I, _VP, _VP, _I, _VP]),
+    "ertd_channel_sums": (_I, [_VP, _I, _I, _I, _VP, _I, _VP, _I, _VP]),
+    "ertd_concat": (_I, [_VP, _VP, _I, _VP, _VP]),
+    "ertd_encoder_train_pack": (_I, [_VP, _VP, _VP, _VP]),
     "ertd_gemm_small": (_I, [_VP, _LL, _LL, _LL, _VP, _LL, _LL, _LL, _VP, _LL, _LL, _LL, _VP, _I, _I,
                              _I, _I, _F, _I, _VP]),
     "ertd_softmax_rows": (_I, [_VP, _LL, _I, _F, _VP, _VP]),

@@ -8,13 +8,21 @@ oracle/unet_torch.forward, the backward is checked against torch autograd on it
 
 The walk below runs the spec's forward keeping what the backward needs, then
 the backward in reverse order, every arithmetic op on a HIP kernel of
-libertdiff_hip.so (csrc/unet_train.hip: GroupNorm(+SiLU) forward/backward,
-im2col + fp32-MFMA weight-gradient GEMMs, channel sums, small GEMMs for the
-dense layers and the attention, softmax backward, the condition encoder's
-saved-activation forward/backward from the reference train step, multi-tensor
-Adam; csrc/unet_conv*.hip: every conv forward and every input gradient -- a
-conv of dY with the flipped weights, Winograd/MFMA like the forward).  torch
-only allocates the device buffers.
+libertdiff_hip.so:
+  csrc/unet_conv*.hip   every conv forward and every input gradient (a conv of
+                        dY with the flipped weights: Winograd / direct MFMA as
+                        the forward)
+  csrc/unet_wgrad.hip   every conv weight gradient (implicit GEMM, fp32 MFMA)
+  csrc/unet_train.hip   GroupNorm(+SiLU) apply / backward, channel sums, small
+                        GEMMs (dense layers, attention), softmax backward, the
+                        condition encoder's saved-activation forward / backward
+                        (the reference train step's kernels), MSE, multi-tensor
+                        Adam, concat
+torch only allocates the device buffers.
+
+The 2 x (ResBlocks) embedding projections run as ONE GEMM each way: the
+forward gathers every ResBlock's emb weight into one (sum C, temb) matrix, the
+backward collects every dL/d(emb bias) column block into one (B, sum C) matrix.
 
   unet_train_forward(model, x, t, cond)            -> eps, tape
   unet_train_backward(model, tape, deps)           -> {param name: grad}
@@ -27,24 +35,25 @@ from __future__ import annotations
 
 import ctypes
 import math
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, Optional
 
 import torch
 
 from . import _lib
-from .unet import ConditionalUNet, conv2d
+from .unet import ConditionalUNet
 
 ACT_GN_SILU, ACT_GN = 1, 2
 MODE_S1, MODE_S2, MODE_UP = 0, 1, 2
 ELT_SILU, ELT_SILU_BWD, ELT_RELU, ELT_RELU_BWD, ELT_ADD, ELT_SCALE = range(6)
-
-
-def _s(dev):
-    return _lib.stream_of(dev)
+PREC_FP32 = 0
 
 
 def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
+
+
+def _arr(ts, ctype=ctypes.c_void_p):
+    return (ctype * len(ts))(*ts)
 
 
 class _K:
@@ -53,12 +62,44 @@ class _K:
     def __init__(self, dev):
         self.dev = dev
         self.lib = _lib.lib()
+        self.s = _lib.stream_of(dev)
+        self._ws: Optional[torch.Tensor] = None
+        self._zero: Dict[int, torch.Tensor] = {}
 
     def empty(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)
 
     def zeros(self, *shape):
         return torch.zeros(*shape, dtype=torch.float32, device=self.dev)
+
+    def zero_vec(self, n):
+        z = self._zero.get(n)
+        if z is None:
+            z = self._zero[n] = self.zeros(n)
+        return z
+
+    def ws(self, n):
+        """Scratch for one launch sequence (stream-ordered reuse is safe)."""
+        if self._ws is None or self._ws.numel() < n:
+            self._ws = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=self.dev)
+        return self._ws
+
+    # ---- convolution forward / input gradient (ertd_conv2d)
+    def conv(self, x, w, b, xb=None, mode=MODE_S1, ebias=None, res=None):
+        """conv(cat(x, xb)) + b (+ ebias[:, :, None, None]) (+ res); ebias may be a
+        column block of a wider (B, n) matrix (its row stride is passed)."""
+        B, Ca, H, _ = x.shape
+        Cb = 0 if xb is None else xb.shape[1]
+        Cout, Cin, ks, _ = w.shape
+        Ho = H // 2 if mode == MODE_S2 else (2 * H if mode == MODE_UP else H)
+        out = self.empty(B, Cout, Ho, Ho)
+        n = self.lib.ertd_conv2d_workspace_bytes(Cin, Cout, ks, PREC_FP32)
+        ws = self.ws(n)
+        _lib.check(self.lib.ertd_conv2d(
+            x.data_ptr(), Ca, _p(xb), Cb, B, H, w.data_ptr(), b.data_ptr(), Cout, ks, mode, None, 0,
+            _p(ebias), 0 if ebias is None else ebias.stride(0), _p(res), out.data_ptr(), PREC_FP32,
+            ws.data_ptr(), ws.numel(), self.s), "conv2d")
+        return out
 
     # ---- GroupNorm
     def gn_stats(self, xa, xb, groups, gamma, beta):
@@ -68,7 +109,7 @@ class _K:
         mr = self.empty(B, groups, 2)
         _lib.check(self.lib.ertd_gn_stats_mr(xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups,
                                              gamma.data_ptr(), beta.data_ptr(), ss.data_ptr(),
-                                             mr.data_ptr(), _s(self.dev)), "gn_stats_mr")
+                                             mr.data_ptr(), self.s), "gn_stats_mr")
         return ss, mr
 
     def gn_apply(self, xa, xb, ss, act):
@@ -76,7 +117,7 @@ class _K:
         Cb = 0 if xb is None else xb.shape[1]
         out = self.empty(B, Ca + Cb, H, W)
         _lib.check(self.lib.ertd_gn_act_apply(xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, ss.data_ptr(),
-                                              act, out.data_ptr(), _s(self.dev)), "gn_act_apply")
+                                              act, out.data_ptr(), self.s), "gn_act_apply")
         return out
 
     def gn_backward(self, xa, xb, groups, gamma, beta, mr, act, dy, dxa, dxb, accumulate):
@@ -84,93 +125,103 @@ class _K:
         B, Ca, H, W = xa.shape
         Cb = 0 if xb is None else xb.shape[1]
         C = Ca + Cb
-        part = self.empty(2, B, C)
+        part = self.empty(B, 2, C)
         _lib.check(self.lib.ertd_gn_act_backward(
             xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups, gamma.data_ptr(), beta.data_ptr(),
             mr.data_ptr(), act, dy.data_ptr(), dxa.data_ptr(), _p(dxb), int(accumulate),
-            part.data_ptr(), _s(self.dev)), "gn_act_backward")
-        dg, db = self.empty(C), self.empty(C)
-        self.reduce_rows(part[0], B, C, dg)
-        self.reduce_rows(part[1], B, C, db)
-        return dg, db
+            part.data_ptr(), self.s), "gn_act_backward")
+        dgb = self.empty(2, C)
+        self.reduce_rows(part, B, 2 * C, dgb)
+        return dgb[0], dgb[1]
 
     def reduce_rows(self, part, rows, cols, out, accumulate=False):
         _lib.check(self.lib.ertd_reduce_rows(part.data_ptr(), rows, cols, out.data_ptr(),
-                                             int(accumulate), _s(self.dev)), "reduce_rows")
+                                             int(accumulate), self.s), "reduce_rows")
 
     # ---- conv gradients
-    def im2col(self, x, ks, mode):
-        B, C, H, _ = x.shape
-        Ho = H // 2 if mode == MODE_S2 else (2 * H if mode == MODE_UP else H)
-        out = self.empty(B, C * ks * ks, Ho * Ho)
-        _lib.check(self.lib.ertd_im2col(x.data_ptr(), C, B, H, ks, mode, out.data_ptr(),
-                                        _s(self.dev)), "im2col")
-        return out
-
-    def wgrad(self, dy, xcol, out, accumulate=False):
-        """out (M, N) (+)= sum_b dy_b (M, P) . xcol_b (N, P)^T."""
-        B, M = dy.shape[0], dy.shape[1]
-        P = dy[0, 0].numel()
-        N = xcol.shape[1]
-        n = self.lib.ertd_wgrad_ws_bytes(M, N, P, B)
-        ws = torch.empty(n, dtype=torch.uint8, device=self.dev)
-        _lib.check(self.lib.ertd_wgrad_gemm(dy.data_ptr(), xcol.data_ptr(), M, N, P, B, M * P, N * P,
-                                            out.data_ptr(), int(accumulate), ws.data_ptr(), n,
-                                            _s(self.dev)), "wgrad_gemm")
-
     def conv_wgrad(self, dy, xa, xb, ks, mode, out):
-        """out (Cout, Cin, ks, ks) = dL/dW of conv(cat(xa, xb)) on the implicit-GEMM
-        kernel; False when the geometry is outside it (caller falls back)."""
+        """out (Cout, Cin, ks, ks) = dL/dW of conv(cat(xa, xb)) (implicit GEMM)."""
         B, Ca, H, _ = xa.shape
         Cb = 0 if xb is None else xb.shape[1]
         Cout = dy.shape[1]
         n = self.lib.ertd_conv_wgrad_ws_bytes(Ca + Cb, Cout, B, H, ks, mode)
         if n == 0:
             return False
-        ws = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        ws = self.ws(n)
         _lib.check(self.lib.ertd_conv_wgrad(dy.data_ptr(), xa.data_ptr(), Ca, _p(xb), Cb, B, H, Cout,
-                                            ks, mode, out.data_ptr(), 0, ws.data_ptr(), n,
-                                            _s(self.dev)), "conv_wgrad")
+                                            ks, mode, out.data_ptr(), 0, ws.data_ptr(), ws.numel(),
+                                            self.s), "conv_wgrad")
         return True
+
+    def wgrad_im2col(self, dy, xa, xb, ks, mode, out):
+        """Fallback outside the implicit-GEMM geometry: patch matrix + GEMM."""
+        B, Ca, H, W = xa.shape
+        x = xa
+        if xb is not None:
+            x = self.empty(B, Ca + xb.shape[1], H, W)
+            self.chan_copy(xa, 0, Ca, x, 0)
+            self.chan_copy(xb, 0, xb.shape[1], x, Ca)
+        C = x.shape[1]
+        if ks == 1:
+            col = x
+        else:
+            Ho = H // 2 if mode == MODE_S2 else (2 * H if mode == MODE_UP else H)
+            col = self.empty(B, C * ks * ks, Ho * Ho)
+            _lib.check(self.lib.ertd_im2col(x.data_ptr(), C, B, H, ks, mode, col.data_ptr(), self.s),
+                       "im2col")
+        M, N, P = dy.shape[1], C * ks * ks, dy[0, 0].numel()
+        n = self.lib.ertd_wgrad_ws_bytes(M, N, P, B)
+        ws = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        _lib.check(self.lib.ertd_wgrad_gemm(dy.data_ptr(), col.data_ptr(), M, N, P, B, M * P, N * P,
+                                            out.data_ptr(), 0, ws.data_ptr(), n, self.s), "wgrad_gemm")
 
     def flip(self, w):
         Cout, Cin, ks, _ = w.shape
         out = self.empty(Cin, Cout, ks, ks)
-        _lib.check(self.lib.ertd_conv_weight_flip(w.data_ptr(), Cout, Cin, ks, out.data_ptr(),
-                                                  _s(self.dev)), "conv_weight_flip")
+        _lib.check(self.lib.ertd_conv_weight_flip(w.data_ptr(), Cout, Cin, ks, out.data_ptr(), self.s),
+                   "conv_weight_flip")
         return out
 
     def zero_insert(self, x):
         B, C, Ho, _ = x.shape
         out = self.empty(B, C, 2 * Ho, 2 * Ho)
-        _lib.check(self.lib.ertd_zero_insert(x.data_ptr(), B, C, Ho, out.data_ptr(), _s(self.dev)),
+        _lib.check(self.lib.ertd_zero_insert(x.data_ptr(), B, C, Ho, out.data_ptr(), self.s),
                    "zero_insert")
         return out
 
     def sum_pool2(self, x, out, accumulate):
         B, C, H2, _ = x.shape
         _lib.check(self.lib.ertd_sum_pool2(x.data_ptr(), B, C, H2 // 2, out.data_ptr(),
-                                           int(accumulate), _s(self.dev)), "sum_pool2")
+                                           int(accumulate), self.s), "sum_pool2")
 
-    def chan_sums(self, x, out_c=None, accumulate_c=False):
+    def chan_sums(self, x, out_c=None, out_bc=None):
+        """Per (sample, channel) sums over HW into out_bc (may be a column block of
+        a wider matrix); optional per-channel sums into out_c."""
         B, C = x.shape[0], x.shape[1]
-        bc = self.empty(B, C)
-        _lib.check(self.lib.ertd_channel_sums(x.data_ptr(), B, C, x[0, 0].numel(), bc.data_ptr(),
-                                              _p(out_c), int(accumulate_c), _s(self.dev)),
-                   "channel_sums")
-        return bc
+        if out_bc is None:
+            out_bc = self.empty(B, C)
+        _lib.check(self.lib.ertd_channel_sums(x.data_ptr(), B, C, x[0, 0].numel(), out_bc.data_ptr(),
+                                              out_bc.stride(0), _p(out_c), 0, self.s), "channel_sums")
+        return out_bc
 
     def chan_copy(self, src, c0, cd, dst, d0, accumulate=False):
         B, Cs = src.shape[0], src.shape[1]
         _lib.check(self.lib.ertd_channel_slice(src.data_ptr(), B, Cs, c0, cd, src[0, 0].numel(),
                                                dst.data_ptr(), dst.shape[1], d0, int(accumulate),
-                                               _s(self.dev)), "channel_slice")
+                                               self.s), "channel_slice")
+
+    def concat(self, ts):
+        out = self.empty(sum(t.numel() for t in ts))
+        _lib.check(self.lib.ertd_concat(_arr([t.data_ptr() for t in ts]),
+                                        _arr([t.numel() for t in ts], ctypes.c_longlong), len(ts),
+                                        out.data_ptr(), self.s), "concat")
+        return out
 
     # ---- dense / attention
     def gemm(self, A, sA, Bm, sB, C, sC, I, J, K, batch=1, bias=None, alpha=1.0, accumulate=False):
         _lib.check(self.lib.ertd_gemm_small(A.data_ptr(), *sA, Bm.data_ptr(), *sB, C.data_ptr(), *sC,
                                             _p(bias), I, J, K, batch, float(alpha), int(accumulate),
-                                            _s(self.dev)), "gemm_small")
+                                            self.s), "gemm_small")
 
     def linear(self, x, w, b):
         """y (B, O) = x (B, K) W^T + b."""
@@ -180,106 +231,137 @@ class _K:
         self.gemm(x, (K, 1, 0), w, (1, K, 0), y, (O, 1, 0), Bn, O, K, bias=b)
         return y
 
-    def linear_backward(self, x, w, dy, dw, db, dx=None, accumulate_dx=False):
-        """dw = dy^T x, db = sum_b dy, dx (+)= dy W."""
+    def linear_backward(self, x, w, dy, dw, db, dx=None):
+        """dw = dy^T x, db = sum_b dy, dx = dy W  (dy (B, O) may be strided by rows).
+        dx with a long reduction (O > 256) is split over O in 64-wide ranges
+        (batched GEMM into partials, fixed-order reduction)."""
         Bn, K = x.shape
         O = w.shape[0]
-        self.gemm(dy, (1, O, 0), x, (K, 1, 0), dw, (K, 1, 0), O, K, Bn)
+        ld = dy.stride(0)
+        self.gemm(dy, (1, ld, 0), x, (K, 1, 0), dw, (K, 1, 0), O, K, Bn)
         self.reduce_rows(dy, Bn, O, db)
-        if dx is not None:
-            self.gemm(dy, (O, 1, 0), w, (K, 1, 0), dx, (K, 1, 0), Bn, K, O, accumulate=accumulate_dx)
+        if dx is None:
+            return
+        if O > 256 and O % 64 == 0:
+            ns = O // 64
+            part = self.empty(ns, Bn, K)
+            self.gemm(dy, (ld, 1, 64), w, (K, 1, 64 * K), part, (K, 1, Bn * K), Bn, K, 64, batch=ns)
+            self.reduce_rows(part, ns, Bn * K, dx)
+        else:
+            self.gemm(dy, (ld, 1, 0), w, (K, 1, 0), dx, (K, 1, 0), Bn, K, O)
 
     def elt(self, op, x, y=None, out=None, alpha=1.0, accumulate=False):
         if out is None:
             out = self.empty(*x.shape)
         _lib.check(self.lib.ertd_eltwise(op, x.data_ptr(), _p(y), out.data_ptr(), x.numel(),
-                                         float(alpha), int(accumulate), _s(self.dev)), "eltwise")
+                                         float(alpha), int(accumulate), self.s), "eltwise")
         return out
 
     def softmax(self, S, N, scale):
         P = self.empty(*S.shape)
         _lib.check(self.lib.ertd_softmax_rows(S.data_ptr(), S.numel() // N, N, float(scale),
-                                              P.data_ptr(), _s(self.dev)), "softmax_rows")
+                                              P.data_ptr(), self.s), "softmax_rows")
         return P
 
     def softmax_backward(self, P, dP, N, scale):
         dS = self.empty(*P.shape)
         _lib.check(self.lib.ertd_softmax_backward(P.data_ptr(), dP.data_ptr(), P.numel() // N, N,
-                                                  float(scale), dS.data_ptr(), _s(self.dev)),
+                                                  float(scale), dS.data_ptr(), self.s),
                    "softmax_backward")
         return dS
 
 
 class _Grads:
-    """Gradient buffers of activations, keyed by tensor identity (accumulated)."""
+    """dL/d(activation) buffers keyed by tensor identity (every keyed tensor is
+    kept alive by the tape).  The first contribution writes, later ones
+    accumulate: no zero fills."""
 
     def __init__(self, k: _K):
         self.k = k
         self.g: Dict[int, torch.Tensor] = {}
 
-    def of(self, t: torch.Tensor) -> torch.Tensor:
-        key = id(t)
-        if key not in self.g:
-            self.g[key] = self.k.zeros(*t.shape)
-        return self.g[key]
-
     def get(self, t):
         return self.g.get(id(t))
 
+    def target(self, t):
+        """(buffer, accumulate) for one more contribution to dL/dt."""
+        buf = self.g.get(id(t))
+        if buf is None:
+            buf = self.g[id(t)] = self.k.empty(*t.shape)
+            return buf, False
+        return buf, True
 
-def _conv_backward(k: _K, G: _Grads, grads, name, w, xa, xb, dy, mode, x_needs_grad=True):
-    """Gradients of y = conv(cat(xa, xb)) (+ bias): weight and bias grads into
-    grads[name.weight/.bias]; returns dL/d cat(xa, xb) (or None)."""
+    def add(self, t, v, owned=False):
+        """dL/dt += v (v adopted as the buffer when it is the first and owned)."""
+        buf = self.g.get(id(t))
+        if buf is None and owned:
+            self.g[id(t)] = v
+            return
+        buf, acc = self.target(t)
+        self.k.elt(ELT_SCALE, v, out=buf, alpha=1.0, accumulate=acc)
+
+    def add_cat(self, dx, xa, xb):
+        """Split dL/d cat(xa, xb) into the two inputs' gradients."""
+        if xb is None:
+            self.add(xa, dx, owned=True)
+            return
+        Ca = xa.shape[1]
+        for t, c0, cd in ((xa, 0, Ca), (xb, Ca, xb.shape[1])):
+            buf, acc = self.target(t)
+            self.k.chan_copy(dx, c0, cd, buf, 0, accumulate=acc)
+
+
+def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True):
+    """Gradients of y = conv(cat(xa, xb)) + bias: weight and bias grads into
+    grads[name.weight / .bias]; returns dL/d cat(xa, xb) (or None)."""
     Cout, Cin, ks, _ = w.shape
-    # weight / bias
-    dW = k.empty(Cout, Cin * ks * ks)
+    dW = k.empty(Cout, Cin, ks, ks)
     if not k.conv_wgrad(dy, xa, xb, ks, mode, dW):
-        # outside the implicit-GEMM kernel's geometry: patch matrix + GEMM
-        x_conv = xa
-        if xb is not None:
-            B, Ca, H, W = xa.shape
-            x_conv = k.empty(B, Cin, H, W)
-            k.chan_copy(xa, 0, Ca, x_conv, 0)
-            k.chan_copy(xb, 0, xb.shape[1], x_conv, Ca)
-        col = x_conv if ks == 1 else k.im2col(x_conv, ks, mode)
-        k.wgrad(dy, col.view(col.shape[0], col.shape[1], -1), dW)
-    grads[name + ".weight"] = dW.view(Cout, Cin, ks, ks)
+        k.wgrad_im2col(dy, xa, xb, ks, mode, dW)
+    grads[name + ".weight"] = dW
     db = k.empty(Cout)
-    k.chan_sums(dy, db)
+    k.chan_sums(dy, out_c=db)
     grads[name + ".bias"] = db
     if not x_needs_grad:
         return None
-    # input gradient: conv of dY with the flipped weights
+    # input gradient: a conv of dY with the flipped, transposed weights
     wf = k.flip(w)
-    zb = k.zeros(Cin)
+    zb = k.zero_vec(Cin)
     if mode == MODE_S2:
-        dx = conv2d(k.zero_insert(dy), wf, zb)
-    elif mode == MODE_UP:
-        du = conv2d(dy, wf, zb)
+        return k.conv(k.zero_insert(dy), wf, zb)
+    if mode == MODE_UP:
+        du = k.conv(dy, wf, zb)
         B, _, H2, _ = du.shape
         dx = k.empty(B, Cin, H2 // 2, H2 // 2)
         k.sum_pool2(du, dx, False)
-    else:
-        dx = conv2d(dy, wf, zb)
-    return dx
+        return dx
+    return k.conv(dy, wf, zb)
 
 
-def _scatter_dx(k: _K, G: _Grads, dx, xa, xb):
-    """Accumulate an input gradient of cat(xa, xb) into the grads of xa and xb."""
-    Ca = xa.shape[1]
-    k.chan_copy(dx, 0, Ca, G.of(xa), 0, accumulate=True)
-    if xb is not None:
-        k.chan_copy(dx, Ca, xb.shape[1], G.of(xb), 0, accumulate=True)
+def _encoder_pack(model: ConditionalUNet, k: _K, W):
+    """The condition encoder's conv weights in the reference-path packing."""
+    n = k.lib.ertd_packed_floats()
+    pk = getattr(model, "_enc_train_pack", None)
+    if pk is None or pk.device != k.dev or pk.numel() != n:
+        pk = torch.empty(n, dtype=torch.float32, device=k.dev)
+        model._enc_train_pack = pk
+    _lib.check(k.lib.ertd_encoder_train_pack(W["condition_encoder.0.weight"].data_ptr(),
+                                             W["condition_encoder.2.weight"].data_ptr(),
+                                             pk.data_ptr(), k.s), "encoder_train_pack")
+    return pk
 
 
 @torch.no_grad()
 def unet_train_forward(model: ConditionalUNet, x, t, cond):
-    """eps (B, image^2) = the spec forward with everything the backward needs."""
+    """eps (B, image^2) = the spec forward, with everything the backward needs."""
     if model.precision != "fp32":
         raise RuntimeError("ertdiff: the U-Net train step runs fp32 (set_precision('fp32'))")
     dev = _lib.require_device(x, t, cond, model.conv_in.weight)
     k = _K(dev)
     W = dict(model.named_parameters())
+    for n, p in W.items():
+        if not p.is_contiguous():
+            raise RuntimeError(f"ertdiff: parameter {n} must be contiguous")
     sp = model.spec
     g = sp["groups"]
     B = x.shape[0]
@@ -294,41 +376,52 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
         e1 = k.linear(sin, W["time_embed.0.weight"], W["time_embed.0.bias"])
         se1 = k.elt(ELT_SILU, e1)
         e2 = k.linear(se1, W["time_embed.2.weight"], W["time_embed.2.bias"])
-        packed = model.packed_weights(dev)      # the reference-layout encoder pack comes first
+        packed = _encoder_pack(model, k, W)
         ews = torch.empty(k.lib.ertd_encoder_train_ws_bytes(B, L), dtype=torch.uint8, device=dev)
         m = k.empty(B, 64)
         _lib.check(k.lib.ertd_encoder_train_fwd(
             packed.data_ptr(), W["condition_encoder.0.bias"].data_ptr(),
             W["condition_encoder.2.bias"].data_ptr(), cond.data_ptr(), B, L, m.data_ptr(),
-            ews.data_ptr(), ews.numel(), _s(dev)), "encoder_train_fwd")
+            ews.data_ptr(), ews.numel(), k.s), "encoder_train_fwd")
         z3 = k.linear(m, W["condition_encoder.6.weight"], W["condition_encoder.6.bias"])
         cemb = k.elt(ELT_RELU, z3)
         cp = k.linear(cemb, W["cond_proj.weight"], W["cond_proj.bias"])
         emb = k.elt(ELT_ADD, e2, cp)
         ea = k.elt(ELT_SILU, emb)
+        # every ResBlock's embedding projection in one GEMM
+        blocks = [n[:-len(".emb.weight")] for n in W if n.endswith(".emb.weight")]
+        eoff, o = {}, 0
+        for n in blocks:
+            eoff[n] = o
+            o += W[n + ".emb.weight"].shape[0]
+        temb = ea.shape[1]
+        w_all = k.concat([W[n + ".emb.weight"] for n in blocks]).view(o, temb)
+        b_all = k.concat([W[n + ".emb.bias"] for n in blocks])
+        eb_all = k.linear(ea, w_all, b_all)
         tape.update(sin=sin, e1=e1, se1=se1, packed=packed, ews=ews, m=m, z3=z3, cemb=cemb, emb=emb,
-                    ea=ea)
+                    ea=ea, w_all=w_all, eoff=eoff, blocks=blocks, ctot=o)
 
         def resblock(n, xa, xb):
             Cin = xa.shape[1] + (0 if xb is None else xb.shape[1])
             cout = W[n + ".conv1.weight"].shape[0]
             ss1, mr1 = k.gn_stats(xa, xb, g, W[n + ".norm1.weight"], W[n + ".norm1.bias"])
             a1 = k.gn_apply(xa, xb, ss1, ACT_GN_SILU)
-            eb = k.linear(ea, W[n + ".emb.weight"], W[n + ".emb.bias"])
-            h = conv2d(a1, W[n + ".conv1.weight"], W[n + ".conv1.bias"], ebias=eb)
+            eb = eb_all[:, eoff[n]:eoff[n] + cout]
+            h = k.conv(a1, W[n + ".conv1.weight"], W[n + ".conv1.bias"], ebias=eb)
             ss2, mr2 = k.gn_stats(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"])
             a2 = k.gn_apply(h, None, ss2, ACT_GN_SILU)
             if Cin != cout:
-                sk = conv2d(xa, W[n + ".skip.weight"], W[n + ".skip.bias"], x2=xb)
+                sk = k.conv(xa, W[n + ".skip.weight"], W[n + ".skip.bias"], xb=xb)
             else:
                 sk = xa
-            y = conv2d(a2, W[n + ".conv2.weight"], W[n + ".conv2.bias"], res=sk)
+            y = k.conv(a2, W[n + ".conv2.weight"], W[n + ".conv2.bias"], res=sk)
             nodes.append(("res", n, dict(xa=xa, xb=xb, mr1=mr1, a1=a1, h=h, mr2=mr2, a2=a2,
                                          skip=Cin != cout, y=y)))
             return y
 
-        h = conv2d(x.reshape(B, 1, img, img), W["conv_in.weight"], W["conv_in.bias"])
-        nodes.append(("conv_in", "conv_in", dict(x=x.reshape(B, 1, img, img), y=h)))
+        x4 = x.reshape(B, 1, img, img)
+        h = k.conv(x4, W["conv_in.weight"], W["conv_in.bias"])
+        nodes.append(("conv_in", "conv_in", dict(x=x4, y=h)))
         hs = [h]
         nl = len(sp["ch_mult"])
         for i in range(nl):
@@ -336,8 +429,8 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
                 h = resblock(f"down.{i}.res.{r}", h, None)
                 hs.append(h)
             if i != nl - 1:
-                y = conv2d(h, W[f"down.{i}.downsample.weight"], W[f"down.{i}.downsample.bias"],
-                           mode="down")
+                y = k.conv(h, W[f"down.{i}.downsample.weight"], W[f"down.{i}.downsample.bias"],
+                           mode=MODE_S2)
                 nodes.append(("down", f"down.{i}.downsample", dict(x=h, y=y)))
                 h = y
                 hs.append(h)
@@ -348,7 +441,7 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             N = h.shape[2] * h.shape[3]
             ssn, mrn = k.gn_stats(h, None, g, W[n + ".norm.weight"], W[n + ".norm.bias"])
             an = k.gn_apply(h, None, ssn, ACT_GN)
-            qkv = conv2d(an, W[n + ".qkv.weight"], W[n + ".qkv.bias"]).view(B, 3, C, N)
+            qkv = k.conv(an, W[n + ".qkv.weight"], W[n + ".qkv.bias"]).view(B, 3, C, N)
             q, kk, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
             S = k.empty(B, N, N)    # S[i][j] = sum_c q[c][i] k[c][j]
             k.gemm(q, (1, N, 3 * C * N), kk, (N, 1, 3 * C * N), S, (N, 1, N * N), N, N, C, batch=B)
@@ -356,7 +449,7 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             O = k.empty(B, C, N)    # O[c][i] = sum_j v[c][j] P[i][j]
             k.gemm(v, (N, 1, 3 * C * N), P, (1, N, N * N), O, (N, 1, C * N), C, N, N, batch=B)
             O4 = O.view(B, C, h.shape[2], h.shape[3])
-            y = conv2d(O4, W[n + ".proj.weight"], W[n + ".proj.bias"], res=h)
+            y = k.conv(O4, W[n + ".proj.weight"], W[n + ".proj.bias"], res=h)
             nodes.append(("attn", n, dict(x=h, mr=mrn, an=an, qkv=qkv, P=P, O=O4, y=y)))
             h = y
         h = resblock("mid.res2", h, None)
@@ -365,12 +458,12 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
                 sk = hs.pop()
                 h = resblock(f"up.{i}.res.{r}", h, sk)
             if i != 0:
-                y = conv2d(h, W[f"up.{i}.upsample.weight"], W[f"up.{i}.upsample.bias"], mode="up")
+                y = k.conv(h, W[f"up.{i}.upsample.weight"], W[f"up.{i}.upsample.bias"], mode=MODE_UP)
                 nodes.append(("up", f"up.{i}.upsample", dict(x=h, y=y)))
                 h = y
         sso, mro = k.gn_stats(h, None, g, W["norm_out.weight"], W["norm_out.bias"])
         ao = k.gn_apply(h, None, sso, ACT_GN_SILU)
-        eps = conv2d(ao, W["conv_out.weight"], W["conv_out.bias"])
+        eps = k.conv(ao, W["conv_out.weight"], W["conv_out.bias"])
         nodes.append(("out", "conv_out", dict(x=h, mr=mro, a=ao, y=eps)))
     return eps.reshape(B, -1), tape
 
@@ -385,35 +478,33 @@ def unet_train_backward(model: ConditionalUNet, tape, deps) -> Dict[str, torch.T
     B = tape["B"]
     grads: Dict[str, torch.Tensor] = {}
     G = _Grads(k)
-    ea = tape["ea"]
-    temb = ea.shape[1]
-    d_ea = k.zeros(B, temb)
+    eoff = tape["eoff"]
+    deb_all = k.empty(B, tape["ctot"])        # dL/d(emb projection), every ResBlock
     with torch.cuda.device(dev):
         nodes = tape["nodes"]
-        # dL/deps seeds the last node's output
         last = nodes[-1][2]["y"]
-        G.g[id(last)] = deps.reshape(last.shape).contiguous()
+        G.g[id(last)] = deps.reshape(last.shape)
         for kind, n, d in reversed(nodes):
             dy = G.get(d["y"])
             if dy is None:
-                dy = k.zeros(*d["y"].shape)
+                raise RuntimeError(f"ertdiff: no gradient reached {n}")
             if kind == "out":
-                dx_a = _conv_backward(k, G, grads, n, W[n + ".weight"], d["a"], None, dy, MODE_S1)
+                da = _conv_backward(k, grads, n, W[n + ".weight"], d["a"], None, dy, MODE_S1)
+                buf, acc = G.target(d["x"])
                 dg, db = k.gn_backward(d["x"], None, g, W["norm_out.weight"], W["norm_out.bias"],
-                                       d["mr"], ACT_GN_SILU, dx_a, G.of(d["x"]), None, True)
+                                       d["mr"], ACT_GN_SILU, da, buf, None, acc)
                 grads["norm_out.weight"], grads["norm_out.bias"] = dg, db
-            elif kind == "up" or kind == "down":
+            elif kind in ("up", "down"):
                 mode = MODE_UP if kind == "up" else MODE_S2
-                dx = _conv_backward(k, G, grads, n, W[n + ".weight"], d["x"], None, dy, mode)
-                k.elt(ELT_ADD, dx, G.of(d["x"]), out=G.of(d["x"]))
+                dx = _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, mode)
+                G.add(d["x"], dx, owned=True)
             elif kind == "conv_in":
-                _conv_backward(k, G, grads, n, W[n + ".weight"], d["x"], None, dy, MODE_S1,
+                _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, MODE_S1,
                                x_needs_grad=False)
             elif kind == "attn":
                 x = d["x"]
-                # y = x + proj(O): residual
-                k.elt(ELT_ADD, dy, G.of(x), out=G.of(x))
-                dO = _conv_backward(k, G, grads, n + ".proj", W[n + ".proj.weight"], d["O"], None,
+                G.add(x, dy)                          # y = x + proj(O)
+                dO = _conv_backward(k, grads, n + ".proj", W[n + ".proj.weight"], d["O"], None,
                                     dy, MODE_S1)
                 C = x.shape[1]
                 N = x.shape[2] * x.shape[3]
@@ -433,63 +524,68 @@ def unet_train_backward(model: ConditionalUNet, tape, deps) -> Dict[str, torch.T
                        N, batch=B)
                 k.gemm(q, (N, 1, 3 * C * N), dS, (N, 1, N * N), dqkv[:, 1], (N, 1, 3 * C * N), C, N,
                        N, batch=B)
-                dan = _conv_backward(k, G, grads, n + ".qkv", W[n + ".qkv.weight"], d["an"], None,
+                dan = _conv_backward(k, grads, n + ".qkv", W[n + ".qkv.weight"], d["an"], None,
                                      dqkv.view(B, 3 * C, x.shape[2], x.shape[3]), MODE_S1)
+                buf, acc = G.target(x)
                 dg, db = k.gn_backward(x, None, g, W[n + ".norm.weight"], W[n + ".norm.bias"],
-                                       d["mr"], ACT_GN, dan, G.of(x), None, True)
+                                       d["mr"], ACT_GN, dan, buf, None, acc)
                 grads[n + ".norm.weight"], grads[n + ".norm.bias"] = dg, db
             elif kind == "res":
                 xa, xb = d["xa"], d["xb"]
-                # y = conv2(a2) + b2 + skip
+                # y = conv2(a2) + b2 + skip(cat(xa, xb))
                 if d["skip"]:
-                    dxs = _conv_backward(k, G, grads, n + ".skip", W[n + ".skip.weight"], xa, xb, dy,
+                    dxs = _conv_backward(k, grads, n + ".skip", W[n + ".skip.weight"], xa, xb, dy,
                                          MODE_S1)
-                    _scatter_dx(k, G, dxs, xa, xb)
+                    G.add_cat(dxs, xa, xb)
                 else:
-                    k.elt(ELT_ADD, dy, G.of(xa), out=G.of(xa))
-                da2 = _conv_backward(k, G, grads, n + ".conv2", W[n + ".conv2.weight"], d["a2"], None,
+                    G.add(xa, dy)
+                da2 = _conv_backward(k, grads, n + ".conv2", W[n + ".conv2.weight"], d["a2"], None,
                                      dy, MODE_S1)
                 h = d["h"]
-                dh = k.zeros(*h.shape)
+                dh = k.empty(*h.shape)
                 dg, db = k.gn_backward(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"],
                                        d["mr2"], ACT_GN_SILU, da2, dh, None, False)
                 grads[n + ".norm2.weight"], grads[n + ".norm2.bias"] = dg, db
                 # h = conv1(a1) + b1 + emb(ea): the emb grad is dh summed over pixels
-                deb = k.chan_sums(dh)
-                we = W[n + ".emb.weight"]
-                dwe, dbe = k.empty(*we.shape), k.empty(we.shape[0])
-                k.linear_backward(ea, we, deb, dwe, dbe, d_ea, accumulate_dx=True)
-                grads[n + ".emb.weight"], grads[n + ".emb.bias"] = dwe, dbe
-                da1 = _conv_backward(k, G, grads, n + ".conv1", W[n + ".conv1.weight"], d["a1"], None,
+                cout = h.shape[1]
+                k.chan_sums(dh, out_bc=deb_all[:, eoff[n]:eoff[n] + cout])
+                da1 = _conv_backward(k, grads, n + ".conv1", W[n + ".conv1.weight"], d["a1"], None,
                                      dh, MODE_S1)
-                dxa = G.of(xa)
-                dxb = None if xb is None else G.of(xb)
+                dxa, acc_a = G.target(xa)
+                dxb, acc_b = (None, acc_a) if xb is None else G.target(xb)
+                if acc_a != acc_b:     # one accumulate flag per launch: pre-zero the new one
+                    (dxb if acc_a else dxa).zero_()
                 dg, db = k.gn_backward(xa, xb, g, W[n + ".norm1.weight"], W[n + ".norm1.bias"],
-                                       d["mr1"], ACT_GN_SILU, da1, dxa, dxb, True)
+                                       d["mr1"], ACT_GN_SILU, da1, dxa, dxb, acc_a or acc_b)
                 grads[n + ".norm1.weight"], grads[n + ".norm1.bias"] = dg, db
+        # ---- every ResBlock's emb projection at once: ea (B, temb) -> (B, sum C)
+        ea, w_all = tape["ea"], tape["w_all"]
+        ctot, temb = w_all.shape
+        dw_all, db_all = k.empty(ctot, temb), k.empty(ctot)
+        d_ea = k.empty(B, temb)
+        k.linear_backward(ea, w_all, deb_all, dw_all, db_all, d_ea)
+        for n in tape["blocks"]:
+            o, c = eoff[n], W[n + ".emb.weight"].shape[0]
+            grads[n + ".emb.weight"], grads[n + ".emb.bias"] = dw_all[o:o + c], db_all[o:o + c]
         # ---- embedding path: ea = silu(emb), emb = time MLP + cond_proj(cond_emb)
         d_emb = k.elt(ELT_SILU_BWD, tape["emb"], d_ea)
-        dse1 = k.zeros(B, tape["se1"].shape[1])
-        for nm, xin, dxin in (("time_embed.2", tape["se1"], dse1),):
-            w = W[nm + ".weight"]
-            dw, db = k.empty(*w.shape), k.empty(w.shape[0])
-            k.linear_backward(xin, w, d_emb, dw, db, dxin)
-            grads[nm + ".weight"], grads[nm + ".bias"] = dw, db
+        w = W["time_embed.2.weight"]
+        dw, db, dse1 = k.empty(*w.shape), k.empty(w.shape[0]), k.empty(B, tape["se1"].shape[1])
+        k.linear_backward(tape["se1"], w, d_emb, dw, db, dse1)
+        grads["time_embed.2.weight"], grads["time_embed.2.bias"] = dw, db
         de1 = k.elt(ELT_SILU_BWD, tape["e1"], dse1)
         w = W["time_embed.0.weight"]
         dw, db = k.empty(*w.shape), k.empty(w.shape[0])
         k.linear_backward(tape["sin"], w, de1, dw, db)
         grads["time_embed.0.weight"], grads["time_embed.0.bias"] = dw, db
         w = W["cond_proj.weight"]
-        dw, db = k.empty(*w.shape), k.empty(w.shape[0])
-        dcemb = k.zeros(B, w.shape[1])
+        dw, db, dcemb = k.empty(*w.shape), k.empty(w.shape[0]), k.empty(B, w.shape[1])
         k.linear_backward(tape["cemb"], w, d_emb, dw, db, dcemb)
         grads["cond_proj.weight"], grads["cond_proj.bias"] = dw, db
-        # condition encoder: cemb = relu(z3), z3 = W6 m + b6, m = pool mean
+        # condition encoder: cemb = relu(z3), z3 = W6 m + b6, m = mean over the L2 positions
         dz3 = k.elt(ELT_RELU_BWD, tape["z3"], dcemb)
         w = W["condition_encoder.6.weight"]
-        dw, db = k.empty(*w.shape), k.empty(w.shape[0])
-        dm = k.zeros(B, 64)
+        dw, db, dm = k.empty(*w.shape), k.empty(w.shape[0]), k.empty(B, 64)
         k.linear_backward(tape["m"], w, dz3, dw, db, dm)
         grads["condition_encoder.6.weight"], grads["condition_encoder.6.bias"] = dw, db
         L = tape["L"]
@@ -499,7 +595,7 @@ def unet_train_backward(model: ConditionalUNet, tape, deps) -> Dict[str, torch.T
         _lib.check(k.lib.ertd_encoder_train_bwd(
             tape["packed"].data_ptr(), tape["cond"].data_ptr(), gm.data_ptr(), B, L,
             enc[0].data_ptr(), enc[1].data_ptr(), enc[2].data_ptr(), enc[3].data_ptr(),
-            tape["ews"].data_ptr(), tape["ews"].numel(), _s(dev)), "encoder_train_bwd")
+            tape["ews"].data_ptr(), tape["ews"].numel(), k.s), "encoder_train_bwd")
         grads["condition_encoder.0.weight"], grads["condition_encoder.0.bias"] = enc[0], enc[1]
         grads["condition_encoder.2.weight"], grads["condition_encoder.2.bias"] = enc[2], enc[3]
     missing = [nm for nm, _ in model.layout if nm not in grads]
@@ -532,9 +628,14 @@ def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *
     t, cond), loss = MSELoss(mean)(eps, noise), backward, torch.optim.Adam
     step (state in optimizer.state).  Returns loss.item() (or the device scalar)."""
     from .model import q_sample
+    names = [nm for nm, _ in model.named_parameters()]
     params = [p for _, p in model.named_parameters()]
     dev = _lib.require_device(x0, cond, alpha_bar, params[0])
     B = x0.size(0)
+    if x0.dim() != 2 or x0.shape[1] != model.param_dim:
+        raise RuntimeError(f"ertdiff: x0 must be (B, {model.param_dim}), got {tuple(x0.shape)}")
+    if cond.dim() != 3 or cond.shape[0] != B or cond.shape[1] != _lib.CIN:
+        raise RuntimeError(f"ertdiff: condition must be (B, 14, L), got {tuple(cond.shape)}")
     if t is None:
         t = torch.randint(0, T, (B,), device=dev).long()
     if noise is None:
@@ -542,23 +643,22 @@ def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *
     x0 = _lib.f32c(x0, "x0")
     noise = _lib.f32c(noise, "noise")
     cond = _lib.f32c(cond, "condition")
+    tt = t.to(device=dev, dtype=torch.int64).contiguous()
     lib = _lib.lib()
     with torch.cuda.device(dev):
-        xn = q_sample(x0, t.to(dev), noise, alpha_bar)
-        eps, tape = unet_train_forward(model, xn, t.to(dev), cond)
+        xn = q_sample(x0, tt, noise, alpha_bar)
+        eps, tape = unet_train_forward(model, xn, tt, cond)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         deps = torch.empty_like(eps)
         _lib.check(lib.ertd_mse_loss(eps.data_ptr(), noise.data_ptr(), eps.numel(), loss.data_ptr(),
-                                     deps.data_ptr(), _s(dev)), "mse_loss")
+                                     deps.data_ptr(), _lib.stream_of(dev)), "mse_loss")
         grads = unet_train_backward(model, tape, deps)
-        names = [nm for nm, _ in model.named_parameters()]
         for nm, p in zip(names, params):
             p.grad = grads[nm].view_as(p)
         lr, b1, b2, ep, ms, vs, step = _adam_state(optimizer, params)
-        sizes = (ctypes.c_longlong * len(params))(*[p.numel() for p in params])
-        arrs = [(ctypes.c_void_p * len(ts))(*[x.data_ptr() for x in ts])
-                for ts in (params, [p.grad for p in params], ms, vs)]   # alive across the call
-        _lib.check(lib.ertd_adam_multi(*arrs, sizes, len(params), step, lr, b1, b2, ep, _s(dev)),
-                   "adam_multi")
+        sizes = _arr([p.numel() for p in params], ctypes.c_longlong)
+        arrs = [_arr([x.data_ptr() for x in ts]) for ts in (params, [p.grad for p in params], ms, vs)]
+        _lib.check(lib.ertd_adam_multi(*arrs, sizes, len(params), step, lr, b1, b2, ep,
+                                       _lib.stream_of(dev)), "adam_multi")
     model._packed_key = None      # parameters changed in place behind autograd's back: re-pack
     return loss if return_tensor else loss.item()

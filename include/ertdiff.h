@@ -323,14 +323,18 @@ int ertd_unet_plan_destroy(ertd_unet_plan* plan);
  * ertd_gn_stats_mr: ertd_group_norm_stats + mr_out (B, groups) {mean, rstd}.
  * ertd_gn_act_apply: out (B, Ca+Cb, HW) = act(cat(x, x2) * ss.x + ss.y), act 1 GN+SiLU / 2 GN.
  * ertd_gn_act_backward: dx / dx2 of act(GroupNorm(cat(x, x2))) given dy (B, C, HW);
- *   dgb_part (2, B, C): per-sample sum dxn*xhat (plane 0) and sum dxn (plane 1) ->
- *   dgamma / dbeta by ertd_reduce_rows.
+ *   dgb_part (B, 2, C): per-sample sum dxn*xhat ([b][0]) and sum dxn ([b][1]) ->
+ *   (dgamma | dbeta) by one ertd_reduce_rows (rows B, cols 2C).
  * ertd_im2col: out (B, C*ks*ks, Ho*Ho) patches of x (B, C, H, H), mode 0 s1 / 1 s2 / 2 upsample.
  * ertd_wgrad_gemm: dW (M, N) = sum_b dY_b (M, P) . X_b (N, P)^T (batch strides bsA, bsB),
  *   fp32 MFMA, split per sample + fixed-order reduction; ws >= ertd_wgrad_ws_bytes.
  * ertd_conv_weight_flip: out (Cin, Cout, ks, ks) = w (Cout, Cin, ks, ks) spatially flipped.
  * ertd_zero_insert: out (B, C, 2Ho, 2Ho) with x at even positions; ertd_sum_pool2: 2x2 sums.
- * ertd_channel_sums: out_bc (B, C) sums over HW; out_c (C) = sum over b (optional).
+ * ertd_channel_sums: out_bc (B, C; row stride ldo, 0 = C) sums over HW; out_c (C) = sum over b
+ *   (optional, ldo = C).
+ * ertd_concat: dst = cat(srcs[0..n)) of contiguous fp32 tensors (sizes in elements).
+ * ertd_encoder_train_pack: the encoder conv regions of the ertd_pack_weights layout
+ *   (ertd_packed_floats() buffer) from condition_encoder.0 / .2 weights.
  * ertd_gemm_small: C[b][i][j] = alpha sum_k A[b][i][k] B[b][k][j] (+ bias[j]) with element
  *   strides (a_i, a_k, a_b, b_k, b_j, b_b, c_i, c_j, c_b).
  * ertd_softmax_rows: P = softmax(scale S) per row; ertd_softmax_backward: dS = scale P (dP - <dP, P>).
@@ -360,7 +364,7 @@ int ertd_reduce_rows(const float* part, int rows, long long cols, float* out, in
 int ertd_conv_weight_flip(const float* w, int Cout, int Cin, int ks, float* out, void* stream);
 int ertd_zero_insert(const float* x, int B, int C, int Ho, float* out, void* stream);
 int ertd_sum_pool2(const float* x, int B, int C, int H, float* out, int accumulate, void* stream);
-int ertd_channel_sums(const float* x, int B, int C, int HW, float* out_bc, float* out_c,
+int ertd_channel_sums(const float* x, int B, int C, int HW, float* out_bc, int ldo, float* out_c,
                       int accumulate_c, void* stream);
 int ertd_gemm_small(const float* A, long long a_i, long long a_k, long long a_b, const float* Bm,
                     long long b_k, long long b_j, long long b_b, float* C, long long c_i,
@@ -384,6 +388,8 @@ size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mod
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
                     int Cout, int ks, int mode, float* dw, int accumulate, void* ws,
                     size_t ws_bytes, void* stream);
+int ertd_concat(const float* const* srcs, const long long* sizes, int n, float* dst, void* stream);
+int ertd_encoder_train_pack(const float* w0, const float* w2, float* packed, void* stream);
 size_t ertd_encoder_train_ws_bytes(int B, int L);
 int ertd_encoder_train_fwd(const float* packed, const float* b1, const float* b2, const float* cond,
                            int B, int L, float* m_out, void* ws, size_t ws_bytes, void* stream);
