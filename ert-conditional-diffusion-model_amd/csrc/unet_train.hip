@@ -75,53 +75,89 @@ __device__ __forceinline__ double wg_sum(double v, double* red, int tid) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Pass 1 reduces each channel's two sums within each wave (shuffles, no
+// barrier) into LDS; one barrier per 64 channels; the wave partials are then
+// added in a fixed order.  float4 loads throughout (HW % 4 == 0).
+constexpr int GNB_CB = 64;
 __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
     const float* __restrict__ xa, int Ca, const float* __restrict__ xb, int Cb, int HW, int groups,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float2* __restrict__ mr,
     int act, const float* __restrict__ dy, float* __restrict__ dxa, float* __restrict__ dxb,
     int accumulate, float* __restrict__ dgb) {
-  __shared__ double red[4];
-  const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int C = Ca + Cb, cpg = C / groups;
+  __shared__ double part[2][GNB_CB][4];
+  const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int C = Ca + Cb, cpg = C / groups, HW4 = HW / 4;
   const float2 m = mr[(size_t)b * groups + g];
   const float mean = m.x, rstd = m.y;
+  auto xptr = [&](int c) {
+    return c < Ca ? xa + ((size_t)b * Ca + c) * HW : xb + ((size_t)b * Cb + c - Ca) * HW;
+  };
+  auto dxn_of = [&](float xv, float dv, float ga, float be, float& xh) {
+    xh = (xv - mean) * rstd;
+    return act == ACT_GN_SILU ? dv * silu_grad(fmaf(ga, xh, be)) : dv;
+  };
   double A = 0.0, Bs = 0.0;
-  for (int cl = 0; cl < cpg; ++cl) {
-    const int c = g * cpg + cl;
-    const float* x = c < Ca ? xa + ((size_t)b * Ca + c) * HW : xb + ((size_t)b * Cb + c - Ca) * HW;
-    const float* d = dy + ((size_t)b * C + c) * HW;
-    const float ga = gamma[c], be = beta[c];
-    double sg = 0.0, sb = 0.0;
-    for (int p = tid; p < HW; p += 256) {
-      const float xh = (x[p] - mean) * rstd;
-      float dxn = d[p];
-      if (act == ACT_GN_SILU) dxn = dxn * silu_grad(fmaf(ga, xh, be));
-      sg += (double)dxn * xh;
-      sb += (double)dxn;
+  for (int c0 = 0; c0 < cpg; c0 += GNB_CB) {
+    const int nc = cpg - c0 < GNB_CB ? cpg - c0 : GNB_CB;
+    for (int cl = 0; cl < nc; ++cl) {
+      const int c = g * cpg + c0 + cl;
+      const float4* x = (const float4*)xptr(c);
+      const float4* d = (const float4*)(dy + ((size_t)b * C + c) * HW);
+      const float ga = gamma[c], be = beta[c];
+      double sg = 0.0, sb = 0.0;
+      for (int p = tid; p < HW4; p += 256) {
+        const float4 xv = x[p], dv = d[p];
+        float xh, dn;
+        dn = dxn_of(xv.x, dv.x, ga, be, xh); sg += (double)dn * xh; sb += (double)dn;
+        dn = dxn_of(xv.y, dv.y, ga, be, xh); sg += (double)dn * xh; sb += (double)dn;
+        dn = dxn_of(xv.z, dv.z, ga, be, xh); sg += (double)dn * xh; sb += (double)dn;
+        dn = dxn_of(xv.w, dv.w, ga, be, xh); sg += (double)dn * xh; sb += (double)dn;
+      }
+      sg = wave_sum_d(sg);
+      sb = wave_sum_d(sb);
+      if (lane == 0) {
+        part[0][cl][w] = sg;
+        part[1][cl][w] = sb;
+      }
     }
-    sg = wg_sum(sg, red, tid);
-    sb = wg_sum(sb, red, tid);
-    if (tid == 0) {
-      dgb[(size_t)(2 * b) * C + c] = (float)sg;        // [b][0][c]: dgamma partial
-      dgb[(size_t)(2 * b + 1) * C + c] = (float)sb;    // [b][1][c]: dbeta partial
+    __syncthreads();
+    for (int cl = 0; cl < nc; ++cl) {
+      const int c = g * cpg + c0 + cl;
+      const double sg = (part[0][cl][0] + part[0][cl][1]) + (part[0][cl][2] + part[0][cl][3]);
+      const double sb = (part[1][cl][0] + part[1][cl][1]) + (part[1][cl][2] + part[1][cl][3]);
+      if (tid == 0) {
+        dgb[(size_t)(2 * b) * C + c] = (float)sg;        // [b][0][c]: dgamma partial
+        dgb[(size_t)(2 * b + 1) * C + c] = (float)sb;    // [b][1][c]: dbeta partial
+      }
+      const double ga = gamma[c];
+      A += ga * sb;     // sum dxhat
+      Bs += ga * sg;    // sum dxhat xhat
     }
-    A += (double)ga * sb;     // sum dxhat
-    Bs += (double)ga * sg;    // sum dxhat xhat
+    __syncthreads();
   }
   const double n = (double)cpg * HW;
   const float mA = (float)(A / n), mB = (float)(Bs / n);
   for (int cl = 0; cl < cpg; ++cl) {
     const int c = g * cpg + cl;
-    const float* x = c < Ca ? xa + ((size_t)b * Ca + c) * HW : xb + ((size_t)b * Cb + c - Ca) * HW;
-    float* dx = c < Ca ? dxa + ((size_t)b * Ca + c) * HW : dxb + ((size_t)b * Cb + c - Ca) * HW;
-    const float* d = dy + ((size_t)b * C + c) * HW;
+    const float4* x = (const float4*)xptr(c);
+    float4* dx = (float4*)(c < Ca ? dxa + ((size_t)b * Ca + c) * HW : dxb + ((size_t)b * Cb + c - Ca) * HW);
+    const float4* d = (const float4*)(dy + ((size_t)b * C + c) * HW);
     const float ga = gamma[c], be = beta[c];
-    for (int p = tid; p < HW; p += 256) {
-      const float xh = (x[p] - mean) * rstd;
-      float dxn = d[p];
-      if (act == ACT_GN_SILU) dxn = dxn * silu_grad(fmaf(ga, xh, be));
-      const float v = rstd * ((ga * dxn - mA) - xh * mB);
-      dx[p] = accumulate ? dx[p] + v : v;
+    for (int p = tid; p < HW4; p += 256) {
+      const float4 xv = x[p], dv = d[p];
+      float4 o = accumulate ? dx[p] : float4{0.f, 0.f, 0.f, 0.f};
+      float xh, dn;
+      dn = dxn_of(xv.x, dv.x, ga, be, xh); o.x += rstd * ((ga * dn - mA) - xh * mB);
+      dn = dxn_of(xv.y, dv.y, ga, be, xh); o.y += rstd * ((ga * dn - mA) - xh * mB);
+      dn = dxn_of(xv.z, dv.z, ga, be, xh); o.z += rstd * ((ga * dn - mA) - xh * mB);
+      dn = dxn_of(xv.w, dv.w, ga, be, xh); o.w += rstd * ((ga * dn - mA) - xh * mB);
+      dx[p] = o;
     }
   }
 }
@@ -503,7 +539,7 @@ int ertd_gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B,
                          void* stream) {
   const int C = Ca + Cb;
   if (!x || !gamma || !beta || !mr || !dy || !dx || !dgb_part || B < 1 || Ca < 1 || Cb < 0 ||
-      (Cb > 0 && (!x2 || !dx2)) || groups < 1 || C % groups || HW < 1 ||
+      (Cb > 0 && (!x2 || !dx2)) || groups < 1 || C % groups || HW < 4 || HW % 4 ||
       (act != ACT_GN_SILU && act != ACT_GN))
     return ERTD_EINVAL;
   gn_act_bwd_kernel<<<dim3(groups, B), 256, 0, (hipStream_t)stream>>>(

@@ -46,7 +46,7 @@ __host__ __device__ constexpr int round_cis(int n) { return n + ((4 - n) % 64 + 
 struct Geo {
   int nr, roww, cis;
 };
-__host__ __device__ inline Geo geo(int mode, int ks, int Ho) {
+__host__ __device__ constexpr Geo geo(int mode, int ks, int Ho) {
   const int R = PXC / Ho;
   Geo g{};
   if (ks == 1) {
@@ -64,12 +64,13 @@ __device__ __forceinline__ const float* chan_ptr(const WgArgs& a, int b, int ci)
   return ci < a.Ca ? a.xa + ((size_t)b * a.Ca + ci) * hw : a.xb + ((size_t)b * a.Cb + ci - a.Ca) * hw;
 }
 
-template <int MODE, int KS>
+template <int MODE, int KS, int HO>
 __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int KK = KS * KS;
-  const int Ho = a.Ho, R = a.R, Cin = a.Ca + a.Cb;
-  const Geo G = geo(MODE, KS, Ho);
+  constexpr int Ho = HO, R = PXC / HO;
+  const int Cin = a.Ca + a.Cb;
+  constexpr Geo G = geo(MODE, KS, HO);
   float* dyL = smem;
   float* xL = smem + TCO * DYS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -86,34 +87,86 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
 #pragma unroll
     for (int t = 0; t < KK; ++t) acc[i][t] = f32x4{};
 
-  const int rows_per_b = Ho / R;
+  constexpr int rows_per_b = Ho / R;
   const int c_lo = split * a.cps, c_hi = min(a.nchunks, c_lo + a.cps);
-  for (int c = c_lo; c < c_hi; ++c) {
+  // Staging.  S1 / UP / 1x1: the next chunk's operands are loaded into
+  // registers while the current chunk's MFMAs run (one LDS buffer, register
+  // double buffering); S2 (two layers) loads synchronously.
+  constexpr int NDY = TCO * PXC / 4 / 256;          // dY float4 per thread
+  constexpr int q = Ho / 4;
+  constexpr int nx = KS == 1 ? TCI * PXC / 4 : TCI * G.nr * q;
+  constexpr int NXR = (nx + 255) / 256;
+  f32x4 dyr[NDY];
+  f32x4 xr[MODE == MODE_S2 ? 1 : NXR];
+  auto load = [&](int c) {
     const int b = c / rows_per_b, y0 = (c - b * rows_per_b) * R;
-    __syncthreads();
-    // ---- stage dY (64 co x 128 pixels): rows y0 .. y0+R-1 are contiguous
-    for (int i = tid; i < TCO * PXC / 4; i += 256) {
-      const int r = i / (PXC / 4), c4 = i - r * (PXC / 4);
-      const int co = co0 + r;
-      f32x4 v = f32x4{};
-      if (co < a.Cout)
-        v = *(const f32x4*)(a.dy + ((size_t)b * a.Cout + co) * Ho * Ho + (size_t)y0 * Ho + 4 * c4);
-      *(f32x4*)(dyL + r * DYS + 4 * c4) = v;
+#pragma unroll
+    for (int k = 0; k < NDY; ++k) {
+      const int i = tid + 256 * k, r = i / (PXC / 4), c4 = i - r * (PXC / 4), co = co0 + r;
+      dyr[k] = co < a.Cout
+                   ? *(const f32x4*)(a.dy + ((size_t)b * a.Cout + co) * Ho * Ho + (size_t)y0 * Ho + 4 * c4)
+                   : f32x4{};
     }
-    // ---- stage the input rows
-    if constexpr (KS == 1) {
-      for (int i = tid; i < TCI * PXC / 4; i += 256) {
-        const int r = i / (PXC / 4), c4 = i - r * (PXC / 4);
-        const int ci = ci0 + r;
+    if constexpr (MODE != MODE_S2) {
+#pragma unroll
+      for (int k = 0; k < NXR; ++k) {
+        const int i = tid + 256 * k;
         f32x4 v = f32x4{};
-        if (ci < Cin) v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)y0 * Ho + 4 * c4);
-        *(f32x4*)(xL + r * G.cis + 4 * c4) = v;
+        if (i < nx) {
+          if constexpr (KS == 1) {
+            const int r = i / (PXC / 4), c4 = i - r * (PXC / 4), ci = ci0 + r;
+            if (ci < Cin) v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)y0 * Ho + 4 * c4);
+          } else {
+            const int r = i / q, c4 = i - r * q;
+            const int cl = r / G.nr, rr = r - cl * G.nr;
+            const int ci = ci0 + cl, vy = y0 - 1 + rr;
+            if (ci < Cin && vy >= 0 && vy < Ho) {
+              if constexpr (MODE == MODE_UP) {
+                const float2 sv = *(const float2*)(chan_ptr(a, b, ci) + (size_t)(vy >> 1) * a.H + 2 * c4);
+                v = f32x4{sv.x, sv.x, sv.y, sv.y};
+              } else {
+                v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)vy * Ho + 4 * c4);
+              }
+            }
+          }
+        }
+        xr[k] = v;
       }
-    } else if constexpr (MODE == MODE_S2) {
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < NDY; ++k) {
+      const int i = tid + 256 * k, r = i / (PXC / 4), c4 = i - r * (PXC / 4);
+      *(f32x4*)(dyL + r * DYS + 4 * c4) = dyr[k];
+    }
+    if constexpr (MODE != MODE_S2) {
+#pragma unroll
+      for (int k = 0; k < NXR; ++k) {
+        const int i = tid + 256 * k;
+        if (i < nx) {
+          if constexpr (KS == 1) {
+            const int r = i / (PXC / 4), c4 = i - r * (PXC / 4);
+            *(f32x4*)(xL + r * G.cis + 4 * c4) = xr[k];
+          } else {
+            const int r = i / q, c4 = i - r * q;
+            const int cl = r / G.nr, rr = r - cl * G.nr;
+            *(f32x4*)(xL + cl * G.cis + rr * G.roww + 4 + 4 * c4) = xr[k];
+          }
+        }
+      }
+    }
+  };
+  if (c_lo < c_hi) load(c_lo);
+  for (int c = c_lo; c < c_hi; ++c) {
+    __syncthreads();
+    store();
+    if constexpr (MODE == MODE_S2) {
       // input rows 2 y0 - 1 .. 2 (y0 + R - 1) + 1, width H = 2 Ho; E at col 4, O at col Ho + 8
-      const int W = a.H, q = W / 4;
-      for (int i = tid; i < TCI * G.nr * q; i += 256) {
-        const int r = i / q, c4 = i - r * q;
+      const int b = c / rows_per_b, y0 = (c - b * rows_per_b) * R;
+      const int W = a.H, qw = W / 4;
+      for (int i = tid; i < TCI * G.nr * qw; i += 256) {
+        const int r = i / qw, c4 = i - r * qw;
         const int cl = r / G.nr, rr = r - cl * G.nr;
         const int ci = ci0 + cl, iy = 2 * y0 - 1 + rr;
         f32x4 v = f32x4{};
@@ -122,30 +175,14 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
         *(float2*)(row + 4 + 2 * c4) = float2{v.x, v.z};
         *(float2*)(row + Ho + 8 + 2 * c4) = float2{v.y, v.w};
       }
-    } else {
-      // virtual input rows y0 - 1 .. y0 + R (UP: source row / col halved)
-      const int q = Ho / 4;
-      for (int i = tid; i < TCI * G.nr * q; i += 256) {
-        const int r = i / q, c4 = i - r * q;
-        const int cl = r / G.nr, rr = r - cl * G.nr;
-        const int ci = ci0 + cl, vy = y0 - 1 + rr;
-        f32x4 v = f32x4{};
-        if (ci < Cin && vy >= 0 && vy < Ho) {
-          if constexpr (MODE == MODE_UP) {
-            const float2 s = *(const float2*)(chan_ptr(a, b, ci) + (size_t)(vy >> 1) * a.H + 2 * c4);
-            v = f32x4{s.x, s.x, s.y, s.y};
-          } else {
-            v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)vy * Ho + 4 * c4);
-          }
-        }
-        *(f32x4*)(xL + cl * G.cis + rr * G.roww + 4 + 4 * c4) = v;
-      }
     }
+    if (c + 1 < c_hi) load(c + 1);
     __syncthreads();
     // ---- MFMAs over the chunk's 128 pixels, 16 at a time
     const float* xw = xL + (cib * 16 + l16) * G.cis;
     const float* a0p = dyL + ((cb0 + 0) * 16 + l16) * DYS + 4 * g;
     const float* a1p = dyL + ((cb0 + 1) * 16 + l16) * DYS + 4 * g;
+#pragma unroll 1
     for (int p16 = 0; p16 < PXC; p16 += 16) {
       const f32x4 A0 = *(const f32x4*)(a0p + p16);
       const f32x4 A1 = *(const f32x4*)(a1p + p16);
@@ -256,7 +293,7 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
       mode > MODE_UP || (ks == 1 && mode != MODE_S1))
     return false;
   const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
-  if (Ho > PXC || PXC % Ho || (mode == MODE_S2 && H != 2 * Ho)) return false;
+  if ((Ho != 16 && Ho != 32 && Ho != 64 && Ho != 128) || (mode == MODE_S2 && H != 2 * Ho)) return false;
   if (ks == 3 && Ho < 16) return false;    // a 16-pixel group stays inside one row
   if (ks == 1 && Ho * Ho < 16) return false;
   const Geo G = geo(mode, ks, Ho);
@@ -267,9 +304,9 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
   p->ntiles = p->nco * p->nci;
   p->nchunks = B * (Ho / p->R);
   if (ks == 1 && Ho * Ho < PXC) return false;
-  // about 2 workgroups per CU, >= 8 chunks per range (keeps the partial
-  // write + reduce traffic well below the operand traffic)
-  static const int wpc = env_int("ERTD_WGRAD_WPC", 2), min_cps = env_int("ERTD_WGRAD_CPS", 8);
+  // about 4 workgroups per CU, >= 4 chunks per range (measured optimum at
+  // U2 B=32 of the partial write + reduce traffic vs occupancy: tools/wgrad_sweep.sh)
+  static const int wpc = env_int("ERTD_WGRAD_WPC", 4), min_cps = env_int("ERTD_WGRAD_CPS", 4);
   const int want = (wpc * n_cu() + p->ntiles - 1) / p->ntiles;
   int cps = (p->nchunks + want - 1) / want;
   if (cps < min_cps) cps = min_cps;
@@ -281,16 +318,27 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
   return true;
 }
 
-template <int MODE, int KS>
+template <int MODE, int KS, int HO>
 hipError_t launch_t(const WgArgs& a, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)wgrad_conv_kernel<MODE, KS>,
+    (void)hipFuncSetAttribute((const void*)wgrad_conv_kernel<MODE, KS, HO>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  wgrad_conv_kernel<MODE, KS><<<(unsigned)(a.ntiles * a.nsplit), 256, lds, s>>>(a);
+  wgrad_conv_kernel<MODE, KS, HO><<<(unsigned)(a.ntiles * a.nsplit), 256, lds, s>>>(a);
   return hipGetLastError();
+}
+
+template <int MODE, int KS>
+hipError_t launch_m(const WgArgs& a, size_t lds, hipStream_t s) {
+  switch (a.Ho) {
+    case 16: return launch_t<MODE, KS, 16>(a, lds, s);
+    case 32: return launch_t<MODE, KS, 32>(a, lds, s);
+    case 64: return launch_t<MODE, KS, 64>(a, lds, s);
+    case 128: return launch_t<MODE, KS, 128>(a, lds, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace
@@ -314,10 +362,10 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
            (float*)ws};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  if (ks == 1) e = launch_t<MODE_S1, 1>(a, p.lds, s);
-  else if (mode == MODE_S2) e = launch_t<MODE_S2, 3>(a, p.lds, s);
-  else if (mode == MODE_UP) e = launch_t<MODE_UP, 3>(a, p.lds, s);
-  else e = launch_t<MODE_S1, 3>(a, p.lds, s);
+  if (ks == 1) e = launch_m<MODE_S1, 1>(a, p.lds, s);
+  else if (mode == MODE_S2) e = launch_m<MODE_S2, 3>(a, p.lds, s);
+  else if (mode == MODE_UP) e = launch_m<MODE_UP, 3>(a, p.lds, s);
+  else e = launch_m<MODE_S1, 3>(a, p.lds, s);
   if (e != hipSuccess) return (int)e;
   const size_t cols = (size_t)Cout * (Ca + Cb) * ks * ks;
   wgrad_reduce_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>((const float*)ws, p.nsplit, cols,

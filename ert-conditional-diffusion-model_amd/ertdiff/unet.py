@@ -224,9 +224,36 @@ class ConditionalUNet(nn.Module):
             self._ws[dev] = ws
         return ws
 
-    @torch.no_grad()
     def forward(self, x: torch.Tensor, t: torch.Tensor, condition: torch.Tensor,
                 return_cond_emb: bool = False):
+        """eps (B, image^2).  With autograd recording and x or any parameter
+        requiring grad (the reference train loop, ERT_Conditional_Diffusion.py:
+        314-318), the call runs the train-mode forward (saved activations) and
+        loss.backward() runs the HIP backward (ertdiff.unet_train.UNetForwardFn);
+        otherwise (no_grad, return_cond_emb, or bf16 precision, which has no
+        backward) the inference forward (ertd_unet_forward)."""
+        if (torch.is_grad_enabled() and not return_cond_emb and self.precision == "fp32" and
+                (x.requires_grad or any(p.requires_grad for p in self.parameters()))):
+            from .unet_train import UNetForwardFn
+            dev = _lib.require_device(x, t, condition, self.conv_in.weight)
+            self._check_call(x, t, condition)
+            return UNetForwardFn.apply(self, _lib.f32c(x, "x"), t.to(device=dev, dtype=torch.int64)
+                                       .contiguous(), _lib.f32c(condition, "condition"),
+                                       *self._params())
+        return self._infer(x, t, condition, return_cond_emb)
+
+    def _check_call(self, x, t, cond):
+        B = x.shape[0]
+        if x.dim() != 2 or x.shape[1] != self.param_dim:
+            raise RuntimeError(f"ertdiff: x must be (B, {self.param_dim}), got {tuple(x.shape)}")
+        if cond.dim() != 3 or cond.shape[0] != B or cond.shape[1] != _lib.CIN:
+            raise RuntimeError(f"ertdiff: condition must be (B, 14, L), got {tuple(cond.shape)}")
+        if t.shape != (B,):
+            raise RuntimeError(f"ertdiff: t must be (B,), got {tuple(t.shape)}")
+
+    @torch.no_grad()
+    def _infer(self, x: torch.Tensor, t: torch.Tensor, condition: torch.Tensor,
+               return_cond_emb: bool = False):
         dev = _lib.require_device(x, t, condition, self.conv_in.weight)
         x = _lib.f32c(x, "x")
         cond = _lib.f32c(condition, "condition")

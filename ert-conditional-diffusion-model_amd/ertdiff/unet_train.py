@@ -469,8 +469,10 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
 
 
 @torch.no_grad()
-def unet_train_backward(model: ConditionalUNet, tape, deps) -> Dict[str, torch.Tensor]:
-    """Gradients of sum(deps * eps) w.r.t. every parameter (state_dict names)."""
+def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
+                        ) -> Dict[str, torch.Tensor]:
+    """Gradients of sum(deps * eps) w.r.t. every parameter (state_dict names),
+    and w.r.t. the input x under the key "__x__" when ``need_x``."""
     k: _K = tape["k"]
     dev = k.dev
     W = dict(model.named_parameters())
@@ -499,8 +501,10 @@ def unet_train_backward(model: ConditionalUNet, tape, deps) -> Dict[str, torch.T
                 dx = _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, mode)
                 G.add(d["x"], dx, owned=True)
             elif kind == "conv_in":
-                _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, MODE_S1,
-                               x_needs_grad=False)
+                dx = _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, MODE_S1,
+                                    x_needs_grad=need_x)
+                if need_x:
+                    grads["__x__"] = dx.view(B, -1)
             elif kind == "attn":
                 x = d["x"]
                 G.add(x, dy)                          # y = x + proj(O)
@@ -602,6 +606,28 @@ def unet_train_backward(model: ConditionalUNet, tape, deps) -> Dict[str, torch.T
     if missing:
         raise RuntimeError(f"ertdiff: no gradient for {missing[:4]}")
     return grads
+
+
+class UNetForwardFn(torch.autograd.Function):
+    """ConditionalUNet.forward under autograd: the train-mode forward keeps
+    its tape on ctx; backward runs unet_train_backward (HIP kernels) and hands
+    torch the per-parameter gradients, so the reference's own loop
+    (criterion(pred, noise).backward(); optimizer.step()) trains the U-Net."""
+
+    @staticmethod
+    def forward(ctx, model, x, t, cond, *params):
+        eps, tape = unet_train_forward(model, x, t, cond)
+        ctx.model, ctx.tape = model, tape
+        return eps
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g):
+        model, tape = ctx.model, ctx.tape
+        ctx.tape = None
+        grads = unet_train_backward(model, tape, g.contiguous(), need_x=ctx.needs_input_grad[1])
+        out = [grads[n].view_as(p) for n, p in model.named_parameters()]
+        return (None, grads.get("__x__"), None, None, *out)
 
 
 def _adam_state(optimizer, params):

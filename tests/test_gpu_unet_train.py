@@ -112,7 +112,8 @@ def test_unet_train_step_deterministic_and_learns(cuda_dev):
     for p, q in zip(m.parameters(), runs[0][1]):
         p.data.copy_(q)
     tt = torch.full((B,), 10, device=cuda_dev, dtype=torch.long)
-    a = m(x0, tt, cond)
+    with torch.no_grad():
+        a = m(x0, tt, cond)
     with torch.no_grad():
         ref = U.forward(x0.cpu(), tt.cpu(), cond.cpu(),
                         {k: v.detach().cpu() for k, v in m.named_parameters()}, cfg)
@@ -178,3 +179,86 @@ def test_conv_wgrad_rejects_bad_geometry(cuda_dev):
     assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 48, 3, 0) == 0      # not a power of two
     assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 32, 1, 1) == 0      # 1x1 stride 2
     assert lib.ertd_conv_wgrad(None, None, 1, None, 0, 1, 16, 1, 3, 0, None, 0, None, 0, None) != 0
+
+
+def test_unet_autograd_matches_fused_step(cuda_dev):
+    """The reference loop shape -- pred = model(x_noisy, t, cond); MSELoss;
+    loss.backward() -- runs the same HIP kernels as unet_train_step (same
+    parameter gradients); dL/dx against float64 autograd."""
+    B, L, T = 2, 129, 1000
+    cfg = U.CONFIGS["U1"]
+    x0 = torch.from_numpy(synth_normal((B, cfg.param_dim), 520)).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 521)).to(cuda_dev)
+    t = torch.from_numpy(synth_timesteps(B, T, 522)).to(cuda_dev)
+    noise = torch.from_numpy(synth_normal((B, cfg.param_dim), 523)).to(cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    m1 = ertdiff.ConditionalUNet.from_config("U1", seed=5).to(cuda_dev)
+    opt = torch.optim.SGD(m1.parameters(), lr=0.0)     # lr 0: grads only
+    m2 = ertdiff.ConditionalUNet.from_config("U1", seed=5).to(cuda_dev)
+    opt2 = torch.optim.Adam(m2.parameters(), lr=1e-3)
+    ertdiff.train_step(m2, opt2, x0, cond, T, ab, t=t, noise=noise)   # U-Net dispatch
+    xn = ertdiff.q_sample(x0, t, noise, ab).requires_grad_(True)
+    pred = m1(xn, t, cond)
+    assert pred.grad_fn is not None
+    loss = F.mse_loss(pred, noise)
+    opt.zero_grad()
+    loss.backward()
+    # (dL/dpred comes from torch's mse_loss backward on one side and ertd_mse_loss
+    # on the other: equal up to the rounding of 2 (e - z) / n)
+    for (k, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert _rel(p1.grad, p2.grad) < 1e-6, k
+    W = {k: v.detach().cpu().double() for k, v in m1.named_parameters()}
+    xr = xn.detach().cpu().double().requires_grad_(True)
+    F.mse_loss(U.forward(xr, t.cpu(), cond.cpu().double(), W, cfg), noise.cpu().double()).backward()
+    err = _rel(xn.grad, xr.grad)
+    record_error("unet_autograd_dx_U1", err)
+    assert err < GRAD_TOL, err
+
+
+@pytest.mark.parametrize("Ca,Cb,HW,groups,act,acc", [
+    (64, 0, 4096, 32, 1, 0),
+    (128, 64, 1024, 32, 1, 1),     # concat input, accumulate into dx
+    (128, 0, 256, 1, 1, 0),        # one group of 128 channels (> 64 per LDS batch)
+    (96, 32, 64, 2, 2, 1),         # GN without SiLU (attention norm)
+])
+def test_gn_act_backward_vs_autograd(Ca, Cb, HW, groups, act, acc, cuda_dev):
+    from ertdiff import _lib
+    g = torch.Generator().manual_seed(HW + Ca + groups)
+    B, C = 3, Ca + Cb
+    x = (torch.randn(B, C, HW, generator=g) * 1.7 + 0.3).double()
+    gamma = (1 + 0.2 * torch.randn(C, generator=g)).double()
+    beta = (0.1 * torch.randn(C, generator=g)).double()
+    dy = torch.randn(B, C, HW, generator=g).double()
+    prev = torch.randn(B, C, HW, generator=g)
+    xr, gr, br = (t.clone().requires_grad_(True) for t in (x, gamma, beta))
+    y = F.group_norm(xr.view(B, C, HW, 1), groups, gr, br, eps=1e-5).view(B, C, HW)
+    if act == 1:
+        y = F.silu(y)
+    (y * dy).sum().backward()
+    lib = _lib.lib()
+    dev = cuda_dev
+    xa = x[:, :Ca].float().contiguous().to(dev)
+    xb = x[:, Ca:].float().contiguous().to(dev) if Cb else None
+    gam, bet = gamma.float().to(dev), beta.float().to(dev)
+    ss = torch.empty(B, C, 2, device=dev)
+    mr = torch.empty(B, groups, 2, device=dev)
+    s = _lib.stream_of(dev)
+    assert lib.ertd_gn_stats_mr(xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(), Cb, B, HW,
+                                groups, gam.data_ptr(), bet.data_ptr(), ss.data_ptr(), mr.data_ptr(),
+                                s) == 0
+    dxa = prev[:, :Ca].contiguous().to(dev)
+    dxb = prev[:, Ca:].contiguous().to(dev) if Cb else None
+    part = torch.empty(B, 2, C, device=dev)
+    dyd = dy.float().to(dev)
+    assert lib.ertd_gn_act_backward(xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(), Cb, B, HW,
+                                    groups, gam.data_ptr(), bet.data_ptr(), mr.data_ptr(), act,
+                                    dyd.data_ptr(), dxa.data_ptr(),
+                                    None if dxb is None else dxb.data_ptr(), acc, part.data_ptr(),
+                                    s) == 0
+    dgb = torch.empty(2, C, device=dev)
+    assert lib.ertd_reduce_rows(part.data_ptr(), B, 2 * C, dgb.data_ptr(), 0, s) == 0
+    dx = dxa if dxb is None else torch.cat([dxa, dxb], 1)
+    want = xr.grad + (prev.double() if acc else 0)
+    e = [_rel(dx, want), _rel(dgb[0], gr.grad), _rel(dgb[1], br.grad)]
+    record_error(f"gn_act_backward_{C}_{HW}_g{groups}_a{act}", max(e))
+    assert max(e) < 1e-5, e
