@@ -92,6 +92,8 @@ def parse():
     ap.add_argument("--no-hoisted", action="store_true", help="skip the secondary hoisted timing")
     ap.add_argument("--no-train", action="store_true", help="skip the secondary train-step timing")
     ap.add_argument("--no-unet-train", action="store_true", help="skip the U-Net train-step timing")
+    ap.add_argument("--no-hbm-kernels", action="store_true",
+                    help="skip the per-kernel GB/s of the HBM-bound U-Net kernels")
     ap.add_argument("--unet-train-steps", type=int, default=5)
     ap.add_argument("--no-strip-roofline", action="store_true")
     ap.add_argument("--no-steps-schedule", action="store_true",
@@ -273,6 +275,83 @@ def train_bench(dev, steps=200, B=32, T=500):
     el = time.perf_counter() - t0
     return {"train_steps_per_s": round(steps / el, 1), "train_batch": B,
             "train_ms_per_step": round(el / steps * 1e3, 4), "train_final_loss": round(float(loss), 5)}
+
+
+def _time_op(fn, reps, dev):
+    """Average µs of fn() (kernel launches on the current stream), HIP events."""
+    stream = torch.cuda.current_stream(dev)
+    fn()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def bench_hbm_kernels(dev, reps=50):
+    """HBM-bound U-Net kernels alone at their bench shapes, each through its
+    C-ABI entry: algorithmic bytes (every input read once, every output
+    written once) / HIP-event duration, against 8 TB/s."""
+    lib = _lib.lib()
+    s = _lib.stream_of(dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    out = {}
+
+    def rec(name, workload, nbytes, us):
+        gbs = nbytes / (us * 1e-6) / 1e9
+        out[name] = {"workload": workload, "algorithmic_bytes": int(nbytes), "avg_us": round(us, 2),
+                     "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(gbs / PEAK_HBM_GBS, 4)}
+
+    # gn_stats_kernel: U2 B=64, 64 channels at 64x64 (the headline's widest activations)
+    B, C, H = 64, 64, 64
+    x = torch.randn(B, C, H, H, device=dev, generator=g)
+    gam, bet = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    ss = torch.empty(B, C, 2, device=dev)
+    us = _time_op(lambda: _lib.check(lib.ertd_group_norm_stats(
+        x.data_ptr(), C, None, 0, B, H * H, 32, gam.data_ptr(), bet.data_ptr(), ss.data_ptr(), s),
+        "gn_stats"), reps, dev)
+    rec("gn_stats_kernel", "U2 B=64, 64 ch, 64x64, 32 groups", x.numel() * 4 + ss.numel() * 4, us)
+    # unet_update_kernel: U2 B=64, P=4096, Philox noise
+    P_ = H * H
+    xs = torch.randn(B, P_, device=dev, generator=g)
+    eps = torch.randn(B, P_, device=dev, generator=g)
+    tab = torch.full((1000,), 0.5, device=dev)
+    tdev = torch.tensor([500], dtype=torch.int32, device=dev)
+    us = _time_op(lambda: _lib.check(lib.ertd_unet_update(
+        xs.data_ptr(), eps.data_ptr(), tab.data_ptr(), tab.data_ptr(), tab.data_ptr(), None, 0,
+        tdev.data_ptr(), 7, 0, B, P_, s), "unet_update"), reps, dev)
+    rec("unet_update_kernel", "U2 B=64, P=4096, Philox noise (x, eps read; x written)",
+        3 * xs.numel() * 4, us)
+    del x, ss, xs, eps
+    # gn_act_bf16_kernel: U3 configs[2] B=256, 64 channels at 64x64 -> stats + bf16 image
+    B = 256
+    x = torch.randn(B, C, H, H, device=dev, generator=g)
+    ss = torch.empty(B, C, 2, device=dev)
+    img = torch.empty(B * ((C + 15) // 16) * H * H * 16, dtype=torch.int16, device=dev)
+    us = _time_op(lambda: _lib.check(lib.ertd_group_norm_act_bf16(
+        x.data_ptr(), C, None, 0, B, H, 32, gam.data_ptr(), bet.data_ptr(), ss.data_ptr(),
+        img.data_ptr(), 1, s), "gn_act_bf16"), reps, dev)
+    rec("gn_act_bf16_kernel", "U3 B=256, 64 ch, 64x64: stats + GN + SiLU + bf16 image",
+        x.numel() * 4 + img.numel() * 2 + ss.numel() * 4, us)
+    del x, img, ss
+    # act_bf16_kernel: U3 B=256, the 192-channel 64x64 concat input (outside the fused plan)
+    Ca, Cb = 128, 64
+    xa = torch.randn(B, Ca, H, H, device=dev, generator=g)
+    xb = torch.randn(B, Cb, H, H, device=dev, generator=g)
+    ss = torch.randn(B, Ca + Cb, 2, device=dev, generator=g)
+    img = torch.empty(B * ((Ca + Cb + 15) // 16) * H * H * 16, dtype=torch.int16, device=dev)
+    us = _time_op(lambda: _lib.check(lib.ertd_act_bf16(
+        xa.data_ptr(), Ca, xb.data_ptr(), Cb, B, H, ss.data_ptr(), 1, 0, img.data_ptr(), s),
+        "act_bf16"), reps, dev)
+    rec("act_bf16_kernel", "U3 B=256, 128+64 ch concat, 64x64: GN + SiLU + bf16 image",
+        (xa.numel() + xb.numel()) * 4 + img.numel() * 2 + ss.numel() * 4, us)
+    del xa, xb, img, ss
+    torch.cuda.empty_cache()
+    return out
 
 
 def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000):
@@ -673,6 +752,8 @@ def main():
                                                     world, dev)
     if not a.no_u5:
         extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev)
+    if not a.no_hbm_kernels:
+        extra["hbm_kernels"] = bench_hbm_kernels(dev)
     if not a.no_unet_train and world == 1:
         extra["unet_train"] = bench_unet_train(dev, steps=a.unet_train_steps)
     if not a.no_kde:

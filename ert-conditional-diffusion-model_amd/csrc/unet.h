@@ -50,6 +50,7 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
 // launch_pack_conv_bf16
 hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
 size_t conv_packed_floats_bf16(int cin, int cout, int ks);
+hipError_t launch_act_bf16(const ConvArgs& a, int act, bool up, int B, hipStream_t s);
 size_t conv_bf16_image_bytes(int cin, int B, int H, int W);
 hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, float* dst,
                                  hipStream_t s);

@@ -675,6 +675,33 @@ int ertd_group_norm_act_bf16(const float* x, int Ca, const float* x2, int Cb, in
   return rcode(launch_gn_act_bf16(g, silu != 0, img, B, (hipStream_t)stream));
 }
 
+int ertd_act_bf16(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* ss,
+                  int act, int up, void* img, void* stream) {
+  if (!x || !img || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) || H < 1 ||
+      act < ACT_NONE || act > ACT_GN || (act != ACT_NONE && !ss) || (up && act != ACT_NONE))
+    return ERTD_EINVAL;
+  ConvArgs a{};
+  a.srcA = x;
+  a.srcB = x2;
+  a.Ca = Ca;
+  a.Cb = Cb;
+  a.Cin = Ca + Cb;
+  a.gn = (const float2*)ss;
+  a.Hs = a.Ws = H;
+  a.Ho = a.Wo = up ? 2 * H : H;
+  a.bimg = img;
+  return rcode(launch_act_bf16(a, act, up != 0, B, (hipStream_t)stream));
+}
+
+int ertd_unet_update(float* x, const float* eps, const float* c1, const float* c2,
+                     const float* sigma, const float* noise, int num_steps, const int* t_dev,
+                     uint64_t seed, uint32_t member_offset, int B, int P, void* stream) {
+  if (!x || !eps || !c1 || !c2 || !sigma || !t_dev || B < 1 || P < 1 || (noise && num_steps < 1))
+    return ERTD_EINVAL;
+  UpdateArgs u{x, eps, c1, c2, sigma, noise, num_steps, t_dev, seed, member_offset, P};
+  return rcode(launch_unet_update(u, B, (hipStream_t)stream));
+}
+
 int ertd_attention(const float* qkv, int B, int C, int N, float* out, void* stream) {
   if (!qkv || !out || B < 1 || N != 256 || C < 2 || C % 256) return ERTD_EINVAL;
   return rcode(launch_attention(qkv, C, N, out, nullptr, B, (hipStream_t)stream));

@@ -602,6 +602,19 @@ static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
   }
 }
 
+// the standalone image transform (act(GN(x)) or the nearest-x2 upsample of x
+// -> the [B][C/16][H][W][16] bf16 image): ertd_act_bf16 (bench per-kernel GB/s)
+hipError_t launch_act_bf16(const ConvArgs& a, int act, bool up, int B, hipStream_t s) {
+  const int HW = a.Wo * a.Wo, G16 = (a.Cin + 15) / 16;
+  const long long n = (long long)B * G16 * HW;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (up) act_bf16_kernel<ACT_NONE, true><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else if (act == ACT_GN_SILU) act_bf16_kernel<ACT_GN_SILU><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else if (act == ACT_GN) act_bf16_kernel<ACT_GN><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else act_bf16_kernel<ACT_NONE><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  return hipGetLastError();
+}
+
 hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);

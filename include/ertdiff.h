@@ -259,6 +259,18 @@ int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B
                           int groups, const float* gamma, const float* beta, float* out,
                           void* stream);
 int ertd_attention(const float* qkv, int B, int C, int N, float* out, void* stream);
+/* ertd_act_bf16: img [B][ceil(C/16)][Ho][Ho][16] bf16 (RNE) of act(cat(x, x2)*ss.x + ss.y)
+ *   (act 0 none / 1 GN+SiLU / 2 GN; ss (B, C, 2) as ertd_group_norm_stats) or, with up = 1
+ *   (act 0), of the nearest-x2 upsample of cat(x, x2) (Ho = 2H): the bf16 path's standalone
+ *   image transform (act_bf16_kernel).
+ * ertd_unet_update: the U-Net sampler's DDPM update (sample_model :111-118) of x (B, P) given
+ *   eps, per-step tables c1/c2/sigma (index t = *t_dev) and injected noise
+ *   (num_steps, B, P) or Philox (noise = null; seed, member ids from member_offset). */
+int ertd_act_bf16(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* ss,
+                  int act, int up, void* img, void* stream);
+int ertd_unet_update(float* x, const float* eps, const float* c1, const float* c2,
+                     const float* sigma, const float* noise, int num_steps, const int* t_dev,
+                     uint64_t seed, uint32_t member_offset, int B, int P, void* stream);
 /* ertd_group_norm_act_bf16: the bf16 path's fused prologue of a 3x3 GN conv
  *   in one pass -- out as ertd_group_norm_stats, and img = bf16 RNE of
  *   act(GroupNorm(cat(x, x2))) (act: silu=1 SiLU, 0 none) in the conv's

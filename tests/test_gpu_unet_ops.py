@@ -191,3 +191,38 @@ def test_attention(cuda_dev):
     a = torch.softmax(torch.einsum("bci,bcj->bij", q, k) / 16.0, dim=-1)
     ref = torch.einsum("bij,bcj->bci", a, v)
     assert RN.rel_l2(out.double().numpy(), ref.double().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("Ca,Cb,H,act,up", [(128, 64, 16, 1, 0), (64, 0, 32, 2, 0), (48, 16, 16, 0, 1)])
+def test_act_bf16_image(Ca, Cb, H, act, up, cuda_dev):
+    """ertd_act_bf16 (the bf16 path's standalone image transform): RNE bf16 of
+    act(x*scale+shift) (or of the nearest-x2 upsample) in [B][C/16][Ho][Ho][16]
+    records; every element within 1 bf16 ulp of torch's, >= 99 % bit-equal."""
+    from ertdiff import _lib
+    B, C = 2, Ca + Cb
+    x = _rand((B, Ca, H, H), 31, 2.0)
+    x2 = _rand((B, Cb, H, H), 32) if Cb else None
+    ss = torch.stack([_rand((B, C), 33) + 1, _rand((B, C), 34)], -1)
+    Ho = 2 * H if up else H
+    img = torch.empty(B, C // 16, Ho, Ho, 16, dtype=torch.int16, device=cuda_dev)
+    dx, dss = x.to(cuda_dev), ss.to(cuda_dev)
+    dx2 = None if x2 is None else x2.to(cuda_dev)
+    rc = _lib.lib().ertd_act_bf16(dx.data_ptr(), Ca, None if dx2 is None else dx2.data_ptr(), Cb, B, H,
+                                  dss.data_ptr() if act else None, act, up, img.data_ptr(),
+                                  _lib.stream_of(cuda_dev))
+    assert rc == 0
+    xin = x if x2 is None else torch.cat([x, x2], 1)
+    if up:
+        y = F.interpolate(xin, scale_factor=2, mode="nearest")
+    else:
+        y = (xin.double() * ss[..., 0][:, :, None, None].double()
+             + ss[..., 1][:, :, None, None].double()).float()
+        if act == 1:
+            y = F.silu(y)
+    ref = y.to(torch.bfloat16).view(torch.int16).reshape(B, C // 16, 16, Ho, Ho).permute(0, 1, 3, 4, 2)
+    got = img.cpu()
+    ref = ref.contiguous()
+    assert (got == ref).float().mean().item() >= 0.99
+    got_f, ref_f = got.view(torch.bfloat16).float(), ref.view(torch.bfloat16).float()
+    ulp = (ref_f.abs() * 2.0 ** -7).clamp_min(1e-6)
+    assert bool(((got_f - ref_f).abs() <= ulp).all())
