@@ -616,12 +616,20 @@ def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev):
     step_s = el / steps
     conv_tf = fl["conv"] * B / step_s / 1e12
     peak = PEAK_FP32_TFLOPS if precision == "fp32" else PEAK_BF16_TFLOPS
-    return {"config": f"{name} B={B} per GPU, {precision}, T={T}", "value": round(world * steps / el, 3),
+    out = {"config": f"{name} B={B} per GPU, {precision}, T={T}", "value": round(world * steps / el, 3),
             "unit": "denoising-steps/sec", "scaling": "weak", "ms_per_step": round(step_s * 1e3, 4),
             "conv_tflops": round(conv_tf, 2), "conv_peak_tflops": peak,
             "conv_frac": round(conv_tf / peak, 4), "steps": steps, "warmup": warmup,
             "member_steps_per_s": round(world * steps / el * B, 1),
-            "gflop_per_sample_step": round(fl["total"] / 1e9, 3)}
+            "gflop_per_sample_step": round(fl["total"] / 1e9, 3),
+            "hbm_bytes_per_step": _traffic(f"unet_{name}_B{B}_{precision}_step"),
+            "hbm_basis": "PMC FETCH_SIZE/WRITE_SIZE passes (tools/unet_traffic.sh, "
+                         "profiles/kernel_traffic.json), every ertd::unet:: dispatch per step"}
+    tr = out["hbm_bytes_per_step"]
+    if tr:
+        out["hbm_gbs_step_avg"] = round(tr / step_s / 1e9, 1)
+        out["hbm_frac_step_avg"] = round(tr / step_s / 1e9 / PEAK_HBM_GBS, 4)
+    return out
 
 
 def bench_ensemble(n_members, name, steps, warmup, T, rank, world, dev):
@@ -720,7 +728,7 @@ def main():
     step_s = el / a.steps
     conv_flop_step = flops["conv"] * B
     achieved = conv_flop_step / (ev_s / a.steps) / 1e12
-    traffic = _traffic(f"unet_{a.unet}_B{B}_step")
+    traffic = _traffic(f"unet_{a.unet}_B{B}_fp32_step")
     ex_flop_step = flops["conv_executed_fp32"] * B
     ex_tf = ex_flop_step / (ev_s / a.steps) / 1e12
     roof = {"kernel": "conv_wino_kernel (ResBlock 3x3, Winograd F(2x2,3x3)) + conv_kernel (the other "

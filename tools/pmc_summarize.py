@@ -54,7 +54,7 @@ if unet_steps > 0:
             "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), summed over "
                       "every ertd::unet:: dispatch / steps; bytes = 2*FETCH_SIZE*1024 + "
                       "WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
-            "workload": "bench.py U2, B=64, L=4693 (steps incl. warmup)",
+            "workload": os.environ.get("UNET_WORKLOAD", "bench.py U2, B=64, L=4693 (steps incl. warmup)"),
         }
         print(unet_key, json.dumps(rec[unet_key]))
     else:

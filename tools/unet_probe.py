@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--L", type=int, default=4693)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
+    torch.set_grad_enabled(False)   # inference forward (not the autograd train-mode path)
     dev = torch.device("cuda", 0)
     m = ertdiff.ConditionalUNet.from_config(a.config, seed=0, precision=a.precision).to(dev).eval()
     cond = torch.rand(a.B, 14, a.L, device=dev)
