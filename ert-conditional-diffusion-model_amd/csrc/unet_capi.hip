@@ -843,9 +843,14 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
     return r;
   }
   hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
-  // ERTD_UNET_SIDE=0 keeps the step graph a single chain (A/B)
+  // The forked skip-conv branch pays only where the convs leave CUs free: the
+  // fp32 Winograd kernel is persistent (one workgroup on every CU), so the side
+  // branch's convs queue behind it and slow it (U2 B=64: 154.9 steps/s single
+  // chain vs 152.6 forked); the bf16 path keeps it (U3 B=256: 94.0 vs 93.1).
+  // ERTD_UNET_SIDE=0/1 overrides (A/B).
   const char* sv = getenv("ERTD_UNET_SIDE");
-  if (e == hipSuccess && (!sv || atoi(sv) != 0)) {
+  const bool side = sv ? atoi(sv) != 0 : c->precision == ERTD_PREC_BF16;
+  if (e == hipSuccess && side) {
     e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evf, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evj, hipEventDisableTiming);

@@ -309,12 +309,14 @@ int ertd_unet_sample(const ertd_unet_config* cfg, const float* packed, const flo
                      uint64_t seed, uint32_t member_offset, float* x_inout, void* ws,
                      size_t ws_bytes, void* stream);
 /* The same call as a plan: the head and one step are captured as hipGraphs
- * once; a launch replays head + n_run x step on `stream`.  The step graph is
- * not a single chain: the embedding dense layers and each ResBlock's 1x1
- * skip conv are captured on a plan-owned side stream (event fork/join), so
- * they run beside conv_in / conv1; results equal the eager call bit for bit.
- * The plan owns its capture streams and events (ertd_unet_plan_destroy frees
- * them); ERTD_UNET_SIDE=0 in the environment captures one chain instead.   */
+ * once; a launch replays head + n_run x step on `stream`.  For bf16
+ * precision the step graph is not a single chain: the embedding dense layers
+ * and each ResBlock's 1x1 skip conv are captured on a plan-owned side stream
+ * (event fork/join), so they run beside conv_in / conv1 (fp32 captures one
+ * chain: its persistent Winograd convs occupy every CU); results equal the
+ * eager call bit for bit either way.  The plan owns its capture streams and
+ * events (ertd_unet_plan_destroy frees them); ERTD_UNET_SIDE=0/1 in the
+ * environment forces one chain / the forked graph.                          */
 typedef struct ertd_unet_plan ertd_unet_plan;
 int ertd_unet_sample_plan_create(const ertd_unet_config* cfg, const float* packed, const float* cond,
                                  long long cond_stride, int L, int B, int num_steps, int t_first,
