@@ -21,8 +21,6 @@ namespace unet {
 
 namespace {
 
-constexpr int OCC = 16;  // input channels per staged chunk
-
 __device__ __forceinline__ float round_bf16(float v) {  // RNE, finite v
   const uint32_t u = __float_as_uint(v);
   return __uint_as_float(((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16) << 16);
@@ -41,18 +39,26 @@ __device__ __forceinline__ float packed_w_bf16(const float* w, int ci, int tap) 
   return __uint_as_float((unsigned)v << 16);
 }
 
-template <int WO>
+// Thread = 4 horizontally adjacent output pixels of one row; a workgroup owns
+// ROWS whole rows (the whole image at W <= 32).  Staged rows: W + 8 floats,
+// data at column 4 (16-B aligned float4 stores / loads), zero columns 3 and
+// W + 4; the 3 taps of a kernel row read one float4 + two neighbours.
+template <int WO, int RWS>
 struct OutGeom {
-  static constexpr int ROWS = NTHR / WO;  // output rows per workgroup (one pixel per thread)
+  static constexpr int TPR = WO / 4;                          // threads per output row
+  static constexpr int ROWS = RWS;
+  static constexpr int NT = TPR * ROWS;                       // threads per workgroup
   static constexpr int IR = ROWS + 2;
-  static constexpr int IP = WO + 2;       // zero column each side
+  static constexpr int IP = WO + 8;
   static constexpr int CSZ = IR * IP;
-  static_assert(NTHR % WO == 0, "whole output rows per workgroup");
+  static constexpr int OCC = 8;                               // channels per staged chunk
+  static_assert(WO % ROWS == 0 && NT <= 256 && NT % 64 == 0, "whole output rows per workgroup");
 };
 
-template <int ACT, int WO, bool BF>
-__global__ __launch_bounds__(NTHR) void conv_out_kernel(ConvArgs a) {
-  using G = OutGeom<WO>;
+template <int ACT, int WO, int RWS, bool BF>
+__global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
+  using G = OutGeom<WO, RWS>;
+  constexpr int OCC = G::OCC;
   extern __shared__ __attribute__((aligned(16))) float smo[];
   const int Cin = a.Cin, Ca = a.Ca;
   float* img = smo;                                   // [OCC][IR][IP]
@@ -62,85 +68,120 @@ __global__ __launch_bounds__(NTHR) void conv_out_kernel(ConvArgs a) {
   const int oy0 = blockIdx.x * G::ROWS;
   constexpr size_t plane = (size_t)WO * WO;
 
-  for (int i = tid; i < Cin * 9; i += NTHR) {
+  for (int i = tid; i < Cin * 9; i += G::NT) {
     const int ci = i / 9, tap = i - ci * 9;
     wl[i] = BF ? packed_w_bf16(a.wpk, ci, tap) : packed_w_f32(a.wpk, ci, tap);
   }
   if constexpr (ACT != ACT_NONE) {
-    for (int c = tid; c < Cin; c += NTHR) gtab[c] = a.gn[(size_t)b * Cin + c];
+    for (int c = tid; c < Cin; c += G::NT) gtab[c] = a.gn[(size_t)b * Cin + c];
   }
-  for (int r = tid; r < OCC * G::IR; r += NTHR) {
-    img[r * G::IP] = 0.f;
-    img[r * G::IP + G::IP - 1] = 0.f;
+  for (int r = tid; r < OCC * G::IR; r += G::NT) {
+    img[r * G::IP + 3] = 0.f;
+    img[r * G::IP + 4 + WO] = 0.f;
   }
 
-  const int py = tid / WO, px = tid - py * WO;
-  float acc = 0.f;
+  const int py = tid / G::TPR, px4 = tid - py * G::TPR;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int c0 = 0; c0 < Cin; c0 += OCC) {
     __syncthreads();  // tables visible / previous chunk consumed
-    constexpr int NE = (OCC * G::IR * WO + NTHR - 1) / NTHR;   // staged elements per thread
-#pragma unroll
-    for (int k = 0; k < NE; ++k) {
-      const int e = tid + k * NTHR;
-      if (OCC * G::IR * WO % NTHR != 0 && e >= OCC * G::IR * WO) break;
-      const int c = e / (G::IR * WO), rem = e - c * (G::IR * WO);
-      const int r = rem / WO, x = rem - r * WO;
+    constexpr int NQ = OCC * G::IR * G::TPR;                   // float4 quads to stage
+    for (int e = tid; e < NQ; e += G::NT) {
+      const int c = e / (G::IR * G::TPR), rem = e - c * (G::IR * G::TPR);
+      const int r = rem / G::TPR, q = rem - r * G::TPR;
       const int cg = c0 + c, iy = oy0 - 1 + r;
-      float v = 0.f;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (cg < Cin && iy >= 0 && iy < WO) {
         const float* src = cg < Ca ? a.srcA + ((size_t)b * Ca + cg) * plane
                                    : a.srcB + ((size_t)b * a.Cb + (cg - Ca)) * plane;
-        v = src[iy * WO + x];
+        v = *reinterpret_cast<const float4*>(src + iy * WO + 4 * q);
         if constexpr (ACT != ACT_NONE) {
           const float2 g = gtab[cg];
-          v = fmaf(v, g.x, g.y);
-          if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+          v.x = fmaf(v.x, g.x, g.y);
+          v.y = fmaf(v.y, g.x, g.y);
+          v.z = fmaf(v.z, g.x, g.y);
+          v.w = fmaf(v.w, g.x, g.y);
+          if constexpr (ACT == ACT_GN_SILU) {
+            v.x = v.x * __builtin_amdgcn_rcpf(1.0f + __expf(-v.x));
+            v.y = v.y * __builtin_amdgcn_rcpf(1.0f + __expf(-v.y));
+            v.z = v.z * __builtin_amdgcn_rcpf(1.0f + __expf(-v.z));
+            v.w = v.w * __builtin_amdgcn_rcpf(1.0f + __expf(-v.w));
+          }
         }
-        if constexpr (BF) v = round_bf16(v);
+        if constexpr (BF) {
+          v.x = round_bf16(v.x);
+          v.y = round_bf16(v.y);
+          v.z = round_bf16(v.z);
+          v.w = round_bf16(v.w);
+        }
       }
-      img[(c * G::IR + r) * G::IP + x + 1] = v;
+      *reinterpret_cast<float4*>(img + (c * G::IR + r) * G::IP + 4 + 4 * q) = v;
     }
     __syncthreads();
     const int nc = Cin - c0 < OCC ? Cin - c0 : OCC;
     for (int c = 0; c < nc; ++c) {
-      const float* ip = img + (c * G::IR + py) * G::IP + px;
       const float* wp = wl + (c0 + c) * 9;
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) acc = fmaf(wp[ky * 3 + kx], ip[ky * G::IP + kx], acc);
+      for (int ky = 0; ky < 3; ++ky) {
+        const float* row = img + (c * G::IR + py + ky) * G::IP + 4 + 4 * px4;
+        const float4 m = *reinterpret_cast<const float4*>(row);
+        const float l = row[-1], rr = row[4];
+        const float w0 = wp[ky * 3], w1 = wp[ky * 3 + 1], w2 = wp[ky * 3 + 2];
+        // per output pixel the taps in the MFMA kernels' order (ky, kx)
+        acc[0] = fmaf(w0, l, acc[0]);   acc[0] = fmaf(w1, m.x, acc[0]); acc[0] = fmaf(w2, m.y, acc[0]);
+        acc[1] = fmaf(w0, m.x, acc[1]); acc[1] = fmaf(w1, m.y, acc[1]); acc[1] = fmaf(w2, m.z, acc[1]);
+        acc[2] = fmaf(w0, m.y, acc[2]); acc[2] = fmaf(w1, m.z, acc[2]); acc[2] = fmaf(w2, m.w, acc[2]);
+        acc[3] = fmaf(w0, m.z, acc[3]); acc[3] = fmaf(w1, m.w, acc[3]); acc[3] = fmaf(w2, rr, acc[3]);
+      }
     }
   }
 
   // epilogue in the MFMA kernels' op order: conv + bias, + emb, + residual
-  const size_t o = (size_t)b * plane + (size_t)(oy0 + py) * WO + px;
-  float v = acc + a.bias[0];
-  if (a.ebias) v = v + a.ebias[(size_t)b * a.eb_stride];
-  if (a.res) v = v + a.res[o];
-  a.out[o] = v;
+  const size_t o = (size_t)b * plane + (size_t)(oy0 + py) * WO + 4 * px4;
+  float4 v = make_float4(acc[0] + a.bias[0], acc[1] + a.bias[0], acc[2] + a.bias[0], acc[3] + a.bias[0]);
+  if (a.ebias) {
+    const float e = a.ebias[(size_t)b * a.eb_stride];
+    v.x = v.x + e; v.y = v.y + e; v.z = v.z + e; v.w = v.w + e;
+  }
+  if (a.res) {
+    const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+    v.x = v.x + r.x; v.y = v.y + r.y; v.z = v.z + r.z; v.w = v.w + r.w;
+  }
+  *reinterpret_cast<float4*>(a.out + o) = v;
 }
 
-template <int ACT, int WO, bool BF>
+template <int ACT, int WO, int RWS, bool BF>
 hipError_t launch_co(const ConvArgs& a, int B, hipStream_t s) {
-  using G = OutGeom<WO>;
-  const size_t lds = ((size_t)OCC * G::CSZ + (((size_t)a.Cin * 9 + 1) & ~(size_t)1)) * sizeof(float) +
+  using G = OutGeom<WO, RWS>;
+  const size_t lds = ((size_t)G::OCC * G::CSZ + (((size_t)a.Cin * 9 + 1) & ~(size_t)1)) * sizeof(float) +
                      (size_t)a.Cin * sizeof(float2);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)conv_out_kernel<ACT, WO, BF>,
+    (void)hipFuncSetAttribute((const void*)conv_out_kernel<ACT, WO, RWS, BF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((unsigned)(WO / G::ROWS), 1u, (unsigned)B);
-  conv_out_kernel<ACT, WO, BF><<<grid, NTHR, lds, s>>>(a);
+  conv_out_kernel<ACT, WO, RWS, BF><<<grid, G::NT, lds, s>>>(a);
   return hipGetLastError();
+}
+
+// rows per workgroup: 256 threads (16 rows; 8 at W = 128; the whole image at
+// W = 16).  Measured on a U2 B=64 step (64x64): 16 rows (256 workgroups)
+// 60.5 us, 4 rows (1024 one-wave workgroups) 70.5 us -- per-workgroup weight
+// gathers and the halo re-reads cost more than the lost occupancy; U3 B=256:
+// 163 us (the one-pixel-per-thread kernel before: 244 us).
+template <int ACT, int WO, bool BF>
+hipError_t launch_co_r(const ConvArgs& a, int B, hipStream_t s) {
+  constexpr int TPR = WO / 4;
+  constexpr int R = (256 / TPR) < WO ? (256 / TPR) : WO;
+  return launch_co<ACT, WO, R, BF>(a, B, s);
 }
 
 template <int ACT, bool BF>
 hipError_t launch_co_w(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
-    case 16: return launch_co<ACT, 16, BF>(a, B, s);
-    case 32: return launch_co<ACT, 32, BF>(a, B, s);
-    case 64: return launch_co<ACT, 64, BF>(a, B, s);
-    case 128: return launch_co<ACT, 128, BF>(a, B, s);
+    case 16: return launch_co_r<ACT, 16, BF>(a, B, s);
+    case 32: return launch_co_r<ACT, 32, BF>(a, B, s);
+    case 64: return launch_co_r<ACT, 64, BF>(a, B, s);
+    case 128: return launch_co_r<ACT, 128, BF>(a, B, s);
     default: return hipErrorInvalidValue;
   }
 }

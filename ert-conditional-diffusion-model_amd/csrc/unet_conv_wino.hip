@@ -58,6 +58,7 @@ constexpr int WSP = WKC / 4;                  // MFMA step pairs per chunk
 constexpr int U_FL = 16 * 2 * WSP * 128;      // U floats per chunk buffer (8192)
 constexpr int V_FL = 16 * WSP * 2 * 128;      // V floats per chunk buffer (8192)
 constexpr int NUB = 3;                        // U ring depth (DMA two chunks ahead)
+constexpr int NRS = 3;                        // producer register sets (loads NRS+1 chunks ahead)
 constexpr size_t WLDS = (size_t)(NUB * U_FL + 2 * V_FL) * sizeof(float);   // 160 KB
 constexpr int XIF = WKC * 64;                 // U / V floats per xi (512)
 using f32x4 = __attribute__((ext_vector_type(4))) float;
@@ -124,9 +125,9 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
     // tile's middle columns; the outer columns are the neighbouring tiles'
     // (lanes t-1 / t+1) by DPP wave shifts -- across a tile-row boundary they
     // are padding (masked), so the shifted-in neighbour never matters there.
-    float2 raw[2][2][4];   // [register set][channel][row]
-    float2 gnv[2][2];
-    unsigned msk[2] = {0u, 0u};   // bits 0-3: row r valid, bit 4: left column, bit 5: right column
+    float2 raw[NRS][2][4];   // [register set][channel][row]
+    float2 gnv[NRS][2];
+    unsigned msk[NRS] = {};   // bits 0-3: row r valid, bit 4: left column, bit 5: right column
     auto load_chunk = [&](const int set, int g) {
       const int il = g / nchunk, k = g - il * nchunk;
       const Item itm = item_of(bid + il * G, ncog, NTBLK);
@@ -221,40 +222,45 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
       }
     };
 
-    // Two register sets (chunk c in set c & 1), loads three chunks ahead of
-    // the MFMAs: in the slot of chunk g the producers transform chunk g+1
-    // (loaded two slots earlier -- the compiler's own vmcnt waits, which count
-    // only these loads) into V[(g+1) & 1] and issue chunk g+3's loads.
-    // Loads past the last chunk re-load the last one (clamped, unused): the
-    // steady-state loop then has no conditional loads, and the compiler's
-    // vmcnt bookkeeping across its back edge stays exact (a transform waits
-    // only for its own set, not for the loads issued one slot earlier).
+    // NRS = 3 register sets (chunk c in set c % 3), loads four chunks ahead
+    // of the MFMAs: in the slot of chunk g the producers transform chunk g+1
+    // (loaded three slots earlier -- the compiler's own vmcnt waits, which
+    // count only these loads) into V[(g+1) & 1] and issue chunk g+4's loads
+    // into the set just freed.  (With two sets, loads three chunks ahead, the
+    // producers waited on their loads: the layer ran as long as the producers
+    // alone.)  Loads past the last chunk re-load the last one (clamped,
+    // unused): the steady-state loop has no conditional loads, and the
+    // compiler's vmcnt bookkeeping across its back edge stays exact.
     const int glast = gtot - 1;
     auto clampg = [&](int g) { return g < glast ? g : glast; };
+    auto slot = [&](const int set, int g) {   // set = (g + 1) % NRS
+      transform_chunk(set, vbuf + ((g + 1) & 1) * V_FL);
+      load_chunk(set, clampg(g + 1 + NRS));
+      __syncthreads();   // (B) end of slot g
+    };
     if (gtot > 0) {
       load_chunk(0, 0);
       load_chunk(1, clampg(1));
+      load_chunk(2, clampg(2));
       transform_chunk(0, vbuf);
-      load_chunk(0, clampg(2));
+      load_chunk(0, clampg(3));
     }
     __syncthreads();   // (A) chunk 0 staged
     int g = 0;
-    for (; g + 1 < gtot; g += 2) {
-      transform_chunk(1, vbuf + V_FL);          // chunk g+1
-      load_chunk(1, clampg(g + 3));
-      __syncthreads();   // (B) end of slot g
-      transform_chunk(0, vbuf);                 // chunk g+2 (unused past the end)
-      load_chunk(0, clampg(g + 4));
-      __syncthreads();   // (B) end of slot g+1
+    for (; g + 2 < gtot; g += 3) {
+      slot(1, g);
+      slot(2, g + 1);
+      slot(0, g + 2);
     }
-    if (g < gtot) __syncthreads();   // (B) end of the last slot (odd chunk count)
+    if (g < gtot) slot(1, g);
+    if (g + 1 < gtot) slot(2, g + 1);
     return;
   }
 
   // =================== MFMA waves ===================
   const int cb = wave & 3, tbp = wave >> 2;
-  const int aoff = cb * 64 + lane;                  // + xi*XIF + s*256
-  const int boff = (2 * tbp) * 64 + lane;           // + xi*XIF + s*256 (+64: second tile block)
+  // operands: U at cb*64 + lane, V at (2 tbp)*64 + lane (+64: second tile
+  // block), + xi*XIF + s*256 (derived per chunk in the K loop)
   f32x4 acc[16][2];
 
   // U slice DMA of chunk g into ring slot g % 3, issued two slots ahead by the
@@ -293,8 +299,14 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
       const int g = il * nchunk + k;
       const bool dma = g + 2 < gtot;
       if (dma) dma_u(g + 2);
-      const float* ub = ubuf + (g % NUB) * U_FL + aoff;
-      const float* vb = vbuf + (g & 1) * V_FL + boff;
+      // the lane-dependent operand offsets are re-derived per chunk from a
+      // fresh lane id (opaque to the compiler): held across the loop they
+      // were spilled to scratch, and the reload's vmcnt(0) waited for the
+      // U DMA just issued for chunk g + 2 -- every chunk
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      const float* ub = ubuf + (g % NUB) * U_FL + cb * 64 + ln;
+      const float* vb = vbuf + (g & 1) * V_FL + (2 * tbp) * 64 + ln;
       // 32 steps (k-step st = s >> 4 of 4 channels, xi = s & 15): operands
       // read 3 steps ahead into a 4-deep register ring, each step's three
       // ds_reads grouped with the two MFMAs of an earlier step (the compiler
