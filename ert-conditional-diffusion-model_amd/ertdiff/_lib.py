@@ -17,7 +17,9 @@ from typing import Optional
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_NAME = "libertdiff_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# ERTD_LIB_PATH: an alternative build of the same library (A/B of kernel variants, tools/)
+LIB_PATH = os.environ.get("ERTD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                           LIB_NAME)
 
 ERTD_OK = 0
 ERTD_EINVAL = -1
