@@ -30,7 +30,7 @@ struct ConvArgs {
   int Ca, Cb;
   const float2* gn;      // (B, Cin) {scale, shift}: GroupNorm(x) = x*scale + shift (ACT_GN*)
   const float* wpk;      // packed weights: [co_tile32][chunk][step pair][64 lanes][2]
-  const float* bias;     // (Cout)
+  const float* bias;     // (Cout), or null (no bias: the training input-gradient convs)
   const float* ebias;    // (B, eb_stride) per-sample per-channel add (offset applied) or null
   int eb_stride;
   const float* res;      // (B, Cout, Ho, Wo) residual add, or null
@@ -63,10 +63,14 @@ hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStre
 hipError_t launch_conv_wino(int act, const ConvArgs& a, int B, hipStream_t s);
 bool conv_wino_ok(int cin, int ca, int cout, int wo);
 size_t conv_packed_floats_wino(int cin, int cout);
-hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s);
+// flipT: w is a forward conv's (cin, cout, 3, 3) weight; pack the input-gradient
+// conv's weight W'[co][ci] = W[ci][co] spatially flipped (training)
+hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s,
+                                 bool flipT = false);
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
-hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s);
+hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s,
+                            bool flipT = false);
 // fp32 Upsample conv weights: 4 parity classes of combined 2x2 taps
 size_t conv_packed_floats_up(int cin, int cout);
 hipError_t launch_pack_conv_up(const float* w, int cin, int cout, float* dst, hipStream_t s);
@@ -119,6 +123,11 @@ struct UpdateArgs {
   int P;
 };
 hipError_t launch_unet_update(const UpdateArgs& a, int B, hipStream_t s);
+// training plumbing (unet_train.hip): stride-2 input-gradient zero insertion
+// (x (B,C,Ho,Ho) -> (B,C,2Ho,2Ho)) and the upsample input gradient's 2x2 sums
+hipError_t launch_zero_insert(const float* x, int B, int C, int Ho, float* out, hipStream_t s);
+hipError_t launch_sum_pool2(const float* x, int B, int C, int H, float* out, int accumulate,
+                            hipStream_t s);
 hipError_t launch_set_word(int* w, int v, hipStream_t s);
 hipError_t launch_dec_word(int* w, hipStream_t s);
 

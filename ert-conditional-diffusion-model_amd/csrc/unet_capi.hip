@@ -622,9 +622,15 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   if (ertd_conv2d_workspace_bytes(Cin, Cout, ks, precision) > ws_bytes) return ERTD_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
   float* pk = (float*)ws;
-  hipError_t e = precision == ERTD_PREC_BF16 ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s)
-                 : (ks == 3 && mode == MODE_UP) ? launch_pack_conv_up(w, Cin, Cout, pk, s)
-                                                : launch_pack_conv(w, Cin, Cout, ks, pk, s);
+  // the Winograd path reads only its own packing: skip the direct one then
+  const int Ho_ = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  const bool wino = precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
+                    conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho_);
+  hipError_t e = hipSuccess;
+  if (!wino)
+    e = precision == ERTD_PREC_BF16 ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s)
+        : (ks == 3 && mode == MODE_UP) ? launch_pack_conv_up(w, Cin, Cout, pk, s)
+                                       : launch_pack_conv(w, Cin, Cout, ks, pk, s);
   if (e != hipSuccess) return (int)e;
   ConvArgs a{};
   a.srcA = x; a.srcB = x2; a.Ca = Ca; a.Cb = Cb;
@@ -633,8 +639,7 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   a.Cin = Cin; a.Cout = Cout; a.Hs = H; a.Ws = H;
   a.Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   a.Wo = a.Ho;
-  if (precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 &&
-      conv_packed_floats_wino(Cin, Cout) > 0) {
+  if (wino) {
     float* pw = pk + a64(std::max(conv_packed_floats(Cin, Cout, ks), conv_packed_floats_up(Cin, Cout)));
     if ((e = launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess) return (int)e;
     a.wpk_wino = pw;
@@ -651,6 +656,57 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
                                   : launch_conv(ks, mode, act, a, B, s);
   if (bimg) (void)hipFreeAsync(bimg, s);
   return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
+}
+
+// dX (B, Cin, H, H) (+)= the input gradient of y = conv(x) (Cout, Cin, ks, ks; mode as
+// ertd_conv2d) given dY (B, Cout, Ho, Ho): a stride-1 conv of dY (stride 2: of dY
+// zero-inserted to H; upsample: at 2H, then 2x2 sum-pooled) with the weight
+// transposed and flipped -- packed straight from w (Winograd where eligible).
+size_t ertd_conv_input_grad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mode) {
+  if (Cin < 1 || Cout < 1 || B < 1 || H < 1 || (ks != 1 && ks != 3) || mode < MODE_S1 ||
+      mode > MODE_UP || (ks == 1 && mode != MODE_S1))
+    return 0;
+  // packing (either layout) + the zero-inserted dY (stride 2) or the 2H gradient (upsample)
+  size_t n = a64(std::max(conv_packed_floats(Cout, Cin, ks), conv_packed_floats_wino(Cout, Cin)));
+  if (mode == MODE_S2) n += a64((size_t)B * Cout * H * H);
+  if (mode == MODE_UP) n += a64((size_t)B * Cin * 4 * H * H);
+  return n * sizeof(float);
+}
+
+int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout, int Cin, int ks,
+                         int mode, float* dx, int accumulate, void* ws, size_t ws_bytes,
+                         void* stream) {
+  const size_t need = ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, ks, mode);
+  if (!dy || !w || !dx || !ws || need == 0) return ERTD_EINVAL;
+  if (need > ws_bytes) return ERTD_ENOSPC;
+  hipStream_t s = (hipStream_t)stream;
+  float* pk = (float*)ws;
+  float* scratch = pk + a64(std::max(conv_packed_floats(Cout, Cin, ks), conv_packed_floats_wino(Cout, Cin)));
+  // the gradient conv: Cin_g = Cout, Cout_g = Cin, at resolution Hg
+  const int Hg = mode == MODE_UP ? 2 * H : H;
+  const float* src = dy;
+  if (mode == MODE_S2) {
+    hipError_t e = launch_zero_insert(dy, B, Cout, H / 2, scratch, s);
+    if (e != hipSuccess) return (int)e;
+    src = scratch;
+  }
+  ConvArgs a{};
+  a.srcA = src; a.Ca = Cout; a.Cb = 0;
+  a.Cin = Cout; a.Cout = Cin;
+  a.Hs = a.Ws = a.Ho = a.Wo = Hg;
+  const bool wino = ks == 3 && Cin > 1 && conv_packed_floats_wino(Cout, Cin) > 0 &&
+                    conv_wino_ok(Cout, Cout, Cin, Hg);
+  hipError_t e = wino ? launch_pack_conv_wino(w, Cout, Cin, pk, s, true)
+                      : launch_pack_conv(w, Cout, Cin, ks, pk, s, true);
+  if (e != hipSuccess) return (int)e;
+  if (wino) a.wpk_wino = pk; else a.wpk = pk;
+  a.bias = nullptr;   // no bias term in a gradient
+  float* out = mode == MODE_UP ? scratch : dx;
+  a.res = (mode != MODE_UP && accumulate) ? dx : nullptr;   // dx += conv(...) via the residual add
+  a.out = out;
+  if ((e = launch_conv(ks, MODE_S1, ACT_NONE, a, B, s)) != hipSuccess) return rcode(e);
+  if (mode == MODE_UP) return rcode(launch_sum_pool2(scratch, B, Cin, H, dx, accumulate, s));
+  return ERTD_OK;
 }
 
 int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B, int HW,

@@ -322,7 +322,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (co >= a.Cout) continue;
-        const float bias = a.bias[co];
+        const float bias = a.bias ? a.bias[co] : 0.f;
 #pragma unroll
         for (int j = 0; j < TPX; ++j) {
           float v = acc[i][j][r] + bias;
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
         int co = (tile0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         co = co < a.Cout ? co : a.Cout - 1;
         off[q] = co * HWo;
-        bias[q] = a.bias[co];
+        bias[q] = a.bias ? a.bias[co] : 0.f;
         eb[q] = ebp ? ebp[co] : 0.f;
 #pragma unroll
         for (int j = 0; j < TPX; ++j) rv[q][j] = resp ? resp[off[q] + j * 32] : 0.f;
@@ -489,7 +489,7 @@ size_t conv_packed_floats(int cin, int cout, int ks) {
 }
 
 __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout, int ks,
-                                 int nchunk, size_t total, float* __restrict__ dst) {
+                                 int nchunk, size_t total, float* __restrict__ dst, bool flipT) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int ck = conv_ck(ks), ch = ck / 2;
@@ -508,7 +508,11 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout,
   if (ks == 3) { ci = k * ck + hh * ch + s / 9; ky = (s % 9) / 3; kx = s % 3; }
   else { ci = k * ck + hh * ch + s; ky = 0; kx = 0; }
   float v = 0.f;
-  if (co < cout && ci < cin) v = w[(((size_t)co * cin + ci) * ks + ky) * ks + kx];
+  // flipT: w is the forward conv's (cin, cout, ks, ks) weight and this packs the
+  // input-gradient conv's W'[co][ci] = W[ci][co] spatially flipped
+  if (co < cout && ci < cin)
+    v = flipT ? w[(((size_t)ci * cout + co) * ks + (ks - 1 - ky)) * ks + (ks - 1 - kx)]
+              : w[(((size_t)co * cin + ci) * ks + ky) * ks + kx];
   dst[i] = v;
 }
 
@@ -557,10 +561,12 @@ hipError_t launch_pack_conv_up(const float* w, int cin, int cout, float* dst, hi
   return hipGetLastError();
 }
 
-hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s) {
+hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s,
+                            bool flipT) {
   const size_t total = conv_packed_floats(cin, cout, ks);
   const int nchunk = (cin + conv_ck(ks) - 1) / conv_ck(ks);
-  pack_conv_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cout, ks, nchunk, total, dst);
+  pack_conv_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cout, ks, nchunk, total, dst,
+                                                                    flipT);
   return hipGetLastError();
 }
 

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
         int co = (tile_wg + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         co = co < a.Cout ? co : a.Cout - 1;
         off[q] = co * HWo;
-        bias[q] = a.bias[co];
+        bias[q] = a.bias ? a.bias[co] : 0.f;
         eb[q] = ebp ? ebp[co] : 0.f;
 #pragma unroll
         for (int t = 0; t < TPX; ++t) rv[q][t] = resp ? resp[off[q] + t * 32] : 0.f;
@@ -536,6 +536,16 @@ static int convh_pre() {
   return v;
 }
 
+// ERTD_UNET_BF16_TPX=1 forces 128-pixel tiles for the 3x3 stride-1/upsample
+// convs (diagnostics); 0 = automatic
+static int convh_tpx_override() {
+  static int v = [] {
+    const char* e = getenv("ERTD_UNET_BF16_TPX");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int KS, int TP>
 static hipError_t launch_pre_w(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
@@ -565,17 +575,8 @@ static hipError_t launch_conv_pre(int ks, int mode, int act, const ConvArgs& a, 
   ConvArgs c = a;
   c.Hs = c.Ws = a.Wo;   // the image is at the output resolution
   if (ks == 1) return launch_pre_w<1, 1>(c, B, s);
+  if (convh_tpx_override() == 1) return launch_pre_w<3, 1>(c, B, s);
   return launch_pre_w<3, 2>(c, B, s);
-}
-
-// ERTD_UNET_BF16_TPX=1 forces 128-pixel tiles for the 3x3 stride-1/upsample
-// convs (diagnostics); 0 = automatic
-static int convh_tpx_override() {
-  static int v = [] {
-    const char* e = getenv("ERTD_UNET_BF16_TPX");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 template <int KS, int MODE, int ACT, int TP>

@@ -137,7 +137,8 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
 
   // epilogue in the MFMA kernels' op order: conv + bias, + emb, + residual
   const size_t o = (size_t)b * plane + (size_t)(oy0 + py) * WO + 4 * px4;
-  float4 v = make_float4(acc[0] + a.bias[0], acc[1] + a.bias[0], acc[2] + a.bias[0], acc[3] + a.bias[0]);
+  const float bb = a.bias ? a.bias[0] : 0.f;
+  float4 v = make_float4(acc[0] + bb, acc[1] + bb, acc[2] + bb, acc[3] + bb);
   if (a.ebias) {
     const float e = a.ebias[(size_t)b * a.eb_stride];
     v.x = v.x + e; v.y = v.y + e; v.z = v.z + e; v.w = v.w + e;

@@ -361,7 +361,7 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       co[i] = itm.cog * 64 + cb * 16 + 4 * (lane >> 4) + i;
-      bias[i] = a.bias[co[i]];
+      bias[i] = a.bias ? a.bias[co[i]] : 0.f;
       eb[i] = ebp ? ebp[co[i]] : 0.f;
     }
 #pragma unroll
@@ -477,8 +477,8 @@ hipError_t launch_act(const ConvArgs& a, int B, hipStream_t s) {
 // (computed in float64, rounded once): the A-operand fragment of
 // v_mfma_f32_16x16x4_f32 for co block cb (16 co) and k-step st, lane l =
 // 16 kk + c16 -> co = 16 cb + c16, channel 4 st + kk of the chunk
-__global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int nchunk, size_t total,
-                                 float* __restrict__ dst) {
+__global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int cout, int nchunk,
+                                 size_t total, float* __restrict__ dst, bool flipT) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c16 = (int)(i & 15);
@@ -494,13 +494,15 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int nchun
   const int ci = k * WKC + 4 * st + kk;
   const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   const int ri = xi >> 2, rj = xi & 3;
-  const float* g = w + ((size_t)co * cin + ci) * 9;
+  // flipT: w is the forward conv's (cin, cout, 3, 3) weight; pack the input-
+  // gradient conv's W'[co][ci] = W[ci][co] spatially flipped
+  const float* g = flipT ? w + ((size_t)ci * cout + co) * 9 : w + ((size_t)co * cin + ci) * 9;
   double u = 0.0;
 #pragma unroll
   for (int y = 0; y < 3; ++y) {
     double row = 0.0;
 #pragma unroll
-    for (int x = 0; x < 3; ++x) row += (double)g[y * 3 + x] * G[rj][x];
+    for (int x = 0; x < 3; ++x) row += (double)(flipT ? g[8 - (y * 3 + x)] : g[y * 3 + x]) * G[rj][x];
     u += G[ri][y] * row;
   }
   dst[i] = (float)u;
@@ -518,10 +520,12 @@ size_t conv_packed_floats_wino(int cin, int cout) {
   return (size_t)16 * cout * cin;
 }
 
-hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s) {
+hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s,
+                                 bool flipT) {
   const size_t total = conv_packed_floats_wino(cin, cout);
   if (!total) return hipErrorInvalidValue;
-  pack_wino_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cin / WKC, total, dst);
+  pack_wino_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cout, cin / WKC, total, dst,
+                                                                    flipT);
   return hipGetLastError();
 }
 

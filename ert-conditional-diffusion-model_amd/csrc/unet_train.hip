@@ -509,6 +509,22 @@ inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
 
+namespace ertd {
+namespace unet {
+hipError_t launch_zero_insert(const float* x, int B, int C, int Ho, float* out, hipStream_t s) {
+  const size_t n = (size_t)B * C * 4 * Ho * Ho;
+  zero_insert_kernel<<<nblk(n), 256, 0, s>>>(x, Ho, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_sum_pool2(const float* x, int B, int C, int H, float* out, int accumulate,
+                            hipStream_t s) {
+  const size_t n = (size_t)B * C * H * H;
+  sum_pool2_kernel<<<nblk(n), 256, 0, s>>>(x, H, n, out, accumulate);
+  return hipGetLastError();
+}
+}  // namespace unet
+}  // namespace ertd
+
 extern "C" {
 
 int ertd_gn_stats_mr(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,

@@ -118,6 +118,8 @@ SIGNATURES = {
     "ertd_channel_slice": (_I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I, _VP]),
     "ertd_mse_loss": (_I, [_VP, _VP, _LL, _VP, _VP, _VP]),
     "ertd_conv_wgrad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
+    "ertd_conv_input_grad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
+    "ertd_conv_input_grad": (_I, [_VP, _I, _I, _VP, _I, _I, _I, _I, _VP, _I, _VP, ctypes.c_size_t, _VP]),
     "ertd_conv_wgrad": (_I, [_VP, _VP, _I, _VP, _I, _I, _I, _I, _I, _I, _VP, _I, _VP, ctypes.c_size_t,
                              _VP]),
     "ertd_encoder_train_ws_bytes": (_SZ, [_I, _I]),

@@ -175,6 +175,19 @@ class _K:
         _lib.check(self.lib.ertd_wgrad_gemm(dy.data_ptr(), col.data_ptr(), M, N, P, B, M * P, N * P,
                                             out.data_ptr(), 0, ws.data_ptr(), n, self.s), "wgrad_gemm")
 
+    def conv_input_grad(self, dy, w, mode, H):
+        """dL/dx (B, Cin, H, H) of y = conv(x) with weight w given dy: a conv of dy with
+        w transposed and flipped, packed straight from w (ertd_conv_input_grad)."""
+        Cout, Cin, ks, _ = w.shape
+        B = dy.shape[0]
+        n = self.lib.ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, ks, mode)
+        ws = self.ws(n)
+        dx = self.empty(B, Cin, H, H)
+        _lib.check(self.lib.ertd_conv_input_grad(dy.data_ptr(), B, H, w.data_ptr(), Cout, Cin, ks, mode,
+                                                 dx.data_ptr(), 0, ws.data_ptr(), ws.numel(), self.s),
+                   "conv_input_grad")
+        return dx
+
     def flip(self, w):
         Cout, Cin, ks, _ = w.shape
         out = self.empty(Cin, Cout, ks, ks)
@@ -325,17 +338,7 @@ def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True):
     if not x_needs_grad:
         return None
     # input gradient: a conv of dY with the flipped, transposed weights
-    wf = k.flip(w)
-    zb = k.zero_vec(Cin)
-    if mode == MODE_S2:
-        return k.conv(k.zero_insert(dy), wf, zb)
-    if mode == MODE_UP:
-        du = k.conv(dy, wf, zb)
-        B, _, H2, _ = du.shape
-        dx = k.empty(B, Cin, H2 // 2, H2 // 2)
-        k.sum_pool2(du, dx, False)
-        return dx
-    return k.conv(dy, wf, zb)
+    return k.conv_input_grad(dy, w, mode, xa.shape[2])
 
 
 def _encoder_pack(model: ConditionalUNet, k: _K, W):

@@ -399,6 +399,14 @@ int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss
  *   fixed-order split reduction; ws >= ertd_conv_wgrad_ws_bytes (0 = unsupported
  *   geometry: output side not a power of two in [16, 128]).  csrc/unet_wgrad.hip. */
 size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mode);
+/* ertd_conv_input_grad: dx (B, Cin, H, H) (+)= dL/dx of y = conv(x) (weight w (Cout, Cin, ks, ks),
+ *   mode as ertd_conv2d) given dy (B, Cout, Ho, Ho): a stride-1 conv of dy (stride 2:
+ *   zero-inserted; upsample: at 2H then 2x2 sum-pooled) with w transposed and flipped, packed
+ *   straight from w (Winograd where eligible); ws >= ertd_conv_input_grad_ws_bytes.       */
+size_t ertd_conv_input_grad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mode);
+int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout, int Cin, int ks,
+                         int mode, float* dx, int accumulate, void* ws, size_t ws_bytes,
+                         void* stream);
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
                     int Cout, int ks, int mode, float* dw, int accumulate, void* ws,
                     size_t ws_bytes, void* stream);

@@ -262,3 +262,39 @@ def test_gn_act_backward_vs_autograd(Ca, Cb, HW, groups, act, acc, cuda_dev):
     e = [_rel(dx, want), _rel(dgb[0], gr.grad), _rel(dgb[1], br.grad)]
     record_error(f"gn_act_backward_{C}_{HW}_g{groups}_a{act}", max(e))
     assert max(e) < 1e-5, e
+
+
+@pytest.mark.parametrize("Cin,Cout,H,ks,mode,B,acc", [
+    (64, 64, 64, 3, 0, 2, 0),      # Winograd-eligible gradient conv
+    (192, 64, 32, 3, 0, 2, 1),     # Cin_grad = 64 -> Cout_grad = 192, accumulate
+    (64, 1, 32, 3, 0, 2, 0),       # conv_out's gradient (Cin_grad = 1)
+    (1, 32, 32, 3, 0, 2, 0),       # conv_in's gradient (Cout_grad = 1: the Cout = 1 kernel)
+    (64, 64, 64, 3, 1, 2, 1),      # stride 2
+    (128, 128, 16, 3, 2, 2, 0),    # upsample
+    (96, 64, 32, 1, 0, 2, 1),      # 1x1
+])
+def test_conv_input_grad_vs_autograd(Cin, Cout, H, ks, mode, B, acc, cuda_dev):
+    from ertdiff import _lib
+    g = torch.Generator().manual_seed(Cin + 3 * Cout + H + mode)
+    w = torch.randn(Cout, Cin, ks, ks, generator=g) / (Cin * ks * ks) ** 0.5
+    Ho = H // 2 if mode == 1 else (2 * H if mode == 2 else H)
+    dy = torch.randn(B, Cout, Ho, Ho, generator=g)
+    prev = torch.randn(B, Cin, H, H, generator=g)
+    if mode == 2:
+        ref = torch.nn.grad.conv2d_input((B, Cin, 2 * H, 2 * H), w.double(), dy.double(), padding=1)
+        ref = ref.view(B, Cin, H, 2, H, 2).sum((3, 5))
+    else:
+        ref = torch.nn.grad.conv2d_input((B, Cin, H, H), w.double(), dy.double(),
+                                         stride=2 if mode == 1 else 1, padding=ks // 2)
+    if acc:
+        ref = ref + prev.double()
+    lib = _lib.lib()
+    n = lib.ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, ks, mode)
+    ws = torch.empty(n, dtype=torch.uint8, device=cuda_dev)
+    dx = prev.to(cuda_dev)
+    wd, dyd = w.to(cuda_dev), dy.to(cuda_dev)
+    assert lib.ertd_conv_input_grad(dyd.data_ptr(), B, H, wd.data_ptr(), Cout, Cin, ks, mode,
+                                    dx.data_ptr(), acc, ws.data_ptr(), n, _lib.stream_of(cuda_dev)) == 0
+    err = _rel(dx, ref)
+    record_error(f"conv_input_grad_{Cin}_{Cout}_{H}_k{ks}_m{mode}", err)
+    assert err < 1e-5, err
