@@ -354,14 +354,17 @@ def bench_hbm_kernels(dev, reps=50):
     return out
 
 
-def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000):
+def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000, rank=0, world=1):
     """The reference train step (:309-320) on the U-Net denoiser: q_sample, the
     HIP forward with saved activations, the hand-written HIP backward, MSE and
-    the multi-tensor Adam kernel (ertdiff.unet_train_step), fp32, batch B."""
+    the multi-tensor Adam kernel (ertdiff.unet_train_step), fp32, batch B per
+    GPU.  N > 1: data parallel (identical replicas, each rank its own shard of
+    the global batch, gradients averaged by one bucketed RCCL all-reduce per
+    step); weak scaling, time = max over ranks."""
     from ertdiff.unet_train import unet_train_step
     model = ertdiff.ConditionalUNet.from_config(name, seed=0).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
-    g = torch.Generator(device=dev).manual_seed(11)
+    g = torch.Generator(device=dev).manual_seed(11 + rank)
     P_ = model.param_dim
     x0 = torch.randn(B, P_, device=dev, generator=g)
     cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
@@ -371,16 +374,26 @@ def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000):
     for i in range(warmup):
         unet_train_step(model, opt, x0, cond, T, ab, t=ts[i], noise=ns[i], return_tensor=True)
     torch.cuda.synchronize(dev)
+    barrier(world)
     t0 = time.perf_counter()
     for i in range(steps):
         loss = unet_train_step(model, opt, x0, cond, T, ab, t=ts[warmup + i], noise=ns[warmup + i],
                                return_tensor=True)
     torch.cuda.synchronize(dev)
+    barrier(world)
     el = time.perf_counter() - t0
-    return {"unet_train_steps_per_s": round(steps / el, 3), "model": name, "batch": B,
+    if world > 1:
+        e = torch.tensor([el], device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    return {"unet_train_steps_per_s": round(steps / el, 3), "model": name, "batch_per_gpu": B,
+            "global_batch": B * world, "samples_per_s": round(steps * B * world / el, 1),
             "ms_per_step": round(el / steps * 1e3, 2), "steps": steps, "warmup": warmup,
-            "final_loss": round(float(loss), 5), "dtype": "f32",
-            "note": "one process, wall clock around the steps (host walk + HIP kernels)"}
+            "final_loss_rank0": round(float(loss), 5), "dtype": "f32",
+            "scaling": "weak" if world > 1 else None,
+            "parallelism": f"dp{world} (one bucketed RCCL all-reduce of the gradients per step)"
+            if world > 1 else "1 GPU",
+            "note": "wall clock around the steps (host walk + HIP kernels), max over ranks"}
 
 
 def _host_cpus():
@@ -762,8 +775,8 @@ def main():
         extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev)
     if not a.no_hbm_kernels:
         extra["hbm_kernels"] = bench_hbm_kernels(dev)
-    if not a.no_unet_train and world == 1:
-        extra["unet_train"] = bench_unet_train(dev, steps=a.unet_train_steps)
+    if not a.no_unet_train:
+        extra["unet_train"] = bench_unet_train(dev, steps=a.unet_train_steps, rank=rank, world=world)
     if not a.no_kde:
         extra["kde_mode"] = bench_kde(dev, world, rank, cpu=not a.no_cpu_baseline)
     if not a.no_reference:

@@ -505,6 +505,21 @@ __global__ __launch_bounds__(256) void concat_kernel(CatMulti c, float* __restri
   dst[i] = c.src[k][i - c.off[k]];
 }
 
+// dst[k] = alpha * src[off[k] .. off[k+1]) (the inverse of concat_kernel, scaled)
+struct SplitMulti {
+  float* dst[CAT_T];
+  long long off[CAT_T + 1];
+  int nt;
+};
+__global__ __launch_bounds__(256) void split_kernel(SplitMulti c, const float* __restrict__ src,
+                                                    float alpha) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= c.off[c.nt]) return;
+  int k = 0;
+  while (k + 1 < c.nt && i >= c.off[k + 1]) ++k;
+  c.dst[k][i - c.off[k]] = alpha * src[i];
+}
+
 inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
@@ -766,6 +781,30 @@ int ertd_concat(const float* const* srcs, const long long* sizes, int n, float* 
     }
     c.off[c.nt] = off;
     if (off > 0) concat_kernel<<<nblk((size_t)off), 256, 0, s>>>(c, dst + base);
+    base += off;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return ERTD_OK;
+}
+
+int ertd_split(const float* src, float* const* dsts, const long long* sizes, int n, float alpha,
+               void* stream) {
+  if (!src || !dsts || !sizes || n < 1) return ERTD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  long long base = 0;
+  for (int t0 = 0; t0 < n; t0 += CAT_T) {
+    SplitMulti c{};
+    c.nt = n - t0 < CAT_T ? n - t0 : CAT_T;
+    long long off = 0;
+    for (int k = 0; k < c.nt; ++k) {
+      if (!dsts[t0 + k] || sizes[t0 + k] < 0) return ERTD_EINVAL;
+      c.dst[k] = dsts[t0 + k];
+      c.off[k] = off;
+      off += sizes[t0 + k];
+    }
+    c.off[c.nt] = off;
+    if (off > 0) split_kernel<<<nblk((size_t)off), 256, 0, s>>>(c, src + base, alpha);
     base += off;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;

@@ -106,6 +106,7 @@ SIGNATURES = {
     "ertd_sum_pool2": (_I, [_VP, _I, _I, _I, _VP, _I, _VP]),
     "ertd_channel_sums": (_I, [_VP, _I, _I, _I, _VP, _I, _VP, _I, _VP]),
     "ertd_concat": (_I, [_VP, _VP, _I, _VP, _VP]),
+    "ertd_split": (_I, [_VP, _VP, _VP, _I, _F, _VP]),
     "ertd_act_bf16": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _I, _I, _VP, _VP]),
     "ertd_unet_update": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, ctypes.c_uint64, ctypes.c_uint32,
                               _I, _I, _VP]),

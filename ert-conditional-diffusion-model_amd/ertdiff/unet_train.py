@@ -633,6 +633,38 @@ class UNetForwardFn(torch.autograd.Function):
         return (None, grads.get("__x__"), None, None, *out)
 
 
+def allreduce_mean(grads, group, ops) -> None:
+    """Data-parallel gradient exchange: ONE all-reduce of every gradient packed
+    into a flat bucket (57 MB for U2: the per-link-bound ring wants few, large
+    messages), scaled by 1 / world, unpacked in place.  ``ops`` supplies the
+    device packing: ``concat(list) -> flat`` and ``split(flat, list, alpha)``
+    (list[k] = alpha * its slice of flat): HIP kernels on the GPU, torch in the
+    CPU tests."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    flat = ops.concat(grads)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    ops.split(flat, grads, 1.0 / world)
+
+
+class _DeviceBucketOps:
+    """allreduce_mean's packing on the device (ertd_concat / eltwise / channel copies)."""
+
+    def __init__(self, k: _K):
+        self.k = k
+
+    def concat(self, ts):
+        return self.k.concat(ts)
+
+    def split(self, flat, ts, alpha):
+        k = self.k
+        _lib.check(k.lib.ertd_split(flat.data_ptr(), _arr([t.data_ptr() for t in ts]),
+                                    _arr([t.numel() for t in ts], ctypes.c_longlong), len(ts),
+                                    float(alpha), k.s), "split")
+
+
 def _adam_state(optimizer, params):
     from .train import _adam_hparams
     lr, b1, b2, eps = _adam_hparams(optimizer, params)
@@ -651,11 +683,19 @@ def _adam_state(optimizer, params):
 
 @torch.no_grad()
 def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *, t=None,
-                    noise=None, return_tensor: bool = False):
+                    noise=None, return_tensor: bool = False, process_group=None):
     """The reference train step (:309-320) on the U-Net: t ~ randint(0, T),
     noise ~ randn_like(x0) (or given), x_noisy = q_sample, eps = model(x_noisy,
     t, cond), loss = MSELoss(mean)(eps, noise), backward, torch.optim.Adam
-    step (state in optimizer.state).  Returns loss.item() (or the device scalar)."""
+    step (state in optimizer.state).  Returns loss.item() (or the device scalar)
+    of this rank's batch.
+
+    Data parallel: with ``process_group`` (or the default group when
+    torch.distributed is initialized with more than one rank) each rank passes
+    its own shard of the global batch and the gradients are averaged across
+    ranks (one bucketed all-reduce, RCCL over xGMI) before the Adam step, so
+    every rank applies the global-batch mean gradient (equal shard sizes) and
+    the replicas stay identical."""
     from .model import q_sample
     names = [nm for nm, _ in model.named_parameters()]
     params = [p for _, p in model.named_parameters()]
@@ -684,6 +724,12 @@ def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *
         grads = unet_train_backward(model, tape, deps)
         for nm, p in zip(names, params):
             p.grad = grads[nm].view_as(p)
+        import torch.distributed as dist
+        group = process_group
+        if group is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            group = dist.group.WORLD
+        if group is not None:
+            allreduce_mean([p.grad for p in params], group, _DeviceBucketOps(tape["k"]))
         lr, b1, b2, ep, ms, vs, step = _adam_state(optimizer, params)
         sizes = _arr([p.numel() for p in params], ctypes.c_longlong)
         arrs = [_arr([x.data_ptr() for x in ts]) for ts in (params, [p.grad for p in params], ms, vs)]

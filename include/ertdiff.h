@@ -411,6 +411,10 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
                     int Cout, int ks, int mode, float* dw, int accumulate, void* ws,
                     size_t ws_bytes, void* stream);
 int ertd_concat(const float* const* srcs, const long long* sizes, int n, float* dst, void* stream);
+/* ertd_split: dsts[k] = alpha * src[sum(sizes[<k]) ...] (the inverse of ertd_concat, scaled):
+ *   the data-parallel train step's gradient bucket back into the per-tensor gradients. */
+int ertd_split(const float* src, float* const* dsts, const long long* sizes, int n, float alpha,
+               void* stream);
 int ertd_encoder_train_pack(const float* w0, const float* w2, float* packed, void* stream);
 size_t ertd_encoder_train_ws_bytes(int B, int L);
 int ertd_encoder_train_fwd(const float* packed, const float* b1, const float* b2, const float* cond,

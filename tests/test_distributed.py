@@ -98,3 +98,54 @@ def test_sharded_ensemble_gloo(world, n_members, kind):
         shards.append(shard)
     # host concatenation of the per-rank shards (the default, collective-free return)
     assert (np.concatenate(shards) == expect).all()
+
+
+class _TorchBucketOps:
+    """allreduce_mean's packing with torch on CPU (the device path uses ertd_concat / ertd_split)."""
+
+    @staticmethod
+    def concat(ts):
+        return torch.cat([t.reshape(-1) for t in ts])
+
+    @staticmethod
+    def split(flat, ts, alpha):
+        o = 0
+        for t in ts:
+            n = t.numel()
+            t.copy_((alpha * flat[o:o + n]).view_as(t))
+            o += n
+
+
+def _dp_worker(rank, world, port, q):
+    from ertdiff.unet_train import allreduce_mean
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(100 + rank)
+        grads = [torch.randn(7, 3, generator=g), torch.randn(5, generator=g), torch.randn(2, 2, 3, 3, generator=g)]
+        mine = [t.clone() for t in grads]
+        allreduce_mean(grads, dist.group.WORLD, _TorchBucketOps())
+        q.put((rank, [t.numpy() for t in mine], [t.numpy() for t in grads]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dp_gradient_mean_gloo(world):
+    """Data-parallel U-Net train step (ertdiff.unet_train.allreduce_mean): every
+    rank ends with the mean of all ranks' gradients, tensor shapes intact."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i in range(3):
+        want = sum(res[r][0][i] for r in range(world)) / world
+        for r in range(world):
+            np.testing.assert_allclose(res[r][1][i], want, rtol=1e-6, atol=1e-7)

@@ -298,3 +298,73 @@ def test_conv_input_grad_vs_autograd(Cin, Cout, H, ks, mode, B, acc, cuda_dev):
     err = _rel(dx, ref)
     record_error(f"conv_input_grad_{Cin}_{Cout}_{H}_k{ks}_m{mode}", err)
     assert err < 1e-5, err
+
+
+def _dp_train_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    # both ranks on the one GPU of the box: gloo carries the (device) gradient bucket
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        cfg = U.CONFIGS["U1"]
+        Bg, L, T = 4, 65, 1000
+        x0 = torch.from_numpy(synth_normal((Bg, cfg.param_dim), 530)).to(dev)
+        cond = torch.from_numpy(synth_uniform((Bg, 14, L), 531)).to(dev)
+        t = torch.from_numpy(synth_timesteps(Bg, T, 532)).to(dev)
+        noise = torch.from_numpy(synth_normal((Bg, cfg.param_dim), 533)).to(dev)
+        _, _, ab = ertdiff.get_diffusion_schedule(T, device=dev)
+        m = ertdiff.ConditionalUNet.from_config("U1", seed=9).to(dev)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        sh = slice(rank * Bg // world, (rank + 1) * Bg // world)
+        unet_train_step(m, opt, x0[sh], cond[sh], T, ab, t=t[sh], noise=noise[sh])
+        # numpy (pickled by value): torch CPU tensors would travel as shared-memory
+        # handles that die with this process
+        q.put((rank, {k: p.grad.cpu().numpy() for k, p in m.named_parameters()},
+               {k: p.detach().cpu().numpy() for k, p in m.named_parameters()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_unet_train_data_parallel(cuda_dev):
+    """Two data-parallel ranks with half the batch each end with the full-batch
+    gradient (the mean of their shard means) and identical parameters."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, w)) for r, g, w in (q.get(timeout=300) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process, whole batch
+    cfg = U.CONFIGS["U1"]
+    Bg, L, T = 4, 65, 1000
+    x0 = torch.from_numpy(synth_normal((Bg, cfg.param_dim), 530)).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((Bg, 14, L), 531)).to(cuda_dev)
+    t = torch.from_numpy(synth_timesteps(Bg, T, 532)).to(cuda_dev)
+    noise = torch.from_numpy(synth_normal((Bg, cfg.param_dim), 533)).to(cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    m = ertdiff.ConditionalUNet.from_config("U1", seed=9).to(cuda_dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    unet_train_step(m, opt, x0, cond, T, ab, t=t, noise=noise)
+    norms = [float(p.grad.double().norm()) for p in m.parameters()]
+    floor = 1e-3 * float(np.sqrt(np.mean(np.square(norms))))
+    worst = 0.0
+    for (k, p), nr in zip(m.named_parameters(), norms):
+        for r in range(2):
+            e = float(np.linalg.norm(res[r][0][k].astype(np.float64) -
+                                     p.grad.detach().cpu().double().numpy())) / max(nr, floor)
+            worst = max(worst, e)
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k     # replicas identical
+    record_error("unet_train_dp2_vs_single", worst)
+    assert worst < 1e-5, worst
