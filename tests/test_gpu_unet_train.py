@@ -368,3 +368,24 @@ def test_unet_train_data_parallel(cuda_dev):
         assert np.array_equal(res[0][1][k], res[1][1][k]), k     # replicas identical
     record_error("unet_train_dp2_vs_single", worst)
     assert worst < 1e-5, worst
+
+
+def test_unet_train_step_u5_runs(cuda_dev):
+    """configs[4]'s network (128x128, 4 levels, ch 128, mid attention) through
+    the fp32 train step: finite loss, every gradient finite, and a second step
+    on the same batch lowers the loss (no spec comparison at this size: the
+    float64 CPU autograd of U5 is minutes; U1/U2/U3 are pinned above)."""
+    cfg = U.CONFIGS["U5"]
+    B, L, T = 1, 65, 1000
+    m = ertdiff.ConditionalUNet.from_config("U5", seed=1).to(cuda_dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    x0 = torch.from_numpy(synth_normal((B, cfg.param_dim), 540)).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 541)).to(cuda_dev)
+    t = torch.tensor([321], device=cuda_dev)
+    noise = torch.from_numpy(synth_normal((B, cfg.param_dim), 542)).to(cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    l0 = unet_train_step(m, opt, x0, cond, T, ab, t=t, noise=noise)
+    assert np.isfinite(l0)
+    assert all(bool(torch.isfinite(p.grad).all()) for p in m.parameters())
+    l1 = unet_train_step(m, opt, x0, cond, T, ab, t=t, noise=noise)
+    assert l1 < l0, (l0, l1)
