@@ -43,6 +43,8 @@ struct ConvArgs {
   int bimg_ready;        // 1: bimg already holds the transformed input (launch_gn_act_bf16)
   const float* wpk_wino; // fp32 3x3 stride-1: Winograd-transformed weights (launch_pack_conv_wino)
                          // or null (direct implicit GEMM)
+  float* ksplit_buf;     // Winograd, optional: (B, Cout, Ho, Wo) scratch that lets a layer with
+                         // fewer tile items than CUs split its K (input channels) in two halves
 };
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
@@ -62,6 +64,8 @@ hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStre
 // disables), the U = G g G^T packing (0 floats: shape not eligible), launch
 hipError_t launch_conv_wino(int act, const ConvArgs& a, int B, hipStream_t s);
 bool conv_wino_ok(int cin, int ca, int cout, int wo);
+// a Winograd layer with this geometry splits its K when given ConvArgs::ksplit_buf
+bool wino_ksplit_wanted(int cin, int cout, int wo, int B);
 size_t conv_packed_floats_wino(int cin, int cout);
 // flipT: w is a forward conv's (cin, cout, 3, 3) weight; pack the input-gradient
 // conv's weight W'[co][ci] = W[ci][co] spatially flipped (training)

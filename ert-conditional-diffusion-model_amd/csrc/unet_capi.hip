@@ -255,6 +255,11 @@ struct Walk {
     if (mode == MODE_S2) { Ho = Hs / 2; Wo = Ws / 2; }
     if (mode == MODE_UP) { Ho = Hs * 2; Wo = Ws * 2; }
     if (!out) out = alloc((size_t)B * Cout * Ho * Wo);
+    // fp32 Winograd layers with fewer tile items than CUs split their K
+    float* kbuf = nullptr;
+    if (c->precision == ERTD_PREC_FP32 && ks == 3 && mode == MODE_S1 && L->offw.count(n + ".weight") &&
+        conv_wino_ok(Cin, Ca, Cout, Wo) && wino_ksplit_wanted(Cin, Cout, Wo, B))
+      kbuf = alloc((size_t)B * Cout * Ho * Wo);
     // bf16 stride-1 convs stage a pre-transformed bf16 copy of their input
     float* bimg = nullptr;
     if (c->precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
@@ -279,6 +284,7 @@ struct Walk {
     a.Cin = Cin; a.Cout = Cout;
     a.Hs = Hs; a.Ws = Ws; a.Ho = Ho; a.Wo = Wo;
     a.bimg = bimg;
+    a.ksplit_buf = kbuf;
     if (has_pend) {
       has_pend = false;
       if (bimg && ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) {
@@ -639,10 +645,16 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   a.Cin = Cin; a.Cout = Cout; a.Hs = H; a.Ws = H;
   a.Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   a.Wo = a.Ho;
+  void* kbuf = nullptr;
   if (wino) {
     float* pw = pk + a64(std::max(conv_packed_floats(Cin, Cout, ks), conv_packed_floats_up(Cin, Cout)));
     if ((e = launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess) return (int)e;
     a.wpk_wino = pw;
+    if (wino_ksplit_wanted(Cin, Cout, Ho_, B)) {   // stream-ordered scratch (freed on the stream)
+      if ((e = hipMallocAsync(&kbuf, (size_t)B * Cout * Ho_ * Ho_ * sizeof(float), s)) != hipSuccess)
+        return rcode(e);
+      a.ksplit_buf = (float*)kbuf;
+    }
   }
   void* bimg = nullptr;
   if (precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
@@ -655,6 +667,7 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   e = precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
                                   : launch_conv(ks, mode, act, a, B, s);
   if (bimg) (void)hipFreeAsync(bimg, s);
+  if (kbuf) (void)hipFreeAsync(kbuf, s);
   return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
 }
 
@@ -670,6 +683,8 @@ size_t ertd_conv_input_grad_ws_bytes(int Cin, int Cout, int B, int H, int ks, in
   size_t n = a64(std::max(conv_packed_floats(Cout, Cin, ks), conv_packed_floats_wino(Cout, Cin)));
   if (mode == MODE_S2) n += a64((size_t)B * Cout * H * H);
   if (mode == MODE_UP) n += a64((size_t)B * Cin * 4 * H * H);
+  const int Hg = mode == MODE_UP ? 2 * H : H;
+  if (ks == 3) n += a64((size_t)B * Cin * Hg * Hg);   // a Winograd K split's second half
   return n * sizeof(float);
 }
 
@@ -700,6 +715,11 @@ int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout
                       : launch_pack_conv(w, Cout, Cin, ks, pk, s, true);
   if (e != hipSuccess) return (int)e;
   if (wino) a.wpk_wino = pk; else a.wpk = pk;
+  if (wino && wino_ksplit_wanted(Cout, Cin, Hg, B)) {
+    const size_t sc = mode == MODE_S2 ? a64((size_t)B * Cout * H * H)
+                      : (mode == MODE_UP ? a64((size_t)B * Cin * 4 * H * H) : 0);
+    a.ksplit_buf = scratch + sc;
+  }
   a.bias = nullptr;   // no bias term in a gradient
   float* out = mode == MODE_UP ? scratch : dx;
   a.res = (mode != MODE_UP && accumulate) ? dx : nullptr;   // dx += conv(...) via the residual add

@@ -95,7 +95,7 @@ __device__ __forceinline__ Item item_of(int it, int ncog, int ntblk) {
 // producers' DPP / padding selects / V stores -- the results are
 // wrong, the timings show where a chunk's time goes
 template <int WO, int ACT, int DBG = 0>
-__global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
+__global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, int ksp) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* ubuf = smem;                 // [3][U_FL] ring
   float* vbuf = smem + NUB * U_FL;    // [2][V_FL]
@@ -109,10 +109,15 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
   const int hh = lane >> 5, l32 = lane & 31;
   const int Cin = a.Cin, Ca = a.Ca;
   const int nchunk = Cin / WKC;
+  // ksp = 2 (K split, few items): work item it = 2 x (tile item) + half; half h
+  // accumulates channel chunks [h nck, (h+1) nck) and writes its partial sum
+  // to a.out (h = 0, with bias / emb / residual) or a.ksplit_buf (h = 1); the
+  // launcher adds the two afterwards
+  const int nck = nchunk / ksp;                                      // chunks per work item
   const int ncog = a.Cout / 64;
   const int bid = blockIdx.x, G = gridDim.x;
   const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;   // items of this workgroup
-  const int gtot = nloc * nchunk;                                    // chunks of this workgroup
+  const int gtot = nloc * nck;                                       // chunks of this workgroup
 
   if (wave >= NMW) {
     // =================== producer waves ===================
@@ -129,8 +134,9 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
     float2 gnv[NRS][2];
     unsigned msk[NRS] = {};   // bits 0-3: row r valid, bit 4: left column, bit 5: right column
     auto load_chunk = [&](const int set, int g) {
-      const int il = g / nchunk, k = g - il * nchunk;
-      const Item itm = item_of(bid + il * G, ncog, NTBLK);
+      const int il = g / nck, it = bid + il * G;
+      const int k = (it % ksp) * nck + (g - il * nck);
+      const Item itm = item_of(it / ksp, ncog, NTBLK);
       const int tg = itm.tblk * 64 + lane;
       const int ty = tg / TPR, tx = tg - ty * TPR;
       unsigned m = (tx > 0 ? 16u : 0u) | (tx < TPR - 1 ? 32u : 0u);
@@ -269,8 +275,9 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
   // (vmcnt(4)) is exactly "chunk g+1's slice has landed"
   auto dma_u = [&](int g) {
     if constexpr (DBG & 4) return;
-    const int il = g / nchunk, k = g - il * nchunk;
-    const int cog = (bid + il * G) % ncog;
+    const int il = g / nck, it = bid + il * G;
+    const int k = (it % ksp) * nck + (g - il * nck);
+    const int cog = (it / ksp) % ncog;
     const float* usrc = a.wpk_wino + ((size_t)cog * nchunk + k) * U_FL;
     float* dst = ubuf + (g % NUB) * U_FL;
 #pragma unroll
@@ -295,8 +302,8 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
   for (int il = 0; il < nloc; ++il) {
 #pragma unroll
     for (int x = 0; x < 16; ++x) acc[x][0] = acc[x][1] = f32x4{};
-    for (int k = 0; k < nchunk; ++k) {
-      const int g = il * nchunk + k;
+    for (int k = 0; k < nck; ++k) {
+      const int g = il * nck + k;
       const bool dma = g + 2 < gtot;
       if (dma) dma_u(g + 2);
       // the lane-dependent operand offsets are re-derived per chunk from a
@@ -354,14 +361,18 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
     // ---- output transform of this wave's 16 co x 32 tiles, in registers:
     // lane l holds M[xi] of co = 16 cb + 4 (l >> 4) + i (acc element i) and
     // tile 16 j + (l & 15) of its tile pair (accumulator j)
-    const Item itm = item_of(bid + il * G, ncog, NTBLK);
-    const float* ebp = a.ebias ? a.ebias + (size_t)itm.b * a.eb_stride : nullptr;
+    const int itg = bid + il * G;
+    const Item itm = item_of(itg / ksp, ncog, NTBLK);
+    const bool part2 = (itg % ksp) != 0;   // second K half: raw partial sum only
+    const float* ebp = (a.ebias && !part2) ? a.ebias + (size_t)itm.b * a.eb_stride : nullptr;
+    const float* resp = part2 ? nullptr : a.res;
+    float* outp = part2 ? a.ksplit_buf : a.out;
     float bias[4], eb[4];
     int co[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       co[i] = itm.cog * 64 + cb * 16 + 4 * (lane >> 4) + i;
-      bias[i] = a.bias ? a.bias[co[i]] : 0.f;
+      bias[i] = (a.bias && !part2) ? a.bias[co[i]] : 0.f;
       eb[i] = ebp ? ebp[co[i]] : 0.f;
     }
 #pragma unroll
@@ -369,8 +380,8 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems) {
       const int tg = itm.tblk * 64 + (2 * tbp + j) * 16 + (lane & 15);
       const int ty = tg / TPR, tx = tg - ty * TPR;
       const size_t pix = (size_t)(2 * ty) * WO + 2 * tx;
-      float* outb = a.out + (size_t)itm.b * a.Cout * HW + pix;
-      const float* resb = a.res ? a.res + (size_t)itm.b * a.Cout * HW + pix : nullptr;
+      float* outb = outp + (size_t)itm.b * a.Cout * HW + pix;
+      const float* resb = resp ? resp + (size_t)itm.b * a.Cout * HW + pix : nullptr;
       float2 rv[4][2];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -415,6 +426,25 @@ int wino_dbg() {
   return v;
 }
 
+// out += part (float4): the K-split halves' fixed-order sum
+__global__ void add_inplace_kernel(float* __restrict__ out, const float* __restrict__ part, size_t n4) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 o = reinterpret_cast<float4*>(out)[i];
+  const float4 p = reinterpret_cast<const float4*>(part)[i];
+  o.x = o.x + p.x; o.y = o.y + p.y; o.z = o.z + p.z; o.w = o.w + p.w;
+  reinterpret_cast<float4*>(out)[i] = o;
+}
+
+// K split when a layer has fewer tile items than ERTD_WINO_KSPLIT x CUs (default 1)
+int ksplit_items() {
+  static int v = [] {
+    const char* e = getenv("ERTD_WINO_KSPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 int cu_count() {
   static int v = [] {
     int dev = 0, n = 0;
@@ -434,9 +464,18 @@ hipError_t launch_wod(const ConvArgs& a, int B, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)WLDS);
     attr = true;
   }
-  const int nitems = (WO / 2) * (WO / 2) / 64 * (a.Cout / 64) * B;
+  const int base = (WO / 2) * (WO / 2) / 64 * (a.Cout / 64) * B;
+  // fewer tile items than the split threshold (x CUs) -> K split in two halves
+  const int nchunk = a.Cin / WKC;
+  const int ksp = (a.ksplit_buf && nchunk % 2 == 0 && nchunk >= 4 &&
+                   base < ksplit_items() * cu_count()) ? 2 : 1;
+  const int nitems = base * ksp;
   const int grid = nitems < cu_count() ? nitems : cu_count();
-  conv_wino_kernel<WO, ACT, DBG><<<grid, WT, WLDS, s>>>(a, nitems);
+  conv_wino_kernel<WO, ACT, DBG><<<grid, WT, WLDS, s>>>(a, nitems, ksp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || ksp == 1) return e;
+  const size_t n = (size_t)B * a.Cout * WO * WO;
+  add_inplace_kernel<<<(unsigned)((n / 4 + 255) / 256), 256, 0, s>>>(a.out, a.ksplit_buf, n / 4);
   return hipGetLastError();
 }
 
@@ -509,6 +548,12 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int cout,
 }
 
 }  // namespace
+
+bool wino_ksplit_wanted(int cin, int cout, int wo, int B) {
+  const int base = (wo / 2) * (wo / 2) / 64 * (cout / 64) * B;
+  const int nchunk = cin / WKC;
+  return nchunk % 2 == 0 && nchunk >= 4 && base < ksplit_items() * cu_count();
+}
 
 bool conv_wino_ok(int cin, int ca, int cout, int wo) {
   return wino_env() != 0 && cin % WKC == 0 && ca % WKC == 0 && cout % 64 == 0 &&
