@@ -36,6 +36,7 @@ struct WgArgs {
   const float* xa;
   const float* xb;
   int Ca, Cb, Cout, H, Ho, R;
+  const float2* gn;   // (B, Cin) {scale, shift} when the conv's input is act(GroupNorm(x)) (ACT)
   int ntiles, nco, nsplit, cps, nchunks;
   float* part;   // (nsplit, Cout, Cin * KK)
 };
@@ -64,7 +65,23 @@ __device__ __forceinline__ const float* chan_ptr(const WgArgs& a, int b, int ci)
   return ci < a.Ca ? a.xa + ((size_t)b * a.Ca + ci) * hw : a.xb + ((size_t)b * a.Cb + ci - a.Ca) * hw;
 }
 
-template <int MODE, int KS, int HO>
+// ACT (stride 1 only): the conv's input is act(GroupNorm(x)) -- applied here
+// while staging (x * scale + shift, then SiLU for ACT_GN_SILU), so the
+// activated tensor never has to exist in HBM; padding stays zero
+template <int ACT>
+__device__ __forceinline__ f32x4 wg_act(f32x4 v, float2 g) {
+  if constexpr (ACT != ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = fmaf(v[e], g.x, g.y);
+      if constexpr (ACT == ACT_GN_SILU) t = t * __builtin_amdgcn_rcpf(1.0f + __expf(-t));
+      v[e] = t;
+    }
+  }
+  return v;
+}
+
+template <int MODE, int KS, int HO, int ACT>
 __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int KK = KS * KS;
@@ -98,6 +115,9 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
   constexpr int NXR = (nx + 255) / 256;
   f32x4 dyr[NDY];
   f32x4 xr[MODE == MODE_S2 ? 1 : NXR];
+  // ACT: the activation is applied in store() (after the chunk's MFMAs), not
+  // in load(), so the prefetch stays in flight; {scale, shift} ride along
+  float2 gr[ACT != ACT_NONE && MODE != MODE_S2 ? NXR : 1];
   auto load = [&](int c) {
     const int b = c / rows_per_b, y0 = (c - b * rows_per_b) * R;
 #pragma unroll
@@ -112,10 +132,14 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
       for (int k = 0; k < NXR; ++k) {
         const int i = tid + 256 * k;
         f32x4 v = f32x4{};
+        if constexpr (ACT != ACT_NONE) gr[k] = float2{0.f, 0.f};   // padding stays zero
         if (i < nx) {
           if constexpr (KS == 1) {
             const int r = i / (PXC / 4), c4 = i - r * (PXC / 4), ci = ci0 + r;
-            if (ci < Cin) v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)y0 * Ho + 4 * c4);
+            if (ci < Cin) {
+              v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)y0 * Ho + 4 * c4);
+              if constexpr (ACT != ACT_NONE) gr[k] = a.gn[(size_t)b * Cin + ci];
+            }
           } else {
             const int r = i / q, c4 = i - r * q;
             const int cl = r / G.nr, rr = r - cl * G.nr;
@@ -126,6 +150,7 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
                 v = f32x4{sv.x, sv.x, sv.y, sv.y};
               } else {
                 v = *(const f32x4*)(chan_ptr(a, b, ci) + (size_t)vy * Ho + 4 * c4);
+                if constexpr (ACT != ACT_NONE) gr[k] = a.gn[(size_t)b * Cin + ci];
               }
             }
           }
@@ -145,13 +170,15 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
       for (int k = 0; k < NXR; ++k) {
         const int i = tid + 256 * k;
         if (i < nx) {
+          f32x4 v = xr[k];
+          if constexpr (ACT != ACT_NONE) v = wg_act<ACT>(v, gr[k]);
           if constexpr (KS == 1) {
             const int r = i / (PXC / 4), c4 = i - r * (PXC / 4);
-            *(f32x4*)(xL + r * G.cis + 4 * c4) = xr[k];
+            *(f32x4*)(xL + r * G.cis + 4 * c4) = v;
           } else {
             const int r = i / q, c4 = i - r * q;
             const int cl = r / G.nr, rr = r - cl * G.nr;
-            *(f32x4*)(xL + cl * G.cis + rr * G.roww + 4 + 4 * c4) = xr[k];
+            *(f32x4*)(xL + cl * G.cis + rr * G.roww + 4 + 4 * c4) = v;
           }
         }
       }
@@ -318,27 +345,37 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
   return true;
 }
 
-template <int MODE, int KS, int HO>
+template <int MODE, int KS, int HO, int ACT>
 hipError_t launch_t(const WgArgs& a, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)wgrad_conv_kernel<MODE, KS, HO>,
+    (void)hipFuncSetAttribute((const void*)wgrad_conv_kernel<MODE, KS, HO, ACT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  wgrad_conv_kernel<MODE, KS, HO><<<(unsigned)(a.ntiles * a.nsplit), 256, lds, s>>>(a);
+  wgrad_conv_kernel<MODE, KS, HO, ACT><<<(unsigned)(a.ntiles * a.nsplit), 256, lds, s>>>(a);
   return hipGetLastError();
 }
 
-template <int MODE, int KS>
+template <int MODE, int KS, int ACT>
 hipError_t launch_m(const WgArgs& a, size_t lds, hipStream_t s) {
   switch (a.Ho) {
-    case 16: return launch_t<MODE, KS, 16>(a, lds, s);
-    case 32: return launch_t<MODE, KS, 32>(a, lds, s);
-    case 64: return launch_t<MODE, KS, 64>(a, lds, s);
-    case 128: return launch_t<MODE, KS, 128>(a, lds, s);
+    case 16: return launch_t<MODE, KS, 16, ACT>(a, lds, s);
+    case 32: return launch_t<MODE, KS, 32, ACT>(a, lds, s);
+    case 64: return launch_t<MODE, KS, 64, ACT>(a, lds, s);
+    case 128: return launch_t<MODE, KS, 128, ACT>(a, lds, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+template <int MODE, int KS>
+hipError_t launch_a(const WgArgs& a, int act, size_t lds, hipStream_t s) {
+  if constexpr (MODE == MODE_S1) {
+    if (act == ACT_GN_SILU) return launch_m<MODE, KS, ACT_GN_SILU>(a, lds, s);
+    if (act == ACT_GN) return launch_m<MODE, KS, ACT_GN>(a, lds, s);
+  }
+  if (act != ACT_NONE) return hipErrorInvalidValue;
+  return launch_m<MODE, KS, ACT_NONE>(a, lds, s);
 }
 
 }  // namespace
@@ -352,20 +389,22 @@ size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mod
 }
 
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
-                    int Cout, int ks, int mode, float* dw, int accumulate, void* ws,
-                    size_t ws_bytes, void* stream) {
-  if (!dy || !x || !dw || !ws || Ca < 1 || Cb < 0 || (Cb > 0 && !x2)) return ERTD_EINVAL;
+                    int Cout, int ks, int mode, const float* gn, int act, float* dw, int accumulate,
+                    void* ws, size_t ws_bytes, void* stream) {
+  if (!dy || !x || !dw || !ws || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) || act < ACT_NONE ||
+      act > ACT_GN || (act != ACT_NONE && (!gn || mode != MODE_S1)))
+    return ERTD_EINVAL;
   Plan p;
   if (!plan_of(Ca + Cb, Cout, B, H, ks, mode, &p)) return ERTD_EINVAL;
   if (p.part_floats * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
-  WgArgs a{dy, x, x2, Ca, Cb, Cout, H, p.Ho, p.R, p.ntiles, p.nco, p.nsplit, p.cps, p.nchunks,
-           (float*)ws};
+  WgArgs a{dy, x, x2, Ca, Cb, Cout, H, p.Ho, p.R, (const float2*)gn, p.ntiles, p.nco, p.nsplit,
+           p.cps, p.nchunks, (float*)ws};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  if (ks == 1) e = launch_m<MODE_S1, 1>(a, p.lds, s);
-  else if (mode == MODE_S2) e = launch_m<MODE_S2, 3>(a, p.lds, s);
-  else if (mode == MODE_UP) e = launch_m<MODE_UP, 3>(a, p.lds, s);
-  else e = launch_m<MODE_S1, 3>(a, p.lds, s);
+  if (ks == 1) e = launch_a<MODE_S1, 1>(a, act, p.lds, s);
+  else if (mode == MODE_S2) e = launch_a<MODE_S2, 3>(a, act, p.lds, s);
+  else if (mode == MODE_UP) e = launch_a<MODE_UP, 3>(a, act, p.lds, s);
+  else e = launch_a<MODE_S1, 3>(a, act, p.lds, s);
   if (e != hipSuccess) return (int)e;
   const size_t cols = (size_t)Cout * (Ca + Cb) * ks * ks;
   wgrad_reduce_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>((const float*)ws, p.nsplit, cols,

@@ -121,8 +121,8 @@ SIGNATURES = {
     "ertd_conv_wgrad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
     "ertd_conv_input_grad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
     "ertd_conv_input_grad": (_I, [_VP, _I, _I, _VP, _I, _I, _I, _I, _VP, _I, _VP, ctypes.c_size_t, _VP]),
-    "ertd_conv_wgrad": (_I, [_VP, _VP, _I, _VP, _I, _I, _I, _I, _I, _I, _VP, _I, _VP, ctypes.c_size_t,
-                             _VP]),
+    "ertd_conv_wgrad": (_I, [_VP, _VP, _I, _VP, _I, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _VP,
+                             ctypes.c_size_t, _VP]),
     "ertd_encoder_train_ws_bytes": (_SZ, [_I, _I]),
     "ertd_encoder_train_fwd": (_I, [_VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _SZ, _VP]),
     "ertd_encoder_train_bwd": (_I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),

@@ -85,8 +85,9 @@ class _K:
         return self._ws
 
     # ---- convolution forward / input gradient (ertd_conv2d)
-    def conv(self, x, w, b, xb=None, mode=MODE_S1, ebias=None, res=None):
-        """conv(cat(x, xb)) + b (+ ebias[:, :, None, None]) (+ res); ebias may be a
+    def conv(self, x, w, b, xb=None, mode=MODE_S1, ebias=None, res=None, gn=None, act=0):
+        """conv(act(cat(x, xb))) + b (+ ebias[:, :, None, None]) (+ res); act(v) =
+        v * gn.scale + gn.shift (+ SiLU) applied while staging; ebias may be a
         column block of a wider (B, n) matrix (its row stride is passed)."""
         B, Ca, H, _ = x.shape
         Cb = 0 if xb is None else xb.shape[1]
@@ -96,7 +97,7 @@ class _K:
         n = self.lib.ertd_conv2d_workspace_bytes(Cin, Cout, ks, PREC_FP32)
         ws = self.ws(n)
         _lib.check(self.lib.ertd_conv2d(
-            x.data_ptr(), Ca, _p(xb), Cb, B, H, w.data_ptr(), b.data_ptr(), Cout, ks, mode, None, 0,
+            x.data_ptr(), Ca, _p(xb), Cb, B, H, w.data_ptr(), b.data_ptr(), Cout, ks, mode, _p(gn), act,
             _p(ebias), 0 if ebias is None else ebias.stride(0), _p(res), out.data_ptr(), PREC_FP32,
             ws.data_ptr(), ws.numel(), self.s), "conv2d")
         return out
@@ -139,8 +140,9 @@ class _K:
                                              int(accumulate), self.s), "reduce_rows")
 
     # ---- conv gradients
-    def conv_wgrad(self, dy, xa, xb, ks, mode, out):
-        """out (Cout, Cin, ks, ks) = dL/dW of conv(cat(xa, xb)) (implicit GEMM)."""
+    def conv_wgrad(self, dy, xa, xb, ks, mode, out, gn=None, act=0):
+        """out (Cout, Cin, ks, ks) = dL/dW of conv(act(cat(xa, xb))) (implicit GEMM; the
+        activation applied while staging)."""
         B, Ca, H, _ = xa.shape
         Cb = 0 if xb is None else xb.shape[1]
         Cout = dy.shape[1]
@@ -149,12 +151,14 @@ class _K:
             return False
         ws = self.ws(n)
         _lib.check(self.lib.ertd_conv_wgrad(dy.data_ptr(), xa.data_ptr(), Ca, _p(xb), Cb, B, H, Cout,
-                                            ks, mode, out.data_ptr(), 0, ws.data_ptr(), ws.numel(),
-                                            self.s), "conv_wgrad")
+                                            ks, mode, _p(gn), act, out.data_ptr(), 0, ws.data_ptr(),
+                                            ws.numel(), self.s), "conv_wgrad")
         return True
 
-    def wgrad_im2col(self, dy, xa, xb, ks, mode, out):
+    def wgrad_im2col(self, dy, xa, xb, ks, mode, out, gn=None, act=0):
         """Fallback outside the implicit-GEMM geometry: patch matrix + GEMM."""
+        if act:
+            xa, xb = self.gn_apply(xa, xb, gn, act), None
         B, Ca, H, W = xa.shape
         x = xa
         if xb is not None:
@@ -324,13 +328,13 @@ class _Grads:
             self.k.chan_copy(dx, c0, cd, buf, 0, accumulate=acc)
 
 
-def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True):
-    """Gradients of y = conv(cat(xa, xb)) + bias: weight and bias grads into
-    grads[name.weight / .bias]; returns dL/d cat(xa, xb) (or None)."""
+def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, gn=None, act=0):
+    """Gradients of y = conv(act(cat(xa, xb))) + bias: weight and bias grads into
+    grads[name.weight / .bias]; returns dL/d act(cat(xa, xb)) (or None)."""
     Cout, Cin, ks, _ = w.shape
     dW = k.empty(Cout, Cin, ks, ks)
-    if not k.conv_wgrad(dy, xa, xb, ks, mode, dW):
-        k.wgrad_im2col(dy, xa, xb, ks, mode, dW)
+    if not k.conv_wgrad(dy, xa, xb, ks, mode, dW, gn, act):
+        k.wgrad_im2col(dy, xa, xb, ks, mode, dW, gn, act)
     grads[name + ".weight"] = dW
     db = k.empty(Cout)
     k.chan_sums(dy, out_c=db)
@@ -407,18 +411,20 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
         def resblock(n, xa, xb):
             Cin = xa.shape[1] + (0 if xb is None else xb.shape[1])
             cout = W[n + ".conv1.weight"].shape[0]
+            # the convs apply GroupNorm + SiLU while staging (gn = {scale, shift}):
+            # the activated tensors are never materialized, the weight-gradient
+            # kernel re-applies them the same way
             ss1, mr1 = k.gn_stats(xa, xb, g, W[n + ".norm1.weight"], W[n + ".norm1.bias"])
-            a1 = k.gn_apply(xa, xb, ss1, ACT_GN_SILU)
             eb = eb_all[:, eoff[n]:eoff[n] + cout]
-            h = k.conv(a1, W[n + ".conv1.weight"], W[n + ".conv1.bias"], ebias=eb)
+            h = k.conv(xa, W[n + ".conv1.weight"], W[n + ".conv1.bias"], xb=xb, ebias=eb, gn=ss1,
+                       act=ACT_GN_SILU)
             ss2, mr2 = k.gn_stats(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"])
-            a2 = k.gn_apply(h, None, ss2, ACT_GN_SILU)
             if Cin != cout:
                 sk = k.conv(xa, W[n + ".skip.weight"], W[n + ".skip.bias"], xb=xb)
             else:
                 sk = xa
-            y = k.conv(a2, W[n + ".conv2.weight"], W[n + ".conv2.bias"], res=sk)
-            nodes.append(("res", n, dict(xa=xa, xb=xb, mr1=mr1, a1=a1, h=h, mr2=mr2, a2=a2,
+            y = k.conv(h, W[n + ".conv2.weight"], W[n + ".conv2.bias"], res=sk, gn=ss2, act=ACT_GN_SILU)
+            nodes.append(("res", n, dict(xa=xa, xb=xb, ss1=ss1, mr1=mr1, h=h, ss2=ss2, mr2=mr2,
                                          skip=Cin != cout, y=y)))
             return y
 
@@ -443,8 +449,7 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             C = h.shape[1]
             N = h.shape[2] * h.shape[3]
             ssn, mrn = k.gn_stats(h, None, g, W[n + ".norm.weight"], W[n + ".norm.bias"])
-            an = k.gn_apply(h, None, ssn, ACT_GN)
-            qkv = k.conv(an, W[n + ".qkv.weight"], W[n + ".qkv.bias"]).view(B, 3, C, N)
+            qkv = k.conv(h, W[n + ".qkv.weight"], W[n + ".qkv.bias"], gn=ssn, act=ACT_GN).view(B, 3, C, N)
             q, kk, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
             S = k.empty(B, N, N)    # S[i][j] = sum_c q[c][i] k[c][j]
             k.gemm(q, (1, N, 3 * C * N), kk, (N, 1, 3 * C * N), S, (N, 1, N * N), N, N, C, batch=B)
@@ -453,7 +458,7 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             k.gemm(v, (N, 1, 3 * C * N), P, (1, N, N * N), O, (N, 1, C * N), C, N, N, batch=B)
             O4 = O.view(B, C, h.shape[2], h.shape[3])
             y = k.conv(O4, W[n + ".proj.weight"], W[n + ".proj.bias"], res=h)
-            nodes.append(("attn", n, dict(x=h, mr=mrn, an=an, qkv=qkv, P=P, O=O4, y=y)))
+            nodes.append(("attn", n, dict(x=h, ss=ssn, mr=mrn, qkv=qkv, P=P, O=O4, y=y)))
             h = y
         h = resblock("mid.res2", h, None)
         for i in reversed(range(nl)):
@@ -465,9 +470,8 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
                 nodes.append(("up", f"up.{i}.upsample", dict(x=h, y=y)))
                 h = y
         sso, mro = k.gn_stats(h, None, g, W["norm_out.weight"], W["norm_out.bias"])
-        ao = k.gn_apply(h, None, sso, ACT_GN_SILU)
-        eps = k.conv(ao, W["conv_out.weight"], W["conv_out.bias"])
-        nodes.append(("out", "conv_out", dict(x=h, mr=mro, a=ao, y=eps)))
+        eps = k.conv(h, W["conv_out.weight"], W["conv_out.bias"], gn=sso, act=ACT_GN_SILU)
+        nodes.append(("out", "conv_out", dict(x=h, ss=sso, mr=mro, y=eps)))
     return eps.reshape(B, -1), tape
 
 
@@ -494,7 +498,8 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
             if dy is None:
                 raise RuntimeError(f"ertdiff: no gradient reached {n}")
             if kind == "out":
-                da = _conv_backward(k, grads, n, W[n + ".weight"], d["a"], None, dy, MODE_S1)
+                da = _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, MODE_S1,
+                                    gn=d["ss"], act=ACT_GN_SILU)
                 buf, acc = G.target(d["x"])
                 dg, db = k.gn_backward(d["x"], None, g, W["norm_out.weight"], W["norm_out.bias"],
                                        d["mr"], ACT_GN_SILU, da, buf, None, acc)
@@ -531,8 +536,9 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                        N, batch=B)
                 k.gemm(q, (N, 1, 3 * C * N), dS, (N, 1, N * N), dqkv[:, 1], (N, 1, 3 * C * N), C, N,
                        N, batch=B)
-                dan = _conv_backward(k, grads, n + ".qkv", W[n + ".qkv.weight"], d["an"], None,
-                                     dqkv.view(B, 3 * C, x.shape[2], x.shape[3]), MODE_S1)
+                dan = _conv_backward(k, grads, n + ".qkv", W[n + ".qkv.weight"], x, None,
+                                     dqkv.view(B, 3 * C, x.shape[2], x.shape[3]), MODE_S1,
+                                     gn=d["ss"], act=ACT_GN)
                 buf, acc = G.target(x)
                 dg, db = k.gn_backward(x, None, g, W[n + ".norm.weight"], W[n + ".norm.bias"],
                                        d["mr"], ACT_GN, dan, buf, None, acc)
@@ -546,8 +552,8 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                     G.add_cat(dxs, xa, xb)
                 else:
                     G.add(xa, dy)
-                da2 = _conv_backward(k, grads, n + ".conv2", W[n + ".conv2.weight"], d["a2"], None,
-                                     dy, MODE_S1)
+                da2 = _conv_backward(k, grads, n + ".conv2", W[n + ".conv2.weight"], d["h"], None,
+                                     dy, MODE_S1, gn=d["ss2"], act=ACT_GN_SILU)
                 h = d["h"]
                 dh = k.empty(*h.shape)
                 dg, db = k.gn_backward(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"],
@@ -556,8 +562,8 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                 # h = conv1(a1) + b1 + emb(ea): the emb grad is dh summed over pixels
                 cout = h.shape[1]
                 k.chan_sums(dh, out_bc=deb_all[:, eoff[n]:eoff[n] + cout])
-                da1 = _conv_backward(k, grads, n + ".conv1", W[n + ".conv1.weight"], d["a1"], None,
-                                     dh, MODE_S1)
+                da1 = _conv_backward(k, grads, n + ".conv1", W[n + ".conv1.weight"], xa, xb,
+                                     dh, MODE_S1, gn=d["ss1"], act=ACT_GN_SILU)
                 dxa, acc_a = G.target(xa)
                 dxb, acc_b = (None, acc_a) if xb is None else G.target(xb)
                 if acc_a != acc_b:     # one accumulate flag per launch: pre-zero the new one

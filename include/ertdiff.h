@@ -408,8 +408,8 @@ int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout
                          int mode, float* dx, int accumulate, void* ws, size_t ws_bytes,
                          void* stream);
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
-                    int Cout, int ks, int mode, float* dw, int accumulate, void* ws,
-                    size_t ws_bytes, void* stream);
+                    int Cout, int ks, int mode, const float* gn, int act, float* dw, int accumulate,
+                    void* ws, size_t ws_bytes, void* stream);
 int ertd_concat(const float* const* srcs, const long long* sizes, int n, float* dst, void* stream);
 /* ertd_split: dsts[k] = alpha * src[sum(sizes[<k]) ...] (the inverse of ertd_concat, scaled):
  *   the data-parallel train step's gradient bucket back into the per-tensor gradients. */

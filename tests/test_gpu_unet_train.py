@@ -165,11 +165,50 @@ def test_conv_wgrad_vs_autograd(Ca, Cb, Cout, H, ks, mode, B, cuda_dev):
     for acc in (0, 1):
         rc = lib.ertd_conv_wgrad(dyd.data_ptr(), xa.data_ptr(), Ca,
                                  None if xb is None else xb.data_ptr(), Cb, B, H, Cout, ks, mode,
-                                 out.data_ptr(), acc, ws.data_ptr(), n, _lib.stream_of(cuda_dev))
+                                 None, 0, out.data_ptr(), acc, ws.data_ptr(), n,
+                                 _lib.stream_of(cuda_dev))
         assert rc == 0
     err = _rel(out, 2 * ref)                    # written, then accumulated once more
     record_error(f"conv_wgrad_{Cin}_{Cout}_{H}_k{ks}_m{mode}", err)
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("Ca,Cb,Cout,H,ks,act,B", [
+    (64, 0, 64, 64, 3, 1, 2),      # conv1 / conv2 / conv_out: GroupNorm + SiLU staged
+    (96, 32, 64, 32, 3, 1, 2),     # decoder conv1 on a concat
+    (256, 0, 768, 16, 1, 2, 2),    # attention qkv: GroupNorm only
+])
+def test_conv_wgrad_fused_activation(Ca, Cb, Cout, H, ks, act, B, cuda_dev):
+    """dL/dW of conv(act(x)) with act(v) = v * scale + shift (+ SiLU) applied by the
+    kernel while staging x (the forward never materializes act(x))."""
+    from ertdiff import _lib
+    g = torch.Generator().manual_seed(Ca + 3 * Cout + H + act)
+    Cin = Ca + Cb
+    x = torch.randn(B, Cin, H, H, generator=g)
+    ss = torch.stack([torch.rand(B, Cin, generator=g) + 0.5, torch.randn(B, Cin, generator=g)], -1)
+    dy = torch.randn(B, Cout, H, H, generator=g)
+    a = x.double() * ss[..., 0, None, None].double() + ss[..., 1, None, None].double()
+    if act == 1:
+        a = F.silu(a)
+    ref = torch.nn.grad.conv2d_weight(a, (Cout, Cin, ks, ks), dy.double(), padding=ks // 2)
+    lib = _lib.lib()
+    n = lib.ertd_conv_wgrad_ws_bytes(Cin, Cout, B, H, ks, 0)
+    ws = torch.empty(n, dtype=torch.uint8, device=cuda_dev)
+    xa = x[:, :Ca].contiguous().to(cuda_dev)
+    xb = x[:, Ca:].contiguous().to(cuda_dev) if Cb else None
+    ssd, dyd = ss.contiguous().to(cuda_dev), dy.to(cuda_dev)
+    out = torch.empty((Cout, Cin, ks, ks), device=cuda_dev)
+    rc = lib.ertd_conv_wgrad(dyd.data_ptr(), xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(),
+                             Cb, B, H, Cout, ks, 0, ssd.data_ptr(), act, out.data_ptr(), 0,
+                             ws.data_ptr(), n, _lib.stream_of(cuda_dev))
+    assert rc == 0
+    err = _rel(out, ref)
+    record_error(f"conv_wgrad_act{act}_{Cin}_{Cout}_{H}_k{ks}", err)
+    assert err < 1e-5, err
+    # an activation needs its scale/shift and is only fused for stride-1 convs
+    assert lib.ertd_conv_wgrad(dyd.data_ptr(), xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(),
+                               Cb, B, H, Cout, ks, 0, None, act, out.data_ptr(), 0,
+                               ws.data_ptr(), n, _lib.stream_of(cuda_dev)) != 0
 
 
 def test_conv_wgrad_rejects_bad_geometry(cuda_dev):
@@ -178,7 +217,8 @@ def test_conv_wgrad_rejects_bad_geometry(cuda_dev):
     assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 8, 3, 0) == 0       # 8x8 rows: outside
     assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 48, 3, 0) == 0      # not a power of two
     assert lib.ertd_conv_wgrad_ws_bytes(64, 64, 2, 32, 1, 1) == 0      # 1x1 stride 2
-    assert lib.ertd_conv_wgrad(None, None, 1, None, 0, 1, 16, 1, 3, 0, None, 0, None, 0, None) != 0
+    assert lib.ertd_conv_wgrad(None, None, 1, None, 0, 1, 16, 1, 3, 0, None, 0, None, 0, None, 0,
+                               None) != 0
 
 
 def test_unet_autograd_matches_fused_step(cuda_dev):
