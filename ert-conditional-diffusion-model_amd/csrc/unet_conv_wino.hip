@@ -22,18 +22,21 @@
 //   * 8 MFMA waves on v_mfma_f32_16x16x4_f32: wave w = (16-co block w & 3,
 //     32-tile pair w >> 2) keeps ALL 16 xi of its 16 co x 32 tiles (2 x 16
 //     accumulators of 4 VGPRs = 128), so the output transform needs no data
-//     of any other wave; inside the K loop it only reads LDS (per xi and
-//     4-channel k-step: one ds_read_b32 of U, two of V, 2 MFMAs);
+//     of any other wave; inside the K loop it only reads LDS (per xi: one
+//     ds_read_b64 of U, two of V, 4 MFMAs);
 //     They also LDS-DMA the weights U (pre-transformed at pack time in
-//     fragment order: [xi 16][k-step 2][co block 4][k 4][co 16] = 32 KB per
+//     fragment order: [xi 16][co block 4][k 4][co 16][k-step 2] = 32 KB per
 //     chunk) two chunks ahead into a 3-slot ring;
-//   * 4 producer waves: the input transform -- lane = tile, 2 channels per
-//     wave: the two middle columns of the tile's 4x4 window are loaded three
-//     chunks ahead into two register sets (one float2 per row, with the
-//     channels' GroupNorm scale/shift), GroupNorm+SiLU applied, the outer
-//     columns taken from the neighbouring lanes (DPP wave shifts), transformed
-//     and written as V [xi][k-step 2][tile block 4][k 4][tile 16] (32 KB,
-//     double-buffered).
+//   * 4 producer waves: the input transform -- lane = tile, wave q owns the
+//     channel pair (2q, 2q+1) = (k-step 0, k-step 1) of MFMA row k = q: the
+//     two middle columns of the tile's 4x4 window are loaded four chunks
+//     ahead into three register sets (one float2 per row, with the channels'
+//     GroupNorm scale/shift), GroupNorm+SiLU applied, the outer columns taken
+//     from the neighbouring lanes (DPP wave shifts), transformed -- both
+//     channels at once in packed fp32 (v_pk_*) -- and written as
+//     V [xi][tile block 4][k 4][tile 16][k-step 2] (32 KB, double-buffered):
+//     one ds_write_b64 per xi, and one ds_read_b64 per xi and operand on the
+//     MFMA side feeds both k-steps.
 //   With 3 waves per SIMD (2 MFMA + 1 producer) the hardware interleaves the
 //   producer's VALU / memory work with the MFMA waves' matrix-pipe time; one
 //   barrier per chunk.
@@ -61,7 +64,11 @@ constexpr int NUB = 3;                        // U ring depth (DMA two chunks ah
 constexpr int NRS = 3;                        // producer register sets (loads NRS+1 chunks ahead)
 constexpr size_t WLDS = (size_t)(NUB * U_FL + 2 * V_FL) * sizeof(float);   // 160 KB
 constexpr int XIF = WKC * 64;                 // U / V floats per xi (512)
+#ifndef WINO_PD
+#define WINO_PD 2                             // MFMA operand read-ahead (xi)
+#endif
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 
 __device__ __forceinline__ unsigned wlds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
@@ -91,8 +98,7 @@ __device__ __forceinline__ Item item_of(int it, int ncog, int ntblk) {
 
 // DBG (diagnostics only, ERTD_WINO_DBG): bit 0 skips the activation VALU,
 // bit 1 the input loads, bit 2 the weight DMA, bit 3 the MFMAs, bit 4 the
-// producers' transform, bit 5 the MFMA waves' LDS reads, bits 6/7/8 the
-// producers' DPP / padding selects / V stores -- the results are
+// producers' transform, bit 5 the MFMA waves' LDS reads -- the results are
 // wrong, the timings show where a chunk's time goes
 template <int WO, int ACT, int DBG = 0>
 __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, int ksp) {
@@ -121,9 +127,9 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
 
   if (wave >= NMW) {
     // =================== producer waves ===================
-    const int q = wave - NMW;          // channels 2q, 2q+1 of every chunk
-    // V offset of (channel c = 2q + hv, tile t = lane): [xi][c >> 2][t >> 4][c & 3][t & 15]
-    const int vwoff = (q >> 1) * 256 + (lane >> 4) * 64 + (2 * (q & 1)) * 16 + (lane & 15);
+    const int q = wave - NMW;          // channels 2q (k-step 0), 2q+1 (k-step 1) of every chunk
+    // V offset of (channel pair q, tile t = lane): [xi][t >> 4][q][t & 15][k-step]
+    const int vwoff = (lane >> 4) * 128 + q * 32 + (lane & 15) * 2;
     // registers of the chunk in flight: the two middle columns of the 4x4
     // window (one float2 per row) of both channels, their GroupNorm
     // {scale, shift}, and the window's padding masks.  Each lane loads its
@@ -164,67 +170,60 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
         }
       }
     };
+    // both channels of the pair in the two halves of every f32x2: the
+    // arithmetic is the same per channel, so it issues as packed fp32
     auto transform_chunk = [&](const int set, float* vb) {
       if constexpr (DBG & 16) return;
       const unsigned m = msk[set];
+      const f32x2 gs = {gnv[set][0].x, gnv[set][1].x}, gh = {gnv[set][0].y, gnv[set][1].y};
+      const float fl = (m & 16u) ? 1.f : 0.f, fr = (m & 32u) ? 1.f : 0.f;
+      f32x2 d[4][4];
 #pragma unroll
-      for (int hv = 0; hv < 2; ++hv) {
-        float d[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float m0 = raw[set][hv][r].x, m1 = raw[set][hv][r].y;
-          if constexpr (ACT != ACT_NONE && !(DBG & 1)) {
-            m0 = fmaf(m0, gnv[set][hv].x, gnv[set][hv].y);   // ATen's folded GroupNorm
-            m1 = fmaf(m1, gnv[set][hv].x, gnv[set][hv].y);
-            if constexpr (ACT == ACT_GN_SILU) {
-              m0 = m0 * __builtin_amdgcn_rcpf(1.0f + __expf(-m0));
-              m1 = m1 * __builtin_amdgcn_rcpf(1.0f + __expf(-m1));
-            }
-          }
-          // left neighbour's column 2tx-1 (lane t-1's m1), right's 2tx+2 (lane t+1's m0)
-          float lf, rt;
-          if constexpr (DBG & 64) {
-            lf = m1;
-            rt = m0;
-          } else {
-            lf = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m1), 0x138, 0xf, 0xf, false));
-            rt = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m0), 0x130, 0xf, 0xf, false));
-          }
-          // the padding pads the activated tensor
-          if constexpr (DBG & 128) {
-            d[r][0] = lf; d[r][1] = m0; d[r][2] = m1; d[r][3] = rt;
-          } else {
-            const bool rok = (m >> r) & 1u;
-            d[r][0] = (rok && (m & 16u)) ? lf : 0.f;
-            d[r][1] = rok ? m0 : 0.f;
-            d[r][2] = rok ? m1 : 0.f;
-            d[r][3] = (rok && (m & 32u)) ? rt : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        f32x2 m0 = {raw[set][0][r].x, raw[set][1][r].x};
+        f32x2 m1 = {raw[set][0][r].y, raw[set][1][r].y};
+        if constexpr (ACT != ACT_NONE && !(DBG & 1)) {
+          m0 = __builtin_elementwise_fma(m0, gs, gh);   // ATen's folded GroupNorm
+          m1 = __builtin_elementwise_fma(m1, gs, gh);
+          if constexpr (ACT == ACT_GN_SILU) {
+            f32x2 e0 = {__expf(-m0.x), __expf(-m0.y)}, e1 = {__expf(-m1.x), __expf(-m1.y)};
+            e0 = 1.0f + e0;
+            e1 = 1.0f + e1;
+            m0 = m0 * f32x2{__builtin_amdgcn_rcpf(e0.x), __builtin_amdgcn_rcpf(e0.y)};
+            m1 = m1 * f32x2{__builtin_amdgcn_rcpf(e1.x), __builtin_amdgcn_rcpf(e1.y)};
           }
         }
-        float tm[4][4];   // B^T d
+        // the padding pads the activated tensor: rows outside the image and
+        // the outer columns at the image's left / right edge are zero
+        const float fy = ((m >> r) & 1u) ? 1.f : 0.f;
+        m0 = m0 * fy;
+        m1 = m1 * fy;
+        // left neighbour's column 2tx-1 (lane t-1's m1), right's 2tx+2 (lane t+1's m0)
+        f32x2 lf, rt;
+        lf.x = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m1.x), 0x138, 0xf, 0xf, true));
+        lf.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m1.y), 0x138, 0xf, 0xf, true));
+        rt.x = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m0.x), 0x130, 0xf, 0xf, true));
+        rt.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m0.y), 0x130, 0xf, 0xf, true));
+        d[r][0] = lf * fl;
+        d[r][1] = m0;
+        d[r][2] = m1;
+        d[r][3] = rt * fr;
+      }
+      f32x2 tm[4][4];   // B^T d
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          tm[0][s] = d[0][s] - d[2][s];
-          tm[1][s] = d[1][s] + d[2][s];
-          tm[2][s] = d[2][s] - d[1][s];
-          tm[3][s] = d[1][s] - d[3][s];
-        }
-        float* o = vb + vwoff + hv * 16;
-        if constexpr (DBG & 256) {
-          float t = 0.f;
+      for (int s = 0; s < 4; ++s) {
+        tm[0][s] = d[0][s] - d[2][s];
+        tm[1][s] = d[1][s] + d[2][s];
+        tm[2][s] = d[2][s] - d[1][s];
+        tm[3][s] = d[1][s] - d[3][s];
+      }
+      float* o = vb + vwoff;
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            t += (tm[i][0] - tm[i][2]) + (tm[i][1] + tm[i][2]) + (tm[i][2] - tm[i][1]) + (tm[i][1] - tm[i][3]);
-          o[0] = t;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {   // (B^T d) B
-            o[(4 * i + 0) * XIF] = tm[i][0] - tm[i][2];
-            o[(4 * i + 1) * XIF] = tm[i][1] + tm[i][2];
-            o[(4 * i + 2) * XIF] = tm[i][2] - tm[i][1];
-            o[(4 * i + 3) * XIF] = tm[i][1] - tm[i][3];
-          }
-        }
+      for (int i = 0; i < 4; ++i) {   // (B^T d) B
+        *reinterpret_cast<f32x2*>(o + (4 * i + 0) * XIF) = tm[i][0] - tm[i][2];
+        *reinterpret_cast<f32x2*>(o + (4 * i + 1) * XIF) = tm[i][1] + tm[i][2];
+        *reinterpret_cast<f32x2*>(o + (4 * i + 2) * XIF) = tm[i][2] - tm[i][1];
+        *reinterpret_cast<f32x2*>(o + (4 * i + 3) * XIF) = tm[i][1] - tm[i][3];
       }
     };
 
@@ -264,6 +263,9 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
   }
 
   // =================== MFMA waves ===================
+#ifdef WINO_PRIO
+  __builtin_amdgcn_s_setprio(WINO_PRIO);   // issue ahead of the producer on a shared SIMD
+#endif
   const int cb = wave & 3, tbp = wave >> 2;
   // operands: U at cb*64 + lane, V at (2 tbp)*64 + lane (+64: second tile
   // block), + xi*XIF + s*256 (derived per chunk in the K loop)
@@ -312,42 +314,45 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
       // U DMA just issued for chunk g + 2 -- every chunk
       int ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-      const float* ub = ubuf + (g % NUB) * U_FL + cb * 64 + ln;
-      const float* vb = vbuf + (g & 1) * V_FL + (2 * tbp) * 64 + ln;
-      // 32 steps (k-step st = s >> 4 of 4 channels, xi = s & 15): operands
-      // read 3 steps ahead into a 4-deep register ring, each step's three
-      // ds_reads grouped with the two MFMAs of an earlier step (the compiler
+      const float* ub = ubuf + (g % NUB) * U_FL + cb * 128 + 2 * ln;
+      const float* vb = vbuf + (g & 1) * V_FL + (2 * tbp) * 128 + 2 * ln;
+      // 16 xi: one ds_read_b64 per operand gives both k-steps (4 MFMAs per
+      // xi); operands read PD xi ahead into a register ring, each xi's three
+      // ds_reads grouped with the MFMAs of an earlier xi (the compiler
       // otherwise spends the few free registers on A operands and waits a
-      // full LDS latency before every MFMA pair)
-      constexpr int NS = 2 * 16, PD = 3;
-      float ra[4], rb0[4], rb1[4];
-      auto ld = [&](const int s2) {
-        const int st = s2 >> 4, x = s2 & 15, r = s2 & 3;
+      // full LDS latency before every MFMA group)
+      constexpr int PD = WINO_PD;
+      f32x2 ra[PD + 1], rb0[PD + 1], rb1[PD + 1];
+      auto ld = [&](const int x) {
+        const int r = x % (PD + 1);
         if constexpr (DBG & 32) {
-          ra[r] = (float)(lane + x + st);
-          rb0[r] = (float)(lane - x + k);
+          ra[r] = f32x2{(float)(lane + x), (float)(lane - x)};
+          rb0[r] = f32x2{(float)(lane - x + k), (float)x};
           rb1[r] = rb0[r] + 1.f;
         } else {
-          ra[r] = ub[x * XIF + st * 256];
-          rb0[r] = vb[x * XIF + st * 256];
-          rb1[r] = vb[x * XIF + st * 256 + 64];
+          ra[r] = *reinterpret_cast<const f32x2*>(ub + x * XIF);
+          rb0[r] = *reinterpret_cast<const f32x2*>(vb + x * XIF);
+          rb1[r] = *reinterpret_cast<const f32x2*>(vb + x * XIF + 128);
         }
       };
 #pragma unroll
-      for (int s2 = 0; s2 < PD; ++s2) ld(s2);
+      for (int x = 0; x < PD; ++x) ld(x);
 #pragma unroll
-      for (int s2 = 0; s2 < NS; ++s2) {
-        if (s2 + PD < NS) ld(s2 + PD);
-        const int x = s2 & 15, r = s2 & 3;
-        if constexpr (DBG & 8) {
-          acc[x][0][0] += ra[r] * rb0[r];
-          acc[x][1][0] += ra[r] * rb1[r];
-        } else {
-          acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[r], rb0[r], acc[x][0], 0, 0, 0);
-          acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[r], rb1[r], acc[x][1], 0, 0, 0);
+      for (int x = 0; x < 16; ++x) {
+        if (x + PD < 16) ld(x + PD);
+        const int r = x % (PD + 1);
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          if constexpr (DBG & 8) {
+            acc[x][0][0] += ra[r][st] * rb0[r][st];
+            acc[x][1][0] += ra[r][st] * rb1[r][st];
+          } else {
+            acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[r][st], rb0[r][st], acc[x][0], 0, 0, 0);
+            acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[r][st], rb1[r][st], acc[x][1], 0, 0, 0);
+          }
         }
-        if (s2 + PD < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS reads
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                      // MFMAs
+        if (x + PD < 16) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                     // MFMAs
       }
       // keep the chunk's MFMAs ahead of the barrier (hipcc would sink them:
       // they touch no memory)
@@ -489,10 +494,7 @@ hipError_t launch_wo(const ConvArgs& a, int B, hipStream_t s) {
       case 8: return launch_wod<WO, ACT, 8>(a, B, s);
       case 7: return launch_wod<WO, ACT, 7>(a, B, s);
       case 16: return launch_wod<WO, ACT, 16>(a, B, s);
-      case 64: return launch_wod<WO, ACT, 64>(a, B, s);
-      case 128: return launch_wod<WO, ACT, 128>(a, B, s);
-      case 256: return launch_wod<WO, ACT, 256>(a, B, s);
-      case 448: return launch_wod<WO, ACT, 448>(a, B, s);
+      case 32: return launch_wod<WO, ACT, 32>(a, B, s);
       case 23: return launch_wod<WO, ACT, 23>(a, B, s);
       case 55: return launch_wod<WO, ACT, 55>(a, B, s);
       default: break;
@@ -512,25 +514,25 @@ hipError_t launch_act(const ConvArgs& a, int B, hipStream_t s) {
   }
 }
 
-// ---- packing: W (Cout, Cin, 3, 3) -> U = G g G^T in [cog][chunk][xi][st][cb][kk][c16]
-// (computed in float64, rounded once): the A-operand fragment of
-// v_mfma_f32_16x16x4_f32 for co block cb (16 co) and k-step st, lane l =
-// 16 kk + c16 -> co = 16 cb + c16, channel 4 st + kk of the chunk
+// ---- packing: W (Cout, Cin, 3, 3) -> U = G g G^T in [cog][chunk][xi][cb][kk][c16][st]
+// (computed in float64, rounded once): the A-operand fragments of
+// v_mfma_f32_16x16x4_f32 for co block cb (16 co), both k-steps st in one
+// float2, lane l = 16 kk + c16 -> co = 16 cb + c16, channel 2 kk + st of the chunk
 __global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int cout, int nchunk,
                                  size_t total, float* __restrict__ dst, bool flipT) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int c16 = (int)(i & 15);
-  const int kk = (int)((i >> 4) & 3);
-  const int cb = (int)((i >> 6) & 3);
-  const int st = (int)((i >> 8) & 1);
+  const int st = (int)(i & 1);
+  const int c16 = (int)((i >> 1) & 15);
+  const int kk = (int)((i >> 5) & 3);
+  const int cb = (int)((i >> 7) & 3);
   size_t rest = i >> 9;
   const int xi = (int)(rest % 16);
   rest /= 16;
   const int k = (int)(rest % nchunk);
   const int cog = (int)(rest / nchunk);
   const int co = cog * 64 + cb * 16 + c16;
-  const int ci = k * WKC + 4 * st + kk;
+  const int ci = k * WKC + 2 * kk + st;
   const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   const int ri = xi >> 2, rj = xi & 3;
   // flipT: w is the forward conv's (cin, cout, 3, 3) weight; pack the input-
