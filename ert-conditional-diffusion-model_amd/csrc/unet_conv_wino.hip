@@ -132,41 +132,66 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
     const int vwoff = (lane >> 4) * 128 + q * 32 + (lane & 15) * 2;
     // registers of the chunk in flight: the two middle columns of the 4x4
     // window (one float2 per row) of both channels, their GroupNorm
-    // {scale, shift}, and the window's padding masks.  Each lane loads its
-    // tile's middle columns; the outer columns are the neighbouring tiles'
-    // (lanes t-1 / t+1) by DPP wave shifts -- across a tile-row boundary they
-    // are padding (masked), so the shifted-in neighbour never matters there.
+    // {scale, shift}, and the window's padding as 0 / 1 factors.  Each lane
+    // loads its tile's middle columns; the outer columns are the neighbouring
+    // tiles' (lanes t-1 / t+1) by DPP wave shifts -- across a tile-row
+    // boundary they are padding (masked), so the shifted-in neighbour never
+    // matters there.  Only rows 0 / 3 of a window can fall outside the image.
     float2 raw[NRS][2][4];   // [register set][channel][row]
-    float2 gnv[NRS][2];
-    unsigned msk[NRS] = {};   // bits 0-3: row r valid, bit 4: left column, bit 5: right column
-    auto load_chunk = [&](const int set, int g) {
-      const int il = g / nck, it = bid + il * G;
-      const int k = (it % ksp) * nck + (g - il * nck);
+    f32x4 gnv[NRS];          // {scale, shift} of channel 2q, then 2q+1
+    f32x4 pad[NRS];          // row 0, row 3, left column, right column
+    // the loads walk this workgroup's chunks in order (a cursor; the item's
+    // geometry is derived once per item, not per chunk)
+    int cur_g = 0, cur_k = 0, cur_k0 = 0, cur_b = 0, cur_il = 0;
+    unsigned roff[4];        // byte offsets of the window's rows (global_load saddr + voffset)
+    f32x4 cur_pad;
+    auto set_item = [&](int il) {
+      const int it = bid + il * G;
+      cur_k0 = (it % ksp) * nck;
       const Item itm = item_of(it / ksp, ncog, NTBLK);
+      cur_b = itm.b;
       const int tg = itm.tblk * 64 + lane;
       const int ty = tg / TPR, tx = tg - ty * TPR;
-      unsigned m = (tx > 0 ? 16u : 0u) | (tx < TPR - 1 ? 32u : 0u);
-      int roff[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int iy = 2 * ty - 1 + r;
-        const bool ok = iy >= 0 && iy < WO;
-        m |= ok ? (1u << r) : 0u;
-        roff[r] = (ok ? iy : 0) * WO + 2 * tx;
+        roff[r] = (unsigned)(((iy >= 0 && iy < WO ? iy : 2 * ty) * WO + 2 * tx) * 4);
       }
-      msk[set] = m;
+      cur_pad = f32x4{ty > 0 ? 1.f : 0.f, ty < TPR - 1 ? 1.f : 0.f, tx > 0 ? 1.f : 0.f,
+                      tx < TPR - 1 ? 1.f : 0.f};
+    };
+    const int glast = gtot - 1;
+    // load the cursor's chunk into a register set and advance (past the last
+    // chunk it stays put: the extra loads re-load the last chunk, unused, so
+    // the steady-state loop has no conditional loads)
+    auto load_next = [&](const int set) {
+      const int cg = (cur_k0 + cur_k) * WKC + 2 * q;    // wave-uniform, channels cg, cg + 1
+      pad[set] = cur_pad;
+      if constexpr (ACT != ACT_NONE) gnv[set] = *reinterpret_cast<const f32x4*>(a.gn + (size_t)cur_b * Cin + cg);
+      if constexpr (DBG & 2) {
 #pragma unroll
-      for (int hv = 0; hv < 2; ++hv) {
-        const int cg = k * WKC + 2 * q + hv;    // wave-uniform
-        if constexpr (ACT != ACT_NONE) gnv[set][hv] = a.gn[(size_t)itm.b * Cin + cg];
-        if constexpr (DBG & 2) {
+        for (int hv = 0; hv < 2; ++hv)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) raw[set][hv][r] = make_float2((float)(r + k), (float)hv);
-        } else {
-          const float* p = cg < Ca ? a.srcA + ((size_t)itm.b * Ca + cg) * HW
-                                   : a.srcB + ((size_t)itm.b * a.Cb + (cg - Ca)) * HW;
+          for (int r = 0; r < 4; ++r) raw[set][hv][r] = make_float2((float)(r + cur_k), (float)hv);
+      } else {
+        const float* p = cg < Ca ? a.srcA + ((size_t)cur_b * Ca + cg) * HW
+                                 : a.srcB + ((size_t)cur_b * a.Cb + (cg - Ca)) * HW;
+        // buffer loads: the channel pair's base in SGPRs, the row offset in one VGPR
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 2 * HW * 4, 0x00020000);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) raw[set][hv][r] = *reinterpret_cast<const float2*>(p + roff[r]);
+        for (int hv = 0; hv < 2; ++hv)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)roff[r], hv * HW * 4, 0);
+            raw[set][hv][r] = make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+          }
+      }
+      if (cur_g < glast) {
+        ++cur_g;
+        if (++cur_k == nck) {
+          cur_k = 0;
+          set_item(++cur_il);
         }
       }
     };
@@ -174,9 +199,8 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
     // arithmetic is the same per channel, so it issues as packed fp32
     auto transform_chunk = [&](const int set, float* vb) {
       if constexpr (DBG & 16) return;
-      const unsigned m = msk[set];
-      const f32x2 gs = {gnv[set][0].x, gnv[set][1].x}, gh = {gnv[set][0].y, gnv[set][1].y};
-      const float fl = (m & 16u) ? 1.f : 0.f, fr = (m & 32u) ? 1.f : 0.f;
+      const f32x2 gs = {gnv[set].x, gnv[set].z}, gh = {gnv[set].y, gnv[set].w};
+      const float fl = pad[set].z, fr = pad[set].w;
       f32x2 d[4][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -195,9 +219,11 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
         }
         // the padding pads the activated tensor: rows outside the image and
         // the outer columns at the image's left / right edge are zero
-        const float fy = ((m >> r) & 1u) ? 1.f : 0.f;
-        m0 = m0 * fy;
-        m1 = m1 * fy;
+        if (r == 0 || r == 3) {
+          const float fy = r == 0 ? pad[set].x : pad[set].y;
+          m0 = m0 * fy;
+          m1 = m1 * fy;
+        }
         // left neighbour's column 2tx-1 (lane t-1's m1), right's 2tx+2 (lane t+1's m0)
         f32x2 lf, rt;
         lf.x = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m1.x), 0x138, 0xf, 0xf, true));
@@ -236,19 +262,18 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
     // alone.)  Loads past the last chunk re-load the last one (clamped,
     // unused): the steady-state loop has no conditional loads, and the
     // compiler's vmcnt bookkeeping across its back edge stays exact.
-    const int glast = gtot - 1;
-    auto clampg = [&](int g) { return g < glast ? g : glast; };
     auto slot = [&](const int set, int g) {   // set = (g + 1) % NRS
       transform_chunk(set, vbuf + ((g + 1) & 1) * V_FL);
-      load_chunk(set, clampg(g + 1 + NRS));
+      load_next(set);    // chunk g + 1 + NRS
       __syncthreads();   // (B) end of slot g
     };
     if (gtot > 0) {
-      load_chunk(0, 0);
-      load_chunk(1, clampg(1));
-      load_chunk(2, clampg(2));
+      set_item(0);
+      load_next(0);
+      load_next(1);
+      load_next(2);
       transform_chunk(0, vbuf);
-      load_chunk(0, clampg(3));
+      load_next(0);
     }
     __syncthreads();   // (A) chunk 0 staged
     int g = 0;
