@@ -98,7 +98,8 @@ __device__ __forceinline__ Item item_of(int it, int ncog, int ntblk) {
 
 // DBG (diagnostics only, ERTD_WINO_DBG): bit 0 skips the activation VALU,
 // bit 1 the input loads, bit 2 the weight DMA, bit 3 the MFMAs, bit 4 the
-// producers' transform, bit 5 the MFMA waves' LDS reads -- the results are
+// producers' transform, bit 5 the MFMA waves' LDS reads, bit 6 the output
+// transform and stores (all but one value per lane) -- the results are
 // wrong, the timings show where a chunk's time goes
 template <int WO, int ACT, int DBG = 0>
 __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, int ksp) {
@@ -391,34 +392,46 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
     // ---- output transform of this wave's 16 co x 32 tiles, in registers:
     // lane l holds M[xi] of co = 16 cb + 4 (l >> 4) + i (acc element i) and
     // tile 16 j + (l & 15) of its tile pair (accumulator j)
+    if constexpr (DBG & 64) {   // no output transform / stores
+      if (il == nloc - 1)
+        for (int x = 0; x < 16; ++x) a.out[(size_t)bid * 64 + lane] += acc[x][0][0] + acc[x][1][1];
+      continue;
+    }
     const int itg = bid + il * G;
     const Item itm = item_of(itg / ksp, ncog, NTBLK);
     const bool part2 = (itg % ksp) != 0;   // second K half: raw partial sum only
-    const float* ebp = (a.ebias && !part2) ? a.ebias + (size_t)itm.b * a.eb_stride : nullptr;
-    const float* resp = part2 ? nullptr : a.res;
-    float* outp = part2 ? a.ksplit_buf : a.out;
-    float bias[4], eb[4];
-    int co[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      co[i] = itm.cog * 64 + cb * 16 + 4 * (lane >> 4) + i;
-      bias[i] = (a.bias && !part2) ? a.bias[co[i]] : 0.f;
-      eb[i] = ebp ? ebp[co[i]] : 0.f;
-    }
+    // wave-uniform flags (a per-lane null test on a derived pointer made the
+    // compiler mask every load)
+    const bool has_eb = a.ebias && !part2, has_res = a.res && !part2, has_bias = a.bias && !part2;
+    // buffer loads / stores: the sample's base in SGPRs, one 32-bit offset
+    // per tile block (64-bit addresses per store spilled)
+    const unsigned smp = (unsigned)(a.Cout * HW * 4);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (part2 ? a.ksplit_buf : a.out) + (size_t)itm.b * a.Cout * HW, (short)0, smp, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        has_res ? const_cast<float*>(a.res) + (size_t)itm.b * a.Cout * HW : nullptr, (short)0, smp, 0x00020000);
+    // a fresh lane id (as in the K loop): lane-derived values held across the
+    // loop were spilled, and each reload's vmcnt(0) waited for this item's
+    // stores
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const int co0 = itm.cog * 64 + cb * 16 + 4 * (ln >> 4);
+    int vo[2];   // byte offset of (co0, the tile's top-left pixel)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int tg = itm.tblk * 64 + (2 * tbp + j) * 16 + (lane & 15);
+      const int tg = itm.tblk * 64 + (2 * tbp + j) * 16 + (ln & 15);
       const int ty = tg / TPR, tx = tg - ty * TPR;
-      const size_t pix = (size_t)(2 * ty) * WO + 2 * tx;
-      float* outb = outp + (size_t)itm.b * a.Cout * HW + pix;
-      const float* resb = resp ? resp + (size_t)itm.b * a.Cout * HW + pix : nullptr;
-      float2 rv[4][2];
+      vo[j] = (co0 * HW + 2 * ty * WO + 2 * tx) * 4;
+    }
+    float bias[4], eb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-          rv[i][y] = resb ? *reinterpret_cast<const float2*>(resb + (size_t)co[i] * HW + y * WO)
-                          : make_float2(0.f, 0.f);
+    for (int i = 0; i < 4; ++i) {
+      bias[i] = has_bias ? a.bias[co0 + i] : 0.f;
+      eb[i] = has_eb ? a.ebias[(size_t)itm.b * a.eb_stride + co0 + i] : 0.f;
+    }
+    // Y = A^T (M A) of tile block j, then the spec's op order: conv + bias,
+    // + emb (the residual is added by the caller)
+    auto out_tile = [&](const int j, f32x2 (&y)[4][2]) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float Pm[4][2];   // P = M A, per row of M
@@ -429,22 +442,49 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
           Pm[r][0] = (m0 + m1) + m2;
           Pm[r][1] = (m1 - m2) - m3;
         }
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          float v[2];
-#pragma unroll
-          for (int x = 0; x < 2; ++x) {
-            // Y = A^T P, then the spec's op order: conv + bias, + emb, + residual
-            float t = y == 0 ? (Pm[0][x] + Pm[1][x]) + Pm[2][x] : (Pm[1][x] - Pm[2][x]) - Pm[3][x];
-            t = t + bias[i];
-            if (ebp) t = t + eb[i];
-            if (resb) t = t + (x == 0 ? rv[i][y].x : rv[i][y].y);
-            v[x] = t;
-          }
-          *reinterpret_cast<float2*>(outb + (size_t)co[i] * HW + y * WO) = make_float2(v[0], v[1]);
+        y[i][0] = f32x2{(Pm[0][0] + Pm[1][0]) + Pm[2][0], (Pm[0][1] + Pm[1][1]) + Pm[2][1]} + bias[i];
+        y[i][1] = f32x2{(Pm[1][0] - Pm[2][0]) - Pm[3][0], (Pm[1][1] - Pm[2][1]) - Pm[3][1]} + bias[i];
+        if (has_eb) {
+          y[i][0] = y[i][0] + eb[i];
+          y[i][1] = y[i][1] + eb[i];
         }
       }
+    };
+    auto store_tile = [&](const int j, const f32x2 (&y)[4][2]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, y[i][r]),
+                                                ro, vo[j] + r * WO * 4, i * HW * 4, 0);
+    };
+    // all outputs first (frees the accumulators), then the residual of both
+    // tile blocks into the freed registers, then the stores: no load is
+    // issued after a store (loads and stores share vmcnt, so it would wait
+    // for the store)
+    f32x2 y[2][4][2];
+    out_tile(0, y[0]);
+    out_tile(1, y[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_res) {
+      f32x2 rv[2][4][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+            rv[j][i][r] = __builtin_bit_cast(
+                f32x2, __builtin_amdgcn_raw_buffer_load_b64(rr, vo[j] + r * WO * 4, i * HW * 4, 0));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 2; ++r) y[j][i][r] = y[j][i][r] + rv[j][i][r];
     }
+    store_tile(0, y[0]);
+    store_tile(1, y[1]);
   }
 }
 
@@ -520,6 +560,7 @@ hipError_t launch_wo(const ConvArgs& a, int B, hipStream_t s) {
       case 7: return launch_wod<WO, ACT, 7>(a, B, s);
       case 16: return launch_wod<WO, ACT, 16>(a, B, s);
       case 32: return launch_wod<WO, ACT, 32>(a, B, s);
+      case 64: return launch_wod<WO, ACT, 64>(a, B, s);
       case 23: return launch_wod<WO, ACT, 23>(a, B, s);
       case 55: return launch_wod<WO, ACT, 55>(a, B, s);
       default: break;
