@@ -69,7 +69,11 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smemh[];
   char* wim = smemh;                          // [2][WBB]
   char* xim = smemh + 2 * G::WBB;             // [2][XB]
-  float2* gtab = reinterpret_cast<float2*>(smemh + 2 * G::WBB + 2 * G::XB);
+  // {bias, emb} of the workgroup's 64 output channels (read by the epilogue
+  // from LDS: its only global loads are then the residual's), then the
+  // GroupNorm table
+  float2* etab = reinterpret_cast<float2*>(smemh + G::LDS);
+  float2* gtab = reinterpret_cast<float2*>(smemh + G::LDS + 64 * sizeof(float2));
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -86,6 +90,12 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
 
   if constexpr (ACT != ACT_NONE) {
     for (int c = tid; c < Cin; c += NTHR) gtab[c] = a.gn[(size_t)b * Cin + c];
+  }
+  if (tid < 64) {
+    const int co = blockIdx.y * 64 + tid;
+    const bool ok = co < a.Cout;
+    etab[tid] = make_float2(ok && a.bias ? a.bias[co] : 0.f,
+                            ok && a.ebias ? a.ebias[(size_t)b * a.eb_stride + co] : 0.f);
   }
   if constexpr (PRE) {
     // every LDS image byte starts at zero: halo columns and out-of-image rows
@@ -280,44 +290,42 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue (as unet_conv.hip): 8-row phases, loads before stores
+  // ---- epilogue: every residual value of the tile is loaded before any
+  // store (loads and stores share vmcnt: a load after a store would wait for
+  // it), bias / emb from LDS
   constexpr int HWo = WO * WO;
   const size_t lbase0 = (size_t)b * a.Cout * HWo + p0 + wave * 32 * TPX + l32;
   const float* __restrict__ resp = a.res ? a.res + lbase0 : nullptr;
   float* __restrict__ outp = a.out + lbase0;
-  const float* ebp = a.ebias ? a.ebias + (size_t)b * a.eb_stride : nullptr;
+  const bool has_eb = a.ebias != nullptr;
+  float rv[2][16][TPX];
+  if (resp) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-      float bias[8], eb[8], rv[8][TPX];
-      int off[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int r = ph * 8 + q;
+      for (int r = 0; r < 16; ++r) {
         int co = (tile_wg + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         co = co < a.Cout ? co : a.Cout - 1;
-        off[q] = co * HWo;
-        bias[q] = a.bias ? a.bias[co] : 0.f;
-        eb[q] = ebp ? ebp[co] : 0.f;
 #pragma unroll
-        for (int t = 0; t < TPX; ++t) rv[q][t] = resp ? resp[off[q] + t * 32] : 0.f;
+        for (int t = 0; t < TPX; ++t) rv[i][r][t] = resp[(size_t)co * HWo + t * 32];
       }
+  }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int r = ph * 8 + q;
-        const int co = (tile_wg + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (co >= a.Cout) continue;
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int t = 0; t < TPX; ++t) {
-          float v = acc[i][t][r] + bias[q];
-          if (ebp) v = v + eb[q];
-          if (resp) v = v + rv[q][t];
-          outp[off[q] + t * 32] = v;
-        }
+    for (int r = 0; r < 16; ++r) {
+      const int cl = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int co = tile_wg * 32 + cl;
+      if (co >= a.Cout) continue;
+      const float2 e = etab[cl];
+#pragma unroll
+      for (int t = 0; t < TPX; ++t) {
+        float v = acc[i][t][r] + e.x;
+        if (has_eb) v = v + e.y;
+        if (resp) v = v + rv[i][r][t];
+        outp[(size_t)co * HWo + t * 32] = v;
       }
     }
-  }
 }
 
 // The input transform of the PRE path: x (srcA | srcB, fp32 NCHW) -> GN/SiLU
@@ -517,7 +525,7 @@ size_t conv_bf16_image_bytes(int cin, int B, int H, int W) {
 template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false>
 static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
   using G = GeomH<KS, MODE, WO, TPX>;
-  const size_t lds = G::LDS + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
+  const size_t lds = G::LDS + 64 * sizeof(float2) + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE>,
