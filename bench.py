@@ -744,12 +744,14 @@ def main():
     traffic = _traffic(f"unet_{a.unet}_B{B}_fp32_step")
     ex_flop_step = flops["conv_executed_fp32"] * B
     ex_tf = ex_flop_step / (ev_s / a.steps) / 1e12
-    roof = {"kernel": "conv_wino_kernel (ResBlock 3x3, Winograd F(2x2,3x3)) + conv_kernel (the other "
-                      "convs): all convs of one U-Net step",
+    roof = {"kernel": "conv_wino4_kernel (ResBlock 3x3 at 64x64 / 32x32, Winograd F(4x4,3x3)) + "
+                      "conv_wino_kernel (16x16, F(2x2,3x3)) + conv_kernel (the other convs): all "
+                      "convs of one U-Net step",
             "bound": "mfma", "achieved": round(ex_tf, 3), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-            "flop_basis": "EXECUTED MFMA FLOP of one step (Winograd layers at 16/36, sub-pixel "
-                          "Upsample at 4/9 of the direct count) / the step's duration",
+            "flop_basis": "EXECUTED MFMA FLOP of one step (F(4x4) Winograd layers at 36/144, "
+                          "F(2x2) at 16/36, sub-pixel Upsample at 4/9 of the direct count) / the "
+                          "step's duration",
             "executed_flop_per_step": ex_flop_step,
             "avg_us_per_step": round(ev_s / a.steps * 1e6, 1),
             "timing": f"HIP events on the launching stream around {a.steps} replayed step graphs "

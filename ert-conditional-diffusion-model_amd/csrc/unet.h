@@ -45,6 +45,8 @@ struct ConvArgs {
                          // or null (direct implicit GEMM)
   float* ksplit_buf;     // Winograd, optional: (B, Cout, Ho, Wo) scratch that lets a layer with
                          // fewer tile items than CUs split its K (input channels) in two halves
+  const float* wpk_wino4;// fp32 3x3 stride-1 at W >= 32: Winograd F(4x4,3x3) weights
+                         // (launch_pack_conv_wino4), preferred over wpk_wino where eligible
 };
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
@@ -67,6 +69,18 @@ bool conv_wino_ok(int cin, int ca, int cout, int wo);
 // a Winograd layer with this geometry splits its K when given ConvArgs::ksplit_buf
 bool wino_ksplit_wanted(int cin, int cout, int wo, int B);
 size_t conv_packed_floats_wino(int cin, int cout);
+// Winograd F(4x4,3x3) (unet_conv_wino4.hip): Cin, Ca multiples of 4, Cout of 64,
+// W in {32, 64, 128} (16 with an even batch); ERTD_UNET_WINO=2 keeps F(2x2) everywhere.  A Winograd
+// launch (launch_conv_wino) takes it when wino4_ok and ConvArgs::wpk_wino4 is set.
+bool wino4_ok(int cin, int ca, int cout, int wo, int B);
+bool wino_dispatchable(const ConvArgs& a, int B);
+size_t conv_packed_floats_wino4(int cin, int cout);
+hipError_t launch_pack_conv_wino4(const float* w, int cin, int cout, float* dst, hipStream_t s,
+                                  bool flipT = false);
+hipError_t launch_conv_wino4(int act, const ConvArgs& a, int B, hipStream_t s, int cus);
+int wino4_tile_items(int cout, int wo, int B);
+bool wino4_ksplit(int cin, int cout, int wo, int B);
+hipError_t launch_add_inplace(float* out, const float* part, size_t n, hipStream_t s);
 // flipT: w is a forward conv's (cin, cout, 3, 3) weight; pack the input-gradient
 // conv's weight W'[co][ci] = W[ci][co] spatially flipped (training)
 hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s,

@@ -139,6 +139,7 @@ struct Layout {
   std::vector<Param> params;
   std::map<std::string, size_t> off;  // packed offset per parameter name
   std::map<std::string, size_t> offw; // fp32: Winograd-packed copy of eligible 3x3 weights
+  std::map<std::string, size_t> offw4;// ... and the F(4x4,3x3) packing (layers at W >= 32 use it)
   std::map<std::string, int> eboff;   // ResBlock name -> column offset in Wall
   size_t enc = 0, dummy = 0, wall = 0, ball = 0, total = 0;
   int ebtotal = 0;
@@ -181,6 +182,10 @@ Layout layout(const ertd_unet_config* c) {
         conv_packed_floats_wino(p.shape[1], p.shape[0]) > 0) {
       L.offw[p.name] = o;
       o += a64(conv_packed_floats_wino(p.shape[1], p.shape[0]));
+      if (conv_packed_floats_wino4(p.shape[1], p.shape[0]) > 0) {
+        L.offw4[p.name] = o;
+        o += a64(conv_packed_floats_wino4(p.shape[1], p.shape[0]));
+      }
     }
   }
   L.total = o;
@@ -257,7 +262,8 @@ struct Walk {
     if (!out) out = alloc((size_t)B * Cout * Ho * Wo);
     // fp32 Winograd layers with fewer tile items than CUs split their K
     float* kbuf = nullptr;
-    if (c->precision == ERTD_PREC_FP32 && ks == 3 && mode == MODE_S1 && L->offw.count(n + ".weight") &&
+    if (c->precision == ERTD_PREC_FP32 && ks == 3 && mode == MODE_S1 &&
+        (L->offw.count(n + ".weight") || L->offw4.count(n + ".weight")) &&
         conv_wino_ok(Cin, Ca, Cout, Wo) && wino_ksplit_wanted(Cin, Cout, Wo, B))
       kbuf = alloc((size_t)B * Cout * Ho * Wo);
     // bf16 stride-1 convs stage a pre-transformed bf16 copy of their input
@@ -277,6 +283,8 @@ struct Walk {
     {
       const auto it = L->offw.find(n + ".weight");
       a.wpk_wino = it != L->offw.end() ? pk + it->second : nullptr;
+      const auto it4 = L->offw4.find(n + ".weight");
+      a.wpk_wino4 = it4 != L->offw4.end() ? pk + it4->second : nullptr;
     }
     a.bias = P(n + ".bias");
     a.ebias = ebias; a.eb_stride = L->ebtotal;
@@ -611,7 +619,8 @@ size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision) {
   if (precision != ERTD_PREC_BF16 && ks == 3 && conv_packed_floats_up(cin, cout) > f)
     f = conv_packed_floats_up(cin, cout);
   // ... and stride-1 ones carry the Winograd packing behind the direct one
-  if (precision != ERTD_PREC_BF16 && ks == 3) f = a64(f) + conv_packed_floats_wino(cin, cout);
+  if (precision != ERTD_PREC_BF16 && ks == 3)
+    f = a64(f) + std::max(conv_packed_floats_wino(cin, cout), conv_packed_floats_wino4(cin, cout));
   return f * sizeof(float);
 }
 
@@ -630,8 +639,10 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   float* pk = (float*)ws;
   // the Winograd path reads only its own packing: skip the direct one then
   const int Ho_ = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
-  const bool wino = precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
-                    conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho_);
+  const bool wino4 = precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
+                     conv_packed_floats_wino4(Cin, Cout) > 0 && wino4_ok(Cin, Ca, Cout, Ho_, B);
+  const bool wino = wino4 || (precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
+                              conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho_));
   hipError_t e = hipSuccess;
   if (!wino)
     e = precision == ERTD_PREC_BF16 ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s)
@@ -648,8 +659,10 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   void* kbuf = nullptr;
   if (wino) {
     float* pw = pk + a64(std::max(conv_packed_floats(Cin, Cout, ks), conv_packed_floats_up(Cin, Cout)));
-    if ((e = launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess) return (int)e;
-    a.wpk_wino = pw;
+    if ((e = wino4 ? launch_pack_conv_wino4(w, Cin, Cout, pw, s)
+                   : launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess)
+      return (int)e;
+    if (wino4) a.wpk_wino4 = pw; else a.wpk_wino = pw;
     if (wino_ksplit_wanted(Cin, Cout, Ho_, B)) {   // stream-ordered scratch (freed on the stream)
       if ((e = hipMallocAsync(&kbuf, (size_t)B * Cout * Ho_ * Ho_ * sizeof(float), s)) != hipSuccess)
         return rcode(e);
@@ -680,7 +693,8 @@ size_t ertd_conv_input_grad_ws_bytes(int Cin, int Cout, int B, int H, int ks, in
       mode > MODE_UP || (ks == 1 && mode != MODE_S1))
     return 0;
   // packing (either layout) + the zero-inserted dY (stride 2) or the 2H gradient (upsample)
-  size_t n = a64(std::max(conv_packed_floats(Cout, Cin, ks), conv_packed_floats_wino(Cout, Cin)));
+  size_t n = a64(std::max(conv_packed_floats(Cout, Cin, ks),
+                          std::max(conv_packed_floats_wino(Cout, Cin), conv_packed_floats_wino4(Cout, Cin))));
   if (mode == MODE_S2) n += a64((size_t)B * Cout * H * H);
   if (mode == MODE_UP) n += a64((size_t)B * Cin * 4 * H * H);
   const int Hg = mode == MODE_UP ? 2 * H : H;
@@ -696,7 +710,9 @@ int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout
   if (need > ws_bytes) return ERTD_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
   float* pk = (float*)ws;
-  float* scratch = pk + a64(std::max(conv_packed_floats(Cout, Cin, ks), conv_packed_floats_wino(Cout, Cin)));
+  float* scratch = pk + a64(std::max(conv_packed_floats(Cout, Cin, ks),
+                                     std::max(conv_packed_floats_wino(Cout, Cin),
+                                              conv_packed_floats_wino4(Cout, Cin))));
   // the gradient conv: Cin_g = Cout, Cout_g = Cin, at resolution Hg
   const int Hg = mode == MODE_UP ? 2 * H : H;
   const float* src = dy;
@@ -709,12 +725,15 @@ int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout
   a.srcA = src; a.Ca = Cout; a.Cb = 0;
   a.Cin = Cout; a.Cout = Cin;
   a.Hs = a.Ws = a.Ho = a.Wo = Hg;
-  const bool wino = ks == 3 && Cin > 1 && conv_packed_floats_wino(Cout, Cin) > 0 &&
-                    conv_wino_ok(Cout, Cout, Cin, Hg);
-  hipError_t e = wino ? launch_pack_conv_wino(w, Cout, Cin, pk, s, true)
-                      : launch_pack_conv(w, Cout, Cin, ks, pk, s, true);
+  const bool wino4 = ks == 3 && Cin > 1 && conv_packed_floats_wino4(Cout, Cin) > 0 &&
+                     wino4_ok(Cout, Cout, Cin, Hg, B);
+  const bool wino = wino4 || (ks == 3 && Cin > 1 && conv_packed_floats_wino(Cout, Cin) > 0 &&
+                              conv_wino_ok(Cout, Cout, Cin, Hg));
+  hipError_t e = wino4 ? launch_pack_conv_wino4(w, Cout, Cin, pk, s, true)
+                 : wino ? launch_pack_conv_wino(w, Cout, Cin, pk, s, true)
+                        : launch_pack_conv(w, Cout, Cin, ks, pk, s, true);
   if (e != hipSuccess) return (int)e;
-  if (wino) a.wpk_wino = pk; else a.wpk = pk;
+  if (wino4) a.wpk_wino4 = pk; else if (wino) a.wpk_wino = pk; else a.wpk = pk;
   if (wino && wino_ksplit_wanted(Cout, Cin, Hg, B)) {
     const size_t sc = mode == MODE_S2 ? a64((size_t)B * Cout * H * H)
                       : (mode == MODE_UP ? a64((size_t)B * Cin * 4 * H * H) : 0);
@@ -850,6 +869,9 @@ int ertd_unet_pack(const ertd_unet_config* c, const float* const* params, const 
       const auto itw = L.offw.find(p.name);
       if (e == hipSuccess && itw != L.offw.end())
         e = launch_pack_conv_wino(src, p.shape[1], p.shape[0], packed + itw->second, s);
+      const auto itw4 = L.offw4.find(p.name);
+      if (e == hipSuccess && itw4 != L.offw4.end())
+        e = launch_pack_conv_wino4(src, p.shape[1], p.shape[0], packed + itw4->second, s);
     } else if (p.shape.size() == 2) {
       e = launch_transpose(src, p.shape[0], p.shape[1], packed + L.off.at(p.name), p.shape[0], s);
     } else {

@@ -545,8 +545,7 @@ hipError_t launch_wod(const ConvArgs& a, int B, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ksp == 1) return e;
   const size_t n = (size_t)B * a.Cout * WO * WO;
-  add_inplace_kernel<<<(unsigned)((n / 4 + 255) / 256), 256, 0, s>>>(a.out, a.ksplit_buf, n / 4);
-  return hipGetLastError();
+  return launch_add_inplace(a.out, a.ksplit_buf, n, s);
 }
 
 template <int WO, int ACT>
@@ -617,7 +616,32 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int cout,
 
 }  // namespace
 
+hipError_t launch_add_inplace(float* out, const float* part, size_t n, hipStream_t s) {
+  add_inplace_kernel<<<(unsigned)((n / 4 + 255) / 256), 256, 0, s>>>(out, part, n / 4);
+  return hipGetLastError();
+}
+
+// W = 16 takes F(4x4) only when its tile items fill the CUs without a K split
+// (U2 B=64: 128 items; split in two halves it measured no faster than F(2x2))
+bool wino4_ok(int cin, int ca, int cout, int wo, int B) {
+  if (wino_env() != 1 || cin % 4 || ca % 4 || cout % 64) return false;
+  if (wo == 16) return B % 2 == 0 && wino4_tile_items(cout, wo, B) >= cu_count();
+  return wo == 32 || wo == 64 || wo == 128;
+}
+
+bool wino4_ksplit(int cin, int cout, int wo, int B) {
+  const int nchunk = cin / 4;
+  return nchunk % 2 == 0 && nchunk >= 4 && wino4_tile_items(cout, wo, B) < ksplit_items() * cu_count();
+}
+
+bool wino_dispatchable(const ConvArgs& a, int B) {
+  if (a.Ho != a.Wo || a.Hs != a.Ho || a.Ws != a.Wo) return false;
+  return (a.wpk_wino4 && wino4_ok(a.Cin, a.Ca, a.Cout, a.Wo, B)) ||
+         (a.wpk_wino && conv_wino_ok(a.Cin, a.Ca, a.Cout, a.Wo));
+}
+
 bool wino_ksplit_wanted(int cin, int cout, int wo, int B) {
+  if (wino4_ok(cin, cin, cout, wo, B)) return wino4_ksplit(cin, cout, wo, B);
   const int base = (wo / 2) * (wo / 2) / 64 * (cout / 64) * B;
   const int nchunk = cin / WKC;
   return nchunk % 2 == 0 && nchunk >= 4 && base < ksplit_items() * cu_count();
@@ -643,6 +667,9 @@ hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, 
 }
 
 hipError_t launch_conv_wino(int act, const ConvArgs& a, int B, hipStream_t s) {
+  if (a.wpk_wino4 && wino4_ok(a.Cin, a.Ca, a.Cout, a.Wo, B) && a.Ho == a.Wo && a.Hs == a.Ho &&
+      a.Ws == a.Wo)
+    return launch_conv_wino4(act, a, B, s, cu_count());
   if (!a.wpk_wino || !conv_wino_ok(a.Cin, a.Ca, a.Cout, a.Wo) || a.Ho != a.Wo || a.Hs != a.Ho ||
       a.Ws != a.Wo)
     return hipErrorInvalidValue;

@@ -76,7 +76,7 @@ def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, a
     (GroupNorm, SiLU, adds) is not counted."""
     cfg = make_config(image, ch, ch_mult, num_res, attn, groups)
     layout = param_layout(cfg)
-    conv = dense = ups = wino = 0
+    conv = dense = ups = wino = wino4 = 0
     # spatial size per conv: walk the layout names
     res_of = {}
     r = image
@@ -107,11 +107,15 @@ def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, a
             conv += f
             if len(parts) > 2 and parts[2] == "upsample":
                 ups += f
-            # ResBlock 3x3 convs the fp32 Winograd F(2x2,3x3) kernel takes
-            # (csrc/unet_conv_wino.hip: Cin % 8 == 0, Cout % 64 == 0)
-            if (parts[-2] in ("conv1", "conv2") and shape[2] == 3 and shape[1] % 8 == 0
-                    and shape[0] % 64 == 0):
-                wino += f
+            # ResBlock 3x3 convs the fp32 Winograd kernels take: F(4x4,3x3) at
+            # W >= 32 (csrc/unet_conv_wino4.hip: Cin % 4 == 0, Cout % 64 == 0),
+            # F(2x2,3x3) at W = 16 (unet_conv_wino.hip: Cin % 8 == 0; F(4x4) there
+            # only for batches whose tile items fill the CUs, not counted here)
+            if parts[-2] in ("conv1", "conv2") and shape[2] == 3 and shape[0] % 64 == 0:
+                if hw >= 32 and shape[1] % 4 == 0:
+                    wino4 += f
+                elif shape[1] % 8 == 0:
+                    wino += f
         elif len(shape) == 2:
             dense += 2 * shape[0] * shape[1]
     attn_f = 0
@@ -122,12 +126,13 @@ def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, a
     enc = 6_308_736 + 14_426_112 + 2 * 64 * 128   # the reference's condition encoder
     # the fp32 kernels run each Upsample conv as 4 sub-pixel 2x2 convs (4 of
     # the 9 counted taps per output pixel) and the ResBlock 3x3 convs by
-    # Winograd F(2x2,3x3) (16 multiplies per 2x2 outputs instead of 36): the
-    # MFMA work actually executed
+    # Winograd F(4x4,3x3) (36 multiplies per 4x4 outputs instead of 144) or
+    # F(2x2,3x3) (16 per 2x2 instead of 36): the MFMA work actually executed
     return {"conv": conv, "attention": attn_f, "dense": dense, "condition_encoder": enc,
             "total": conv + attn_f + dense + enc,
-            "conv_winograd": wino,
-            "conv_executed_fp32": conv - ups * 5 // 9 - wino * 5 // 9}
+            "conv_winograd": wino + wino4,
+            "conv_winograd_f4": wino4,
+            "conv_executed_fp32": conv - ups * 5 // 9 - wino * 5 // 9 - wino4 * 3 // 4}
 
 
 class ConditionalUNet(nn.Module):
