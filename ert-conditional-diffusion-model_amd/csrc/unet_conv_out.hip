@@ -82,18 +82,38 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
 
   const int py = tid / G::TPR, px4 = tid - py * G::TPR;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < Cin; c0 += OCC) {
-    __syncthreads();  // tables visible / previous chunk consumed
-    constexpr int NQ = OCC * G::IR * G::TPR;                   // float4 quads to stage
-    for (int e = tid; e < NQ; e += G::NT) {
+  // staging in two phases: the next chunk's float4 loads are issued into
+  // registers before the current chunk's fma chains, so the global-load
+  // latency hides behind them (one staging phase per chunk, load -> transform
+  // -> compute in series, left the layer latency-bound at one workgroup per CU)
+  constexpr int NQ = OCC * G::IR * G::TPR;                   // float4 quads per chunk
+  constexpr int NPT = (NQ + G::NT - 1) / G::NT;
+  float4 raw[NPT];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + k * G::NT;
       const int c = e / (G::IR * G::TPR), rem = e - c * (G::IR * G::TPR);
       const int r = rem / G::TPR, q = rem - r * G::TPR;
       const int cg = c0 + c, iy = oy0 - 1 + r;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cg < Cin && iy >= 0 && iy < WO) {
+      raw[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < NQ && cg < Cin && iy >= 0 && iy < WO) {
         const float* src = cg < Ca ? a.srcA + ((size_t)b * Ca + cg) * plane
                                    : a.srcB + ((size_t)b * a.Cb + (cg - Ca)) * plane;
-        v = *reinterpret_cast<const float4*>(src + iy * WO + 4 * q);
+        raw[k] = *reinterpret_cast<const float4*>(src + iy * WO + 4 * q);
+      }
+    }
+  };
+  auto stage = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + k * G::NT;
+      if (e >= NQ) continue;
+      const int c = e / (G::IR * G::TPR), rem = e - c * (G::IR * G::TPR);
+      const int r = rem / G::TPR, q = rem - r * G::TPR;
+      const int cg = c0 + c, iy = oy0 - 1 + r;
+      float4 v = raw[k];
+      if (cg < Cin && iy >= 0 && iy < WO) {
         if constexpr (ACT != ACT_NONE) {
           const float2 g = gtab[cg];
           v.x = fmaf(v.x, g.x, g.y);
@@ -116,7 +136,13 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
       }
       *reinterpret_cast<float4*>(img + (c * G::IR + r) * G::IP + 4 + 4 * q) = v;
     }
+  };
+  load(0);
+  for (int c0 = 0; c0 < Cin; c0 += OCC) {
+    __syncthreads();  // tables visible / previous chunk consumed
+    stage(c0);
     __syncthreads();
+    if (c0 + OCC < Cin) load(c0 + OCC);
     const int nc = Cin - c0 < OCC ? Cin - c0 : OCC;
     for (int c = 0; c < nc; ++c) {
       const float* wp = wl + (c0 + c) * 9;

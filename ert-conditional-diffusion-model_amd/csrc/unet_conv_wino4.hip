@@ -41,6 +41,7 @@
 //     Y = A^T M A per (co, tile), + bias (+ emb) (+ residual), float4 stores.
 // LDS 144 KB: one workgroup per CU.
 #include <cstdlib>
+#include <type_traits>
 
 #include "unet.h"
 
@@ -217,10 +218,14 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
         }
       }
     };
-    auto transform_chunk = [&](const int set, float* vb) {
+    // Two stages, software-pipelined one chunk apart so that each slot holds
+    // two independent dependency chains (a lone producer wave per SIMD is
+    // latency-bound otherwise): act (GroupNorm + SiLU + padding + the outer
+    // column by ds_bpermute: 18 values into an act buffer) for chunk g+2 and
+    // tr (the transform, the row swap, the V stores) for chunk g+1.
+    float act[2][3][6];      // [buffer][local column (1+2h, 2+2h, outer)][row]
+    auto act_stage = [&](const int set, const int ab) {
       if constexpr (DBG & 1) return;
-      // local columns (window column 1+2h, 2+2h, outer) x rows
-      float dc[3][6];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
         float2 m = raw[set][r];
@@ -240,32 +245,35 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
         }
         const float give = h ? m.y : m.x;
         const float nb = __int_as_float(__builtin_amdgcn_ds_bpermute(nbaddr, __float_as_int(give)));
-        dc[0][r] = m.x;
-        dc[1][r] = m.y;
-        dc[2][r] = nb * pad[set].z;
+        act[ab][0][r] = m.x;
+        act[ab][1][r] = m.y;
+        act[ab][2][r] = nb * pad[set].z;
       }
+    };
+    auto tr_stage = [&](const int ab, float* vb) {
+      if constexpr (DBG & 1) return;
       // B^T d on the three local columns
       float w[6][3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         float o[6];
-        bt6(dc[c], o);
+        bt6(act[ab][c], o);
 #pragma unroll
         for (int i = 0; i < 6; ++i) w[i][c] = o[i];
       }
-      // rows 0-2 to the lower half, 3-5 to the upper: afterwards lo[a][c] is
-      // row 3h+a at the lower half's local column c (window column {1,2,0}[c]),
-      // hi[a][c] at the upper half's (window column 3+c)
+      // rows 0-2 to the lower half, 3-5 to the upper: afterwards row[a][j] is
+      // row 3h+a of window column j (the lower half's local columns are
+      // window columns {1,2,0}, the upper half's 3,4,5)
       float row[3][6];
 #pragma unroll
       for (int aa = 0; aa < 3; ++aa)
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(w[aa][c]),
-                                                          __float_as_uint(w[3 + aa][c]), false, false);
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(w[aa][c]),
+                                                           __float_as_uint(w[3 + aa][c]), false, false);
           const int jl = c == 0 ? 1 : (c == 1 ? 2 : 0);
-          row[aa][jl] = __uint_as_float(s[0]);
-          row[aa][3 + c] = __uint_as_float(s[1]);
+          row[aa][jl] = __uint_as_float(sw[0]);
+          row[aa][3 + c] = __uint_as_float(sw[1]);
         }
       // (B^T d) B: V[3h+a][j'] = sum_j B^T[j'][j] row[a][j]
       float* o = vb + vwoff;
@@ -278,28 +286,45 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
           *reinterpret_cast<f32x2*>(o + (aa * 3 + jp / 2) * 256) = f32x2{vv[jp], vv[jp + 1]};
       }
     };
-    auto slot = [&](const int set, int g) {   // set = (g + 1) % NRS
-      transform_chunk(set, vbuf + ((g + 1) & 1) * V_FL);
-      load_next(set);    // chunk g + 1 + NRS
+    // slot g: tr(chunk g+1) -> V[(g+1)&1]; act(chunk g+2, register set (g+2)%3)
+    // -> act[g&1]; reload that set with chunk g+5; barrier.  Register sets and
+    // act buffers are compile-time indices: the loop is unrolled by 6.
+    auto slot = [&](auto sa, auto ab, int g) {
+      constexpr int SA = decltype(sa)::value, AB = decltype(ab)::value;
+      tr_stage(AB ^ 1, vbuf + ((g + 1) & 1) * V_FL);
+      act_stage(SA, AB);
+      load_next(SA);
       __syncthreads();   // (B) end of slot g
     };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
     if (gtot > 0) {
       set_item(0);
       load_next(0);
       load_next(1);
       load_next(2);
-      transform_chunk(0, vbuf);
-      load_next(0);
+      act_stage(0, 0);
+      tr_stage(0, vbuf);
+      load_next(0);      // chunk 3
+      act_stage(1, 1);
+      load_next(1);      // chunk 4
     }
     __syncthreads();   // (A) chunk 0 staged
     int g = 0;
-    for (; g + 2 < gtot; g += 3) {
-      slot(1, g);
-      slot(2, g + 1);
-      slot(0, g + 2);
+    for (; g + 5 < gtot; g += 6) {
+      slot(I2{}, I0{}, g);
+      slot(I0{}, I1{}, g + 1);
+      slot(I1{}, I0{}, g + 2);
+      slot(I2{}, I1{}, g + 3);
+      slot(I0{}, I0{}, g + 4);
+      slot(I1{}, I1{}, g + 5);
     }
-    if (g < gtot) slot(1, g);
-    if (g + 1 < gtot) slot(2, g + 1);
+    if (g < gtot) slot(I2{}, I0{}, g);
+    if (g + 1 < gtot) slot(I0{}, I1{}, g + 1);
+    if (g + 2 < gtot) slot(I1{}, I0{}, g + 2);
+    if (g + 3 < gtot) slot(I2{}, I1{}, g + 3);
+    if (g + 4 < gtot) slot(I0{}, I0{}, g + 4);
     return;
   }
 
