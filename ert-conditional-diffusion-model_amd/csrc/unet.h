@@ -61,6 +61,10 @@ hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, floa
 // Cout = 1, 3x3 stride 1 (conv_out; unet_conv_out.hip): per-pixel fp32 fma
 // chains, weights read from either packing (bf16: staged input rounded too)
 hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStream_t s);
+// Cin = 1, 3x3 stride 1, no activation / emb / residual (conv_in; unet_conv_out.hip):
+// one thread per output pixel, every output channel's 9-tap fp32 fma chain
+bool conv_in_ok(const ConvArgs& a, int ks, int mode, int act);
+hipError_t launch_conv_in(const ConvArgs& a, int B, bool bf16, hipStream_t s);
 // fp32 3x3 stride-1 convs by Winograd F(2x2,3x3) (unet_conv_wino.hip): eligible
 // shapes (Cin, Ca multiples of 8, Cout of 64, W in 16..128; ERTD_UNET_WINO=0
 // disables), the U = G g G^T packing (0 floats: shape not eligible), launch

@@ -457,6 +457,7 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
   if (a.Wo != expect) return hipErrorInvalidValue;
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)
     return launch_conv_out(act, a, B, false, s);
+  if (conv_in_ok(a, ks, mode, act)) return launch_conv_in(a, B, false, s);
   if (ks == 3 && mode == MODE_S1 && wino_dispatchable(a, B))
     return launch_conv_wino(act, a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_t<3, MODE_S1, ACT_NONE>(a, B, s);

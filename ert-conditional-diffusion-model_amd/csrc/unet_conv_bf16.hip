@@ -63,7 +63,10 @@ struct GeomH {
 // by act_bf16_kernel into a.bimg = [B][ceil(Cin/16)][H][W][16] bf16 -- the LDS
 // image layout row by row -- so staging is LDS-DMA of whole rows (stride-1
 // convs only): no staging VALU in the conv at all.
-template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE>
+// DBG (diagnostics only, ERTD_BF16_DBG, 3x3 PRE path; results wrong): bit 0
+// skips the epilogue's stores and residual loads, bit 1 the MFMAs, bit 2 the
+// row DMA, bit 3 the weight DMA
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE, int DBG = 0>
 __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   using G = GeomH<KS, MODE, WO, TPX>;
   extern __shared__ __attribute__((aligned(16))) char smemh[];
@@ -174,6 +177,7 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
 
   const int tile_wg = blockIdx.y * 2;
   auto dma_weights = [&](int k, char* wdst) {
+    if constexpr (DBG & 8) return;
 #pragma unroll
     for (int j = 0; j < (G::NGL + 3) / 4; ++j) {
       const int ins = wave + 4 * j;
@@ -201,6 +205,7 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   constexpr int IPR = RB >= 1024 ? RB / 1024 : 1;          // DMA instructions per row
   const int G16 = (Cin + 15) / 16;
   auto dma_rows = [&](int k, char* img) {
+    if constexpr (DBG & 4) return;
     for (int q = wave; q < G::NG * G::IR * IPR; q += 4) {  // wave-uniform
       const int g = q / (G::IR * IPR), rr = q - g * (G::IR * IPR);
       const int r = rr / IPR, part = rr - r * IPR;
@@ -282,8 +287,13 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
 #pragma unroll
       for (int t = 0; t < TPX; ++t) {
         const bf16x8 bv = *reinterpret_cast<const bf16x8*>(xb + lbase[t] + off);
-        acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bv, acc[0][t], 0, 0, 0);
-        acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bv, acc[1][t], 0, 0, 0);
+        if constexpr (DBG & 2) {
+          acc[0][t][0] += (float)a0[0] * (float)bv[0];
+          acc[1][t][0] += (float)a1[1] * (float)bv[1];
+        } else {
+          acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bv, acc[0][t], 0, 0, 0);
+          acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bv, acc[1][t], 0, 0, 0);
+        }
       }
     }
     dma_wait();
@@ -294,6 +304,17 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   // store (loads and stores share vmcnt: a load after a store would wait for
   // it), bias / emb from LDS
   constexpr int HWo = WO * WO;
+  if constexpr (DBG & 1) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int t = 0; t < TPX; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc += acc[i][t][r];
+    if (sacc == 12345.f) a.out[tid] = sacc;
+    return;
+  }
   const size_t lbase0 = (size_t)b * a.Cout * HWo + p0 + wave * 32 * TPX + l32;
   const float* __restrict__ resp = a.res ? a.res + lbase0 : nullptr;
   float* __restrict__ outp = a.out + lbase0;
@@ -522,17 +543,42 @@ size_t conv_bf16_image_bytes(int cin, int B, int H, int W) {
   return (size_t)B * ((cin + 15) / 16) * H * W * 32;
 }
 
-template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false>
-static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false, int DBG = 0>
+static hipError_t launch_hgd(const ConvArgs& a, int B, hipStream_t s) {
   using G = GeomH<KS, MODE, WO, TPX>;
   const size_t lds = G::LDS + 64 * sizeof(float2) + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE>,
+    (void)hipFuncSetAttribute((const void*)conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE, DBG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((unsigned)(WO * WO / G::BM), (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
-  conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE><<<grid, NTHR, lds, s>>>(a);
+  conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE, DBG><<<grid, NTHR, lds, s>>>(a);
   return hipGetLastError();
+}
+
+static int bf16_dbg() {
+  static int v = [] {
+    const char* e = getenv("ERTD_BF16_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false>
+static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
+  if constexpr (KS == 3 && PRE && WO == 64 && TPX == 2) {
+    switch (bf16_dbg()) {
+      case 1: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 1>(a, B, s);
+      case 2: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 2>(a, B, s);
+      case 3: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 3>(a, B, s);
+      case 4: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 4>(a, B, s);
+      case 8: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 8>(a, B, s);
+      case 12: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 12>(a, B, s);
+      case 15: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 15>(a, B, s);
+      default: break;
+    }
+  }
+  return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 0>(a, B, s);
 }
 
 // ERTD_UNET_BF16_PRE=0 keeps the register staging for stride-1 convs (diagnostics)
@@ -630,6 +676,7 @@ hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B,
   if (a.Wo != expect) return hipErrorInvalidValue;
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)
     return launch_conv_out(act, a, B, true, s);
+  if (conv_in_ok(a, ks, mode, act)) return launch_conv_in(a, B, true, s);
   // the pre-transform pays where the staging VALU is heaviest: 3x3 convs with
   // a GroupNorm(+SiLU) prologue and the Upsample convs (measured on U3 B=256:
   // the extra read+write pass costs more than it saves for 1x1 convs)

@@ -213,7 +213,87 @@ hipError_t launch_co_w(const ConvArgs& a, int B, hipStream_t s) {
   }
 }
 
+// ---- one-INPUT-channel 3x3 convolution (conv_in: x (B,1,H,W) -> (B,Cout,H,W)) ----
+// The MFMA kernels pad Cin = 1 to a whole K chunk (4 / 16 channels): 31.9 us
+// per U2 B=64 step at 6 % of the fp32 peak for a layer whose floor is its
+// output write (67 MB).  Here a thread owns one output pixel: its 9 taps in
+// registers (zero padding), the weights of all output channels in LDS
+// (broadcast reads), one fp32 fma chain of 9 taps per channel in (ky, kx)
+// order, and a coalesced store per channel (consecutive threads =
+// consecutive pixels).  bf16: the input tap is rounded to bf16 (RNE) and the
+// weights come from the bf16 packing, so the products equal the bf16 MFMA's.
+// W[co][0][tap] in the fp32 packing (ks 3: 4-channel chunks, [tile][chunk][9 step pairs][lane][2])
+__device__ __forceinline__ float packed_w0_f32(const float* w, int co, int tap) {
+  return w[((size_t)(co >> 5) * 9 + (tap >> 1)) * 128 + (co & 31) * 2 + (tap & 1)];
+}
+// ... and in the bf16 packing ([tile][chunk][9 steps][lane][8], lane = co & 31 for ci 0..7)
+__device__ __forceinline__ float packed_w0_bf16(const float* w, int co, int tap) {
+  const unsigned short* p = reinterpret_cast<const unsigned short*>(w);
+  return __uint_as_float((unsigned)p[((size_t)(co >> 5) * 9 + tap) * 512 + (co & 31) * 8] << 16);
+}
+
+template <int WO, bool BF>
+__global__ __launch_bounds__(256) void conv_in_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smi[];
+  float* wl = smi;                    // [Cout][9]
+  float* bl = smi + a.Cout * 9;       // [Cout]
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const int Cout = a.Cout;
+  for (int i = tid; i < Cout * 9; i += 256) {
+    const int co = i / 9, tap = i - co * 9;
+    wl[i] = BF ? packed_w0_bf16(a.wpk, co, tap) : packed_w0_f32(a.wpk, co, tap);
+  }
+  for (int i = tid; i < Cout; i += 256) bl[i] = a.bias ? a.bias[i] : 0.f;
+  constexpr int HW = WO * WO;
+  const int p = blockIdx.x * 256 + tid;
+  const int y = p / WO, x = p - y * WO;
+  const float* src = a.srcA + (size_t)b * HW;
+  float v[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int iy = y - 1 + ky, ix = x - 1 + kx;
+      float t = (iy >= 0 && iy < WO && ix >= 0 && ix < WO) ? src[iy * WO + ix] : 0.f;
+      if constexpr (BF) t = round_bf16(t);
+      v[ky * 3 + kx] = t;
+    }
+  __syncthreads();
+  float* out = a.out + (size_t)b * Cout * HW + p;
+  for (int co = 0; co < Cout; ++co) {
+    const float* wp = wl + co * 9;
+    float acc = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) acc = fmaf(wp[tap], v[tap], acc);
+    out[(size_t)co * HW] = acc + bl[co];
+  }
+}
+
+template <int WO, bool BF>
+hipError_t launch_ci(const ConvArgs& a, int B, hipStream_t s) {
+  const size_t lds = (size_t)a.Cout * 10 * sizeof(float);
+  if (lds > 65536) return hipErrorInvalidValue;
+  conv_in_kernel<WO, BF><<<dim3((unsigned)(WO * WO / 256), (unsigned)B), 256, lds, s>>>(a);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+bool conv_in_ok(const ConvArgs& a, int ks, int mode, int act) {
+  return a.Cin == 1 && a.Ca == 1 && ks == 3 && mode == MODE_S1 && act == ACT_NONE && !a.ebias &&
+         !a.res && a.Ho == a.Wo && a.Hs == a.Ws && a.Ws == a.Wo &&
+         (a.Wo == 16 || a.Wo == 32 || a.Wo == 64 || a.Wo == 128) && a.Cout <= 1024;
+}
+
+hipError_t launch_conv_in(const ConvArgs& a, int B, bool bf16, hipStream_t s) {
+  switch (a.Wo) {
+    case 16: return bf16 ? launch_ci<16, true>(a, B, s) : launch_ci<16, false>(a, B, s);
+    case 32: return bf16 ? launch_ci<32, true>(a, B, s) : launch_ci<32, false>(a, B, s);
+    case 64: return bf16 ? launch_ci<64, true>(a, B, s) : launch_ci<64, false>(a, B, s);
+    case 128: return bf16 ? launch_ci<128, true>(a, B, s) : launch_ci<128, false>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStream_t s) {
   if (a.Cout != 1 || a.Ho != a.Wo || a.Hs != a.Ws || a.Ws != a.Wo || a.Cin != a.Ca + a.Cb)

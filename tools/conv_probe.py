@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--act", default="gn_silu")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     x = torch.randn(a.B, a.Cin, a.H, a.H, device=dev)
@@ -34,12 +35,12 @@ def main():
     b = torch.zeros(a.Cout, device=dev)
     gn = torch.stack([torch.ones(a.B, a.Cin, device=dev), torch.zeros(a.B, a.Cin, device=dev)], -1)
     for _ in range(3):
-        conv2d(x, w, b, act=a.act, gn=gn if a.act != "none" else None)
+        conv2d(x, w, b, act=a.act, gn=gn if a.act != "none" else None, precision=a.precision)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.reps):
-        conv2d(x, w, b, act=a.act, gn=gn if a.act != "none" else None)
+        conv2d(x, w, b, act=a.act, gn=gn if a.act != "none" else None, precision=a.precision)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps

@@ -13,7 +13,7 @@ for v in ${VALUES:-0 1 2 4 8 6 7}; do
   python3 - "$f" "$v" <<'PY'
 import csv, sys
 r = [int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in csv.DictReader(open(sys.argv[1]))
-     if "conv_wino" in x["Kernel_Name"] or "conv_kernel<" in x["Kernel_Name"]]
+     if "conv_wino" in x["Kernel_Name"] or "conv_kernel<" in x["Kernel_Name"] or "conv_bf16_kernel<" in x["Kernel_Name"]]
 r = r[3:] if len(r) > 3 else r
 print(f"[dbg={sys.argv[2]}] conv kernel {sum(r) / len(r) / 1000:.1f} us avg over {len(r)}")
 PY
