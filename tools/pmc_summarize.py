@@ -22,7 +22,9 @@ def per_launch(d, counter, name):
 
 fetch_dir, write_dir, out = sys.argv[1:4]
 rec = json.load(open(out)) if os.path.exists(out) else {}
-for key, name in KERNELS.items():
+# a U-Net probe run (UNET_KEY set) records only its step total: its encoder
+# launches are not the R2 bench shape the per-kernel keys describe
+for key, name in ({} if os.environ.get("UNET_KEY") else KERNELS).items():
     fk, wk = per_launch(fetch_dir, "FETCH_SIZE", name), per_launch(write_dir, "WRITE_SIZE", name)
     if not fk or not wk:
         print(f"no {name} rows ({len(fk)} fetch, {len(wk)} write)")
