@@ -48,6 +48,25 @@ def test_unet_forward_vs_oracle(name, B, L, ts, cuda_dev):
     assert err < 1e-5, err
 
 
+def test_unet_forward_batch_split_consistency(cuda_dev):
+    """U2 at B=128 runs its 16x16 ResBlock convs by Winograd F(4x4) (tile items
+    fill the CUs); the same members as two B=64 batches run them by F(2x2).
+    Both sides are held to the spec at 1e-5 (test above); here the B=128 path
+    end to end against the split one (the spec at B=128 is minutes of CPU)."""
+    m = ertdiff.ConditionalUNet.from_config("U2", seed=3).to(cuda_dev).eval()
+    cfg = U.CONFIGS["U2"]
+    B = 128
+    x = torch.from_numpy(synth_normal((B, cfg.param_dim), 131)).to(cuda_dev)
+    cond = torch.from_numpy(synth_uniform((B, 14, 257), 132)).to(cuda_dev)
+    t = torch.arange(B, device=cuda_dev) * 7 % 1000
+    with torch.no_grad():
+        full = m(x, t, cond)
+        split = torch.cat([m(x[:64], t[:64], cond[:64]), m(x[64:], t[64:], cond[64:])])
+    err = RN.rel_l2(full.cpu().double().numpy(), split.cpu().double().numpy())
+    record_error("unet_forward_U2_B128_vs_split", err)
+    assert err < 1e-5, err
+
+
 SAMPLER_TOL = 1e-4
 # bf16-operand budget at T = 1000 (configs[2]): against the bf16 spec (same
 # operand rounding, another fp32 summation order: flips of single bf16

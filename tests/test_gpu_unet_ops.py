@@ -88,6 +88,23 @@ def test_conv2d(Ca, Cb, Cout, H, ks, mode, act, precision, cuda_dev):
     assert err < (1e-4 if precision == "bf16" else 1e-5), err
 
 
+def test_conv2d_wino4_16x16_two_sample_blocks(cuda_dev):
+    """Winograd F(4x4,3x3) at 16x16 (taken only when its tile items fill the
+    CUs without a K split: B=128, Cout=256 -> 256 items): a 32-tile block holds
+    two samples (per-lane sample offset, GroupNorm row and epilogue base), with
+    the embedding and residual epilogue."""
+    B, C, H = 128, 256, 16
+    x, w, b = _rand((B, C, H, H), 40), _rand((C, C, 3, 3), 41, 1.0 / np.sqrt(9 * C)), _rand((C,), 42, 0.1)
+    gn = torch.stack([_rand((B, C), 43, 0.3) + 1.0, _rand((B, C), 44, 0.2)], -1)
+    eb, res = _rand((B, C), 45), _rand((B, C, H, H), 46)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), act="gn_silu", gn=gn.to(cuda_dev),
+                 ebias=eb.to(cuda_dev), res=res.to(cuda_dev)).cpu()
+    ref = _ref_conv(x, w, b, "same", "gn_silu", gn, False) + eb[:, :, None, None] + res
+    err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
+    record_error("conv2d_wino4_16x16_B128", err)
+    assert err < 1e-5, err
+
+
 def test_conv2d_up_epilogue(cuda_dev):
     """Sub-pixel Upsample conv (fp32: 4 parity classes of 2x2 taps) with the
     per-sample channel add and residual scattered to the right parity."""
