@@ -64,6 +64,9 @@ constexpr int NUB = 3;                        // U ring depth (DMA two chunks ah
 constexpr int NRS = 3;                        // producer register sets (loads NRS+1 chunks ahead)
 constexpr size_t WLDS = (size_t)(NUB * U_FL + 2 * V_FL) * sizeof(float);   // 160 KB
 constexpr int XIF = WKC * 64;                 // U / V floats per xi (512)
+#ifndef WINO_PPRIO
+#define WINO_PPRIO 2                          // producer wave priority (s_setprio)
+#endif
 #ifndef WINO_PD
 #define WINO_PD 2                             // MFMA operand read-ahead (xi)
 #endif
@@ -128,6 +131,9 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
 
   if (wave >= NMW) {
     // =================== producer waves ===================
+    // the producers issue ahead of the MFMA waves on a shared SIMD (as in the
+    // F(4x4) kernel; U2 B=64 190.0 -> 191.6 steps/s)
+    __builtin_amdgcn_s_setprio(WINO_PPRIO);
     const int q = wave - NMW;          // channels 2q (k-step 0), 2q+1 (k-step 1) of every chunk
     // V offset of (channel pair q, tile t = lane): [xi][t >> 4][q][t & 15][k-step]
     const int vwoff = (lane >> 4) * 128 + q * 32 + (lane & 15) * 2;

@@ -62,6 +62,9 @@ constexpr int NRS = 3;                        // producer register sets
 constexpr size_t WLDS = (size_t)(NUB * U_FL + 2 * V_FL) * sizeof(float);   // 144 KB
 constexpr int NDMA = U_FL / 256;              // 1-KB DMA instructions per chunk (36)
 static_assert(NDMA == 4 * 5 + 4 * 4, "waves 0-3 issue 5 DMAs per chunk, waves 4-7 issue 4");
+#ifndef WINO4_PPRIO
+#define WINO4_PPRIO 2                         // producer wave priority (s_setprio)
+#endif
 #ifndef WINO4_PD
 #define WINO4_PD 2                            // MFMA operand read-ahead (xi pairs)
 #endif
@@ -151,6 +154,9 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
 
   if (wave >= NMW) {
     // =================== producer waves ===================
+    // the producers issue ahead of the MFMA waves on a shared SIMD: their
+    // transform is the chunk's critical path (U2 B=64: 185.0 -> 189.2 steps/s)
+    __builtin_amdgcn_s_setprio(WINO4_PPRIO);
     const int q = wave - NMW;          // channel q of every chunk (MFMA k row q)
     const int h = lane >> 5, t = lane & 31;
     // V offset of (xi pair 9h, tile t, k q): [xi/2][t >> 4][q][t & 15][xi&1]
@@ -329,6 +335,9 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
   }
 
   // =================== MFMA waves ===================
+#ifdef WINO4_MPRIO
+  __builtin_amdgcn_s_setprio(WINO4_MPRIO);
+#endif
   const int cb = wave & 3, tb = wave >> 2;
   f32x4 acc[NX];
   // U slice DMA of chunk g into ring slot g % 3 (36 x 1 KB: waves 0-3 five,

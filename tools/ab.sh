@@ -13,9 +13,9 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
 VAR=${VAR:?set VAR to the environment variable to vary}
 for v in ${VALUES:?set VALUES}; do
   env "$VAR=$v" timeout -k 10 300 python3 tools/unet_probe.py --config "${CFG:-U2}" --B "${B:-64}" \
-    --precision "${PREC:-fp32}" --steps "${STEPS:-50}" > "gpurun_out/ab_${VAR}_$v.log" 2>&1
+    --precision "${PREC:-fp32}" --steps "${STEPS:-50}" > "gpurun_out/ab_${VAR}_${v//\//_}.log" 2>&1
   rc=$?
-  echo "[$VAR=$v] rc=$rc $(tail -1 "gpurun_out/ab_${VAR}_$v.log")"
+  echo "[$VAR=$v] rc=$rc $(tail -1 "gpurun_out/ab_${VAR}_${v//\//_}.log")"
   [ $rc -ne 0 ] && exit $rc
 done
 exit 0
