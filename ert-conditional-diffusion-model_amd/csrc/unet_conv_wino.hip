@@ -629,9 +629,19 @@ hipError_t launch_add_inplace(float* out, const float* part, size_t n, hipStream
 
 // W = 16 takes F(4x4) only when its tile items fill the CUs without a K split
 // (U2 B=64: 128 items; split in two halves it measured no faster than F(2x2))
+// ERTD_WINO4_W16=1: F(4x4) at 16x16 for every even batch (K split), A/B only
+static int wino4_w16_env() {
+  static int v = [] {
+    const char* e = getenv("ERTD_WINO4_W16");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 bool wino4_ok(int cin, int ca, int cout, int wo, int B) {
   if (wino_env() != 1 || cin % 4 || ca % 4 || cout % 64) return false;
-  if (wo == 16) return B % 2 == 0 && wino4_tile_items(cout, wo, B) >= cu_count();
+  if (wo == 16)
+    return B % 2 == 0 && (wino4_w16_env() == 1 || wino4_tile_items(cout, wo, B) >= cu_count());
   return wo == 32 || wo == 64 || wo == 128;
 }
 
