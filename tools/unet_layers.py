@@ -77,9 +77,11 @@ for (n, cin, cout, ks, wo), r in zip(layers, last):
         n = n + "W"
     tot_t += us
     tot_f += fl
+    peak = 2500.0 if "conv_bf16_kernel<" in r["Kernel_Name"] else 157.3   # dense bf16 / fp32 MFMA peak
     tmpl = r["Kernel_Name"][r["Kernel_Name"].find("<"):r["Kernel_Name"].find(">") + 1]
     wgs = int(r["Grid_Size_X"]) // int(r.get("Workgroup_Size_X", 256) or 256) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
     print(f"{n:14s} {cin:4d}->{cout:4d} k{ks} {wo:3d}  {tmpl:22s} wg {wgs:5d}  {us:8.1f} us  "
-          f"{fl / us / 1e6:7.1f} TF  {fl / us / 1e6 / 157.3 * 100:5.1f}%  (alg {alg / us / 1e6:6.1f} TF)")
+          f"{fl / us / 1e6:7.1f} TF  {fl / us / 1e6 / peak * 100:5.1f}%  (alg {alg / us / 1e6:6.1f} TF)")
 print(f"total {tot_t:.0f} us, {tot_f / tot_t / 1e6:.1f} TF (executed FLOP; * = sub-pixel Upsample, "
-      f"4 of 9 taps; w = Winograd F(2x2,3x3), 16 of 36 multiplies; W = F(4x4,3x3), 36 of 144)")
+      f"4 of 9 taps; w = Winograd F(2x2,3x3), 16 of 36 multiplies; W = F(4x4,3x3), 36 of 144; "
+      f"% of the fp32 peak, of the bf16 peak for bf16 kernels)")
