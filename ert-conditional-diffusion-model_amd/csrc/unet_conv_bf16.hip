@@ -68,7 +68,7 @@ struct GeomH {
 // skips the epilogue's stores and residual loads, bit 1 the MFMAs, bit 2 the
 // row DMA, bit 3 the weight DMA
 template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE, int DBG = 0>
-__global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void conv_bf16_kernel(ConvArgs a) {
   using G = GeomH<KS, MODE, WO, TPX>;
   extern __shared__ __attribute__((aligned(16))) char smemh[];
   char* wim = smemh;                          // [2][WBB]
@@ -328,21 +328,27 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
   float* et = reinterpret_cast<float*>(smemh);
   const bool has_eb = a.ebias != nullptr;
   const bool has_res = a.res != nullptr;
+  // (TPX = 4: 2 x 16 float4 residual registers would cost a wave per SIMD;
+  // the second tile's residual is loaded after the first tile's stores)
+  constexpr int RV = TPX >= 4 ? 1 : 2;
   f32x4 rv[2][NQ4];
+  auto load_res = [&](int i) {
+#pragma unroll
+    for (int j = 0; j < NQ4; ++j) {
+      const int idx = tid + j * NTHR;
+      const int cl = idx / (G::BM / 4), q = idx - cl * (G::BM / 4);
+      int co = (tile_wg + i) * 32 + cl;
+      co = co < a.Cout ? co : a.Cout - 1;
+      rv[i % RV][j] = *reinterpret_cast<const f32x4*>(a.res + ((size_t)b * a.Cout + co) * HWo + p0 + 4 * q);
+    }
+  };
   if (has_res) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NQ4; ++j) {
-        const int idx = tid + j * NTHR;
-        const int cl = idx / (G::BM / 4), q = idx - cl * (G::BM / 4);
-        int co = (tile_wg + i) * 32 + cl;
-        co = co < a.Cout ? co : a.Cout - 1;
-        rv[i][j] = *reinterpret_cast<const f32x4*>(a.res + ((size_t)b * a.Cout + co) * HWo + p0 + 4 * q);
-      }
+    for (int i = 0; i < RV; ++i) load_res(i);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
+    if (RV == 1 && i == 1 && has_res) load_res(1);
     __syncthreads();   // the K loop's (or the previous tile's) LDS reads are done
 #pragma unroll
     for (int t = 0; t < TPX; ++t)
@@ -361,7 +367,7 @@ __global__ __launch_bounds__(NTHR) void conv_bf16_kernel(ConvArgs a) {
       const float2 e = etab[i * 32 + cl];
       f32x4 v = *reinterpret_cast<const f32x4*>(et + cl * TP + 4 * q) + e.x;
       if (has_eb) v = v + e.y;
-      if (has_res) v = v + rv[i][j];
+      if (has_res) v = v + rv[i % RV][j];
       *reinterpret_cast<f32x4*>(a.out + ((size_t)b * a.Cout + co) * HWo + p0 + 4 * q) = v;
     }
   }
@@ -608,8 +614,8 @@ static int convh_pre() {
   return v;
 }
 
-// ERTD_UNET_BF16_TPX=1 forces 128-pixel tiles for the 3x3 stride-1/upsample
-// convs (diagnostics); 0 = automatic
+// ERTD_UNET_BF16_TPX=1 / 2 forces 128- / 256-pixel tiles for the 3x3
+// stride-1/upsample convs (diagnostics); 0 = automatic (512 at W = 32, 64)
 static int convh_tpx_override() {
   static int v = [] {
     const char* e = getenv("ERTD_UNET_BF16_TPX");
@@ -626,6 +632,17 @@ static hipError_t launch_pre_w(const ConvArgs& a, int B, hipStream_t s) {
     case 64: return launch_hg<KS, MODE_S1, ACT_NONE, 64, TP, true>(a, B, s);
     case 128: return launch_hg<KS, MODE_S1, ACT_NONE, 128, TP, true>(a, B, s);
     default: return hipErrorInvalidValue;
+  }
+}
+
+// TPX = 4 (512-pixel tiles, 64 co x 128 px per wave: 6 LDS operand reads per
+// 8 MFMAs instead of 4 per 4) where two workgroups still fit a CU (W = 32, 64)
+template <int KS>
+static hipError_t launch_pre_w4(const ConvArgs& a, int B, hipStream_t s) {
+  switch (a.Wo) {
+    case 32: return launch_hg<KS, MODE_S1, ACT_NONE, 32, 4, true>(a, B, s);
+    case 64: return launch_hg<KS, MODE_S1, ACT_NONE, 64, 4, true>(a, B, s);
+    default: return launch_pre_w<KS, 2>(a, B, s);
   }
 }
 
@@ -648,7 +665,8 @@ static hipError_t launch_conv_pre(int ks, int mode, int act, const ConvArgs& a, 
   c.Hs = c.Ws = a.Wo;   // the image is at the output resolution
   if (ks == 1) return launch_pre_w<1, 1>(c, B, s);
   if (convh_tpx_override() == 1) return launch_pre_w<3, 1>(c, B, s);
-  return launch_pre_w<3, 2>(c, B, s);
+  if (convh_tpx_override() == 2) return launch_pre_w<3, 2>(c, B, s);
+  return launch_pre_w4<3>(c, B, s);   // U3 B=256: 101.5 -> 103.1 steps/s over TPX = 2
 }
 
 template <int KS, int MODE, int ACT, int TP>
