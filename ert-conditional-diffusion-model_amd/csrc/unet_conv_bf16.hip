@@ -685,7 +685,15 @@ static hipError_t launch_hwt(const ConvArgs& a, int B, hipStream_t s) {
 template <int KS, int MODE, int ACT>
 static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
   // TPX = 2 (256-pixel tiles) except stride 2 / 1x1 (staging registers)
-  if constexpr (MODE == MODE_S2 || KS == 1) {
+  if constexpr (KS == 1) {
+    // ERTD_UNET_BF16_TPX1=2: 256-pixel tiles for the 1x1 convs (A/B)
+    static const int t1 = [] {
+      const char* e = getenv("ERTD_UNET_BF16_TPX1");
+      return e ? atoi(e) : 1;
+    }();
+    if (t1 == 2) return launch_hwt<KS, MODE, ACT, 2>(a, B, s);
+    return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
+  } else if constexpr (MODE == MODE_S2) {
     return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
   } else {
     if (convh_tpx_override() == 1) return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
