@@ -246,7 +246,10 @@ typedef struct ertd_unet_config {
  *   act 0 none / 1 GroupNorm+SiLU / 2 GroupNorm, gn = (B, Cin) float2
  *   {scale, shift} from ertd_group_norm_stats; precision FP32 | BF16;
  *   H in {16,32,64,128} (Ho likewise); ws >= ertd_conv2d_workspace_bytes
- *   (the packed weights).
+ *   (the packed weights).  fp32 3x3 stride-1 convs with Cout % 64 == 0 run as
+ *   Winograd F(4x4,3x3) (Cin, Ca % 4 == 0; H >= 32, or 16 when the tile items
+ *   fill the device) or F(2x2,3x3) (Cin, Ca % 8 == 0), the rest as direct
+ *   implicit GEMMs; ERTD_UNET_WINO=2 keeps F(2x2), 0 disables Winograd.
  * ertd_group_norm_stats: per (sample, channel) {gamma*rstd, beta-mean*gamma*rstd}
  *   of cat(x, x2) over `groups` groups (eps 1e-5), out (B, Ca+Cb) float2.
  * ertd_attention: qkv (B, 3C, N) -> out (B, C, N) = v softmax(q^T k / sqrt C)^T, N = 256. */
