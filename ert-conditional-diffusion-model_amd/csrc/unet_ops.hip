@@ -165,16 +165,29 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     for (int x = 0; x < 2; ++x)
 #pragma unroll
       for (int y = 0; y < 2; ++y) acc[x][y] = f32x16{};
-    for (int s = 0; s < C / 2; ++s) {
-      const int c = 2 * s + h;
-      const float a0 = q[(size_t)c * N + i0 + l32];
-      const float a1 = q[(size_t)c * N + i0 + 32 + l32];
-      const float b0 = k[(size_t)c * N + j0 + l32];
-      const float b1 = k[(size_t)c * N + j0 + 32 + l32];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    // operands straight from global memory (L2), in batches of 8 k-steps
+    // whose 32 loads are all issued before the batch's MFMAs (one load
+    // latency per batch instead of per k-step; same MFMA order)
+    constexpr int KBT = 8;
+    for (int s0 = 0; s0 < C / 2; s0 += KBT) {
+      float a0[KBT], a1[KBT], b0[KBT], b1[KBT];
+#pragma unroll
+      for (int u = 0; u < KBT; ++u) {
+        const int c = 2 * (s0 + u) + h;
+        const bool ok = s0 + u < C / 2;
+        a0[u] = ok ? q[(size_t)c * N + i0 + l32] : 0.f;
+        a1[u] = ok ? q[(size_t)c * N + i0 + 32 + l32] : 0.f;
+        b0[u] = ok ? k[(size_t)c * N + j0 + l32] : 0.f;
+        b1[u] = ok ? k[(size_t)c * N + j0 + 32 + l32] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < KBT; ++u) {
+        if (s0 + u >= C / 2) break;
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b0[u], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b1[u], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b0[u], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b1[u], acc[1][1], 0, 0, 0);
+      }
     }
     // scale, row max over this wave's 64 keys
 #pragma unroll
@@ -236,20 +249,32 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     for (int x = 0; x < 2; ++x)
 #pragma unroll
       for (int y = 0; y < 2; ++y) acc[x][y] = f32x16{};
-    for (int g = 0; g < N / 8; ++g) {
-      const float4 va = *reinterpret_cast<const float4*>(v + (size_t)(c0 + l32) * N + 8 * g + 4 * h);
-      const float4 vb = *reinterpret_cast<const float4*>(v + (size_t)(c0 + 32 + l32) * N + 8 * g + 4 * h);
-      const float A0[4] = {va.x, va.y, va.z, va.w};
-      const float A1[4] = {vb.x, vb.y, vb.z, vb.w};
+    // V rows in batches of 4 groups (8 float4 loads in flight per lane)
+    constexpr int GBT = 4;
+    for (int g0 = 0; g0 < N / 8; g0 += GBT) {
+      float4 va[GBT], vb[GBT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = 8 * g + 4 * h + e;
-        const float p0 = PT[(size_t)j * APITCH + l32];
-        const float p1 = PT[(size_t)j * APITCH + 32 + l32];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[e], p0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[e], p1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[e], p0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[e], p1, acc[1][1], 0, 0, 0);
+      for (int u = 0; u < GBT; ++u) {
+        const int g = g0 + u < N / 8 ? g0 + u : g0;
+        va[u] = *reinterpret_cast<const float4*>(v + (size_t)(c0 + l32) * N + 8 * g + 4 * h);
+        vb[u] = *reinterpret_cast<const float4*>(v + (size_t)(c0 + 32 + l32) * N + 8 * g + 4 * h);
+      }
+#pragma unroll
+      for (int u = 0; u < GBT; ++u) {
+        const int g = g0 + u;
+        if (g >= N / 8) break;
+        const float A0[4] = {va[u].x, va[u].y, va[u].z, va[u].w};
+        const float A1[4] = {vb[u].x, vb[u].y, vb[u].z, vb[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 8 * g + 4 * h + e;
+          const float p0 = PT[(size_t)j * APITCH + l32];
+          const float p1 = PT[(size_t)j * APITCH + 32 + l32];
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[e], p0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[e], p1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[e], p0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[e], p1, acc[1][1], 0, 0, 0);
+        }
       }
     }
     float* ob = out + (size_t)b * C * N;
