@@ -177,26 +177,37 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     // operands straight from global memory (L2), in batches of 8 k-steps
     // whose 32 loads are all issued before the batch's MFMAs (one load
     // latency per batch instead of per k-step; same MFMA order)
+    // (double-buffered: the next batch's loads are issued before this
+    // batch's MFMAs; one wave per SIMD here, so the registers are there)
     constexpr int KBT = 8;
-    for (int s0 = 0; s0 < C / 2; s0 += KBT) {
-      float a0[KBT], a1[KBT], b0[KBT], b1[KBT];
+    float a0[2][KBT], a1[2][KBT], b0[2][KBT], b1[2][KBT];
+    auto load_b = [&](const int buf, const int s0) {
 #pragma unroll
       for (int u = 0; u < KBT; ++u) {
         const int c = 2 * (s0 + u) + h;
         const bool ok = s0 + u < C / 2;
-        a0[u] = ok ? q[(size_t)c * N + i0 + l32] : 0.f;
-        a1[u] = ok ? q[(size_t)c * N + i0 + 32 + l32] : 0.f;
-        b0[u] = ok ? k[(size_t)c * N + j0 + l32] : 0.f;
-        b1[u] = ok ? k[(size_t)c * N + j0 + 32 + l32] : 0.f;
+        a0[buf][u] = ok ? q[(size_t)c * N + i0 + l32] : 0.f;
+        a1[buf][u] = ok ? q[(size_t)c * N + i0 + 32 + l32] : 0.f;
+        b0[buf][u] = ok ? k[(size_t)c * N + j0 + l32] : 0.f;
+        b1[buf][u] = ok ? k[(size_t)c * N + j0 + 32 + l32] : 0.f;
       }
+    };
+    auto mfma_b = [&](const int buf, const int s0) {
 #pragma unroll
       for (int u = 0; u < KBT; ++u) {
         if (s0 + u >= C / 2) break;
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b0[u], acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b1[u], acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b0[u], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b1[u], acc[1][1], 0, 0, 0);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[buf][u], b0[buf][u], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[buf][u], b1[buf][u], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[buf][u], b0[buf][u], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[buf][u], b1[buf][u], acc[1][1], 0, 0, 0);
       }
+    };
+    load_b(0, 0);
+    for (int s0 = 0; s0 < C / 2; s0 += 2 * KBT) {
+      load_b(1, s0 + KBT);            // past C/2: zero operands, MFMAs skipped
+      mfma_b(0, s0);
+      load_b(0, s0 + 2 * KBT);
+      mfma_b(1, s0 + KBT);
     }
     // scale, row max over this wave's 64 keys
 #pragma unroll
