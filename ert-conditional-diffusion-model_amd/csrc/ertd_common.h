@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "ertdiff.h"
 
 namespace ertd {
@@ -38,6 +40,35 @@ constexpr int PACKH_W1_STEPS = 3;                         // ceil(42/16)
 constexpr int PACKH_W2_STEPS = 6;                         // 96/16
 constexpr int PACKH_FLOATS = (PACKH_W1_STEPS + 2 * PACKH_W2_STEPS) * 64 * 4;  // 8 bf16 = 4 floats
 constexpr int PACK_TOTAL = PACK_FLOATS + PACKH_FLOATS;
+
+// ---- per-device host state ----------------------------------------------------
+// A process may drive several GPUs (of different kinds) from several threads:
+// the dynamic-LDS opt-in of a kernel and the CU count are kept per device.
+constexpr int MAX_DEVICES = 64;
+inline int current_device() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEVICES) d = 0;
+  return d;
+}
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device);
+// `done` is the kernel's own flag word (one bit per device).  Two threads
+// racing both set the attribute, which is idempotent.
+inline void set_max_lds_once(const void* kernel, int bytes, std::atomic<unsigned long long>& done) {
+  const unsigned long long bit = 1ull << current_device();
+  if (done.load(std::memory_order_acquire) & bit) return;
+  (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
+// compute units of the current device (grid sizing of persistent kernels)
+inline int device_cu_count() {
+  static std::atomic<int> cache[MAX_DEVICES];
+  const int d = current_device();
+  int n = cache[d].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n < 1) n = 256;
+  cache[d].store(n, std::memory_order_relaxed);
+  return n;
+}
 
 __host__ __device__ constexpr int conv_len(int L) { return (L - 1) / 2 + 1; }
 __host__ __device__ constexpr int n_strips(int L2) { return (L2 + J - 1) / J; }

@@ -610,9 +610,29 @@ extern "C" {
 
 // ---- single operators of the U-Net (the SURVEY 8a' operator rows), for
 // per-operator parity tests and microbenchmarks -----------------------------
+}  // extern "C"
 
-size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision) {
-  if (cin < 1 || cout < 1 || (ks != 1 && ks != 3)) return 0;
+namespace {
+// Caller-owned workspace of one ertd_conv2d call: the packed weights (every
+// layout the dispatch may read), then the stream-ordered scratch the launch
+// needs -- a Winograd K split's second half (fp32) or the pre-transformed bf16
+// input image -- so the library never allocates (include/ertdiff.h).
+struct Conv2dWs {
+  size_t pack_floats = 0;   // packed weights (floats, 64-aligned)
+  size_t kbuf_floats = 0;   // fp32 Winograd K-split partial (B, Cout, Ho, Ho)
+  size_t bimg_bytes = 0;    // bf16 image
+  size_t total() const { return a64(pack_floats) * sizeof(float) + a64(kbuf_floats) * sizeof(float) +
+                                (bimg_bytes + 255) / 256 * 256; }
+};
+
+bool conv2d_geom_ok(int cin, int cout, int ks, int precision, int B, int H, int mode) {
+  return cin >= 1 && cout >= 1 && (ks == 1 || ks == 3) && B >= 1 && H >= 1 && mode >= MODE_S1 &&
+         mode <= MODE_UP && !(ks == 1 && mode != MODE_S1) &&
+         (precision == ERTD_PREC_FP32 || precision == ERTD_PREC_BF16);
+}
+
+Conv2dWs conv2d_ws(int cin, int ca, int cout, int ks, int precision, int B, int H, int mode, int act) {
+  Conv2dWs w;
   size_t f = precision == ERTD_PREC_BF16 ? conv_packed_floats_bf16(cin, cout, ks)
                                          : conv_packed_floats(cin, cout, ks);
   // fp32 3x3 convs may be Upsample convs (sub-pixel packing)
@@ -621,7 +641,30 @@ size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision) {
   // ... and stride-1 ones carry the Winograd packing behind the direct one
   if (precision != ERTD_PREC_BF16 && ks == 3)
     f = a64(f) + std::max(conv_packed_floats_wino(cin, cout), conv_packed_floats_wino4(cin, cout));
-  return f * sizeof(float);
+  w.pack_floats = f;
+  const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  if (precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && cout > 1 &&
+      (conv_packed_floats_wino(cin, cout) > 0 || conv_packed_floats_wino4(cin, cout) > 0) &&
+      conv_wino_ok(cin, ca, cout, Ho) && wino_ksplit_wanted(cin, cout, Ho, B))
+    w.kbuf_floats = (size_t)B * cout * Ho * Ho;
+  if (precision == ERTD_PREC_BF16 && ks == 3 && cout > 1 &&
+      ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
+    w.bimg_bytes = conv_bf16_image_bytes(cin, B, Ho, Ho);
+  return w;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision, int B, int H, int mode) {
+  if (!conv2d_geom_ok(cin, cout, ks, precision, B, H, mode)) return 0;
+  // the K-split / image scratch does not depend on the activation except for
+  // the bf16 image, which stride-1 convs need only with an activation: size
+  // for the larger of the two cases (ca = cin: the split depends on Cin only)
+  const Conv2dWs a = conv2d_ws(cin, cin, cout, ks, precision, B, H, mode, ACT_GN_SILU);
+  const Conv2dWs b = conv2d_ws(cin, cin, cout, ks, precision, B, H, mode, ACT_NONE);
+  return std::max(a.total(), b.total());
 }
 
 int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
@@ -630,13 +673,16 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
                 void* ws, size_t ws_bytes, void* stream) {
   const int Cin = Ca + Cb;
   if (!x || !w || !bias || !out || !ws || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
-      Cout < 1 || (ks != 1 && ks != 3) || mode < MODE_S1 || mode > MODE_UP ||
-      (ks == 1 && mode != MODE_S1) || act < ACT_NONE || act > ACT_GN || (act != ACT_NONE && !gn) ||
-      (precision != ERTD_PREC_FP32 && precision != ERTD_PREC_BF16))
+      !conv2d_geom_ok(Cin, Cout, ks, precision, B, H, mode) || act < ACT_NONE || act > ACT_GN ||
+      (act != ACT_NONE && !gn))
     return ERTD_EINVAL;
-  if (ertd_conv2d_workspace_bytes(Cin, Cout, ks, precision) > ws_bytes) return ERTD_ENOSPC;
+  const Conv2dWs need = conv2d_ws(Cin, Ca, Cout, ks, precision, B, H, mode, act);
+  if (need.total() > ws_bytes) return ERTD_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
   float* pk = (float*)ws;
+  // caller-owned scratch behind the packing (stream-ordered: reused by the next call)
+  float* kbuf = need.kbuf_floats ? pk + a64(need.pack_floats) : nullptr;
+  void* bimg = need.bimg_bytes ? (void*)(pk + a64(need.pack_floats) + a64(need.kbuf_floats)) : nullptr;
   // the Winograd path reads only its own packing: skip the direct one then
   const int Ho_ = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   const bool wino4 = precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
@@ -654,33 +700,19 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   a.gn = (const float2*)gn;
   a.wpk = pk; a.bias = bias; a.ebias = ebias; a.eb_stride = eb_stride; a.res = res; a.out = out;
   a.Cin = Cin; a.Cout = Cout; a.Hs = H; a.Ws = H;
-  a.Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  a.Ho = Ho_;
   a.Wo = a.Ho;
-  void* kbuf = nullptr;
   if (wino) {
     float* pw = pk + a64(std::max(conv_packed_floats(Cin, Cout, ks), conv_packed_floats_up(Cin, Cout)));
     if ((e = wino4 ? launch_pack_conv_wino4(w, Cin, Cout, pw, s)
                    : launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess)
       return (int)e;
     if (wino4) a.wpk_wino4 = pw; else a.wpk_wino = pw;
-    if (wino_ksplit_wanted(Cin, Cout, Ho_, B)) {   // stream-ordered scratch (freed on the stream)
-      if ((e = hipMallocAsync(&kbuf, (size_t)B * Cout * Ho_ * Ho_ * sizeof(float), s)) != hipSuccess)
-        return rcode(e);
-      a.ksplit_buf = (float*)kbuf;
-    }
+    a.ksplit_buf = kbuf;
   }
-  void* bimg = nullptr;
-  if (precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
-      ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE))) {
-    // stream-ordered scratch for the pre-transformed input (freed on the stream)
-    e = hipMallocAsync(&bimg, conv_bf16_image_bytes(Cin, B, a.Ho, a.Wo), s);
-    if (e != hipSuccess) return rcode(e);
-    a.bimg = bimg;
-  }
+  a.bimg = bimg;
   e = precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
                                   : launch_conv(ks, mode, act, a, B, s);
-  if (bimg) (void)hipFreeAsync(bimg, s);
-  if (kbuf) (void)hipFreeAsync(kbuf, s);
   return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
 }
 

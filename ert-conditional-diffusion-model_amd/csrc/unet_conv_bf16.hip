@@ -605,6 +605,9 @@ static hipError_t launch_hgd(const ConvArgs& a, int B, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifdef ERTD_DIAG
+// ablation variants (results wrong): only in a diagnostic build of the library
+// (tools/build_variant.sh ... "-DERTD_DIAG"), never in the shipped one
 static int bf16_dbg() {
   static int v = [] {
     const char* e = getenv("ERTD_BF16_DBG");
@@ -612,9 +615,11 @@ static int bf16_dbg() {
   }();
   return v;
 }
+#endif
 
 template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false>
 static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
+#ifdef ERTD_DIAG
   if constexpr (KS == 3 && PRE && WO == 64 && TPX == 2) {
     switch (bf16_dbg()) {
       case 1: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 1>(a, B, s);
@@ -627,6 +632,7 @@ static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
       default: break;
     }
   }
+#endif
   return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 0>(a, B, s);
 }
 

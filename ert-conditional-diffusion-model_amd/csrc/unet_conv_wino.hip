@@ -494,6 +494,9 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
   }
 }
 
+#ifdef ERTD_DIAG
+// ablation variants (results wrong): only in a diagnostic build of the library
+// (tools/build_variant.sh ... "-DERTD_DIAG"), never in the shipped one
 int wino_dbg() {
   static int v = [] {
     const char* e = getenv("ERTD_WINO_DBG");
@@ -501,6 +504,7 @@ int wino_dbg() {
   }();
   return v;
 }
+#endif
 
 // out += part (float4): the K-split halves' fixed-order sum
 __global__ void add_inplace_kernel(float* __restrict__ out, const float* __restrict__ part, size_t n4) {
@@ -521,25 +525,12 @@ int ksplit_items() {
   return v;
 }
 
-int cu_count() {
-  static int v = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
-      n = 256;
-    return n;
-  }();
-  return v;
-}
+int cu_count() { return device_cu_count(); }
 
 template <int WO, int ACT, int DBG>
 hipError_t launch_wod(const ConvArgs& a, int B, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino_kernel<WO, ACT, DBG>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)WLDS);
-    attr = true;
-  }
+  static std::atomic<unsigned long long> attr{0};
+  set_max_lds_once((const void*)conv_wino_kernel<WO, ACT, DBG>, (int)WLDS, attr);
   const int base = (WO / 2) * (WO / 2) / 64 * (a.Cout / 64) * B;
   // fewer tile items than the split threshold (x CUs) -> K split in two halves
   const int nchunk = a.Cin / WKC;
@@ -556,6 +547,7 @@ hipError_t launch_wod(const ConvArgs& a, int B, hipStream_t s) {
 
 template <int WO, int ACT>
 hipError_t launch_wo(const ConvArgs& a, int B, hipStream_t s) {
+#ifdef ERTD_DIAG
   if constexpr (WO == 64 && ACT == ACT_GN_SILU) {
     switch (wino_dbg()) {
       case 1: return launch_wod<WO, ACT, 1>(a, B, s);
@@ -571,6 +563,7 @@ hipError_t launch_wo(const ConvArgs& a, int B, hipStream_t s) {
       default: break;
     }
   }
+#endif
   return launch_wod<WO, ACT, 0>(a, B, s);
 }
 

@@ -68,6 +68,9 @@ static_assert(NDMA == 4 * 5 + 4 * 4, "waves 0-3 issue 5 DMAs per chunk, waves 4-
 #ifndef WINO4_PD
 #define WINO4_PD 2                            // MFMA operand read-ahead (xi pairs)
 #endif
+#ifndef WINO4_DMAI
+#define WINO4_DMAI 1                          // U DMA interleaved with the MFMAs (0: all after the barrier)
+#endif
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x2 = __attribute__((ext_vector_type(2))) float;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
@@ -114,6 +117,27 @@ __device__ __forceinline__ unsigned wlds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
+#ifdef WINO4_STAMP
+// Diagnostic build only (tools/wino4_stamps.py): per-wave s_memtime stamps of
+// the first NSS chunks, staged in the 16 KB of LDS above the ring and copied to
+// g_w4stamps at the end.  Per wave: [0] s_memrealtime, [1] s_memtime at entry,
+// then NSS x 5 events.
+constexpr int NSS = 64;
+constexpr int SPW = 2 + NSS * 5;
+__device__ unsigned g_w4stamps[256 * 12 * SPW];
+#define W4STAMP(ev, sl)                                                                  \
+  do {                                                                                   \
+    if (lane == 0 && (sl) < NSS)                                                         \
+      stamps[wave * SPW + 2 + (sl) * 5 + (ev)] = (unsigned)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+constexpr size_t WLDS_LAUNCH = WLDS + 12 * SPW * sizeof(unsigned);
+#else
+#define W4STAMP(ev, sl) \
+  do {                  \
+  } while (0)
+constexpr size_t WLDS_LAUNCH = WLDS;
+#endif
+
 // item it -> (co block, tile block): co block fastest; tile block blk covers
 // tiles [32 blk, 32 blk + 32) of the batch's tiles in (sample, row, column)
 // order -- within one sample at W >= 32, two whole samples at W = 16
@@ -151,6 +175,18 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
   const int bid = blockIdx.x, G = gridDim.x;
   const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;
   const int gtot = nloc * nck;
+#ifdef WINO4_STAMP
+  unsigned* stamps = reinterpret_cast<unsigned*>(smem + NUB * U_FL + 2 * V_FL);
+  if (lane == 0) {
+    stamps[wave * SPW] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    stamps[wave * SPW + 1] = (unsigned)__builtin_amdgcn_s_memtime();
+  }
+  auto stamp_flush = [&]() {
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int i = lane; i < SPW; i += 64)
+      g_w4stamps[((size_t)bid * 12 + wave) * SPW + i] = stamps[wave * SPW + i];
+  };
+#endif
 
   if (wave >= NMW) {
     // =================== producer waves ===================
@@ -297,10 +333,15 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
     // act buffers are compile-time indices: the loop is unrolled by 6.
     auto slot = [&](auto sa, auto ab, int g) {
       constexpr int SA = decltype(sa)::value, AB = decltype(ab)::value;
+      W4STAMP(0, g);
       tr_stage(AB ^ 1, vbuf + ((g + 1) & 1) * V_FL);
+      W4STAMP(1, g);
       act_stage(SA, AB);
+      W4STAMP(4, g);
       load_next(SA);
+      W4STAMP(2, g);
       __syncthreads();   // (B) end of slot g
+      W4STAMP(3, g);
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -331,6 +372,9 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
     if (g + 2 < gtot) slot(I1{}, I0{}, g + 2);
     if (g + 3 < gtot) slot(I2{}, I1{}, g + 3);
     if (g + 4 < gtot) slot(I0{}, I0{}, g + 4);
+#ifdef WINO4_STAMP
+    stamp_flush();
+#endif
     return;
   }
 
@@ -345,45 +389,64 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
   // the K loop, so vmcnt(own count) = "the previous slot's slice has landed"
   const int ndma = wave < 4 ? 5 : 4;
   const int dfirst = wave < 4 ? wave * 5 : 20 + (wave - 4) * 4;
-  auto dma_u = [&](int g) {
+  // DMA cursor (wave-uniform, scalar): the chunk whose U slice goes out next
+  // (chunk g + 2 while chunk g computes): item d_il, chunk d_k of its K range.
+  // The item's base pointer is formed once per item -- per chunk only an add
+  // (the per-chunk integer divisions cost ~700 cycles of issue per chunk).
+  int d_k = 0, d_il = 0;
+  const float* d_src = a.wpk_wino4;
+  auto d_item = [&](int il) {
+    const int it = bid + il * G;
+    d_src = a.wpk_wino4 + ((size_t)((it / ksp) % ncog) * nchunk + (size_t)(it % ksp) * nck) * U_FL;
+  };
+  if (nloc > 0) d_item(0);
+  // DMA instruction j (1 KB) of the cursor's chunk into ring slot `slot`
+  auto dma_one = [&](const int j, const int slot) {
     if constexpr (DBG & 4) return;
-    const int il = g / nck, it = bid + il * G;
-    const int k = (it % ksp) * nck + (g - il * nck);
-    const int cog = (it / ksp) % ncog;
-    const float* usrc = a.wpk_wino4 + ((size_t)cog * nchunk + k) * U_FL;
-    float* dst = ubuf + (g % NUB) * U_FL;
     int ln;   // a fresh lane id: one held across the item loop was spilled
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      if (j < ndma) {
-        const int ins = dfirst + j;
-        const float* src = usrc + ins * 256 + ln * 4;
-        const unsigned ldst = __builtin_amdgcn_readfirstlane(wlds_addr(dst + ins * 256));
-        unsigned keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(src), "s"(ldst)
-            : "memory");
-      }
+    const int ins = dfirst + j;
+    const float* src = d_src + (size_t)d_k * U_FL + ins * 256 + ln * 4;
+    const unsigned ldst = __builtin_amdgcn_readfirstlane(wlds_addr(ubuf + slot * U_FL + ins * 256));
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(ldst)
+        : "memory");
+  };
+  auto dma_advance = [&]() {
+    if (++d_k == nck) {
+      d_k = 0;
+      if (++d_il < nloc) d_item(d_il);
     }
   };
-  if (gtot > 0) dma_u(0);
-  if (gtot > 1) dma_u(1);
+  auto dma_all = [&](const int slot) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      if (j < 4 || wave < 4) dma_one(j, slot);
+    dma_advance();
+  };
+  if (gtot > 0) dma_all(0);
+  if (gtot > 1) dma_all(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // (A)
+  int su = 0, sd = 2;   // ring slots of the computed chunk (g % 3) and of the DMA'd one ((g + 2) % 3)
   for (int il = 0; il < nloc; ++il) {
 #pragma unroll
     for (int x = 0; x < NX; ++x) acc[x] = f32x4{};
     for (int k = 0; k < nck; ++k) {
       const int g = il * nck + k;
       const bool dma = g + 2 < gtot;
-      if (dma) dma_u(g + 2);
+      W4STAMP(0, g);
+#if !WINO4_DMAI
+      if (dma) dma_all(sd);
+#endif
+      W4STAMP(1, g);
       int ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-      const float* ub = ubuf + (g % NUB) * U_FL + (cb * 64 + ln) * 2;
+      const float* ub = ubuf + su * U_FL + (cb * 64 + ln) * 2;
       const float* vb = vbuf + (g & 1) * V_FL + (tb * 64 + ln) * 2;
       constexpr int PD = WINO4_PD;   // xi pairs read ahead
       f32x2 ra[PD + 1], rb[PD + 1];
@@ -412,16 +475,32 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
         }
         if (xp + PD < NX / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS reads
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                          // MFMAs
+#if WINO4_DMAI
+        // the next-but-one chunk's U slice, one 1-KB DMA after each of the
+        // first MFMA pairs: its issue cost (~140 cycles each) hides behind the
+        // MFMAs instead of holding every MFMA wave for ~700 cycles after the
+        // barrier, when no MFMA is in flight
+        if (xp >= 1 && xp <= 5 && (xp <= 4 || wave < 4))
+          if (dma) dma_one(xp - 1, sd);
+#endif
       }
+#if WINO4_DMAI
+      if (dma) dma_advance();
+#endif
+      su = su == NUB - 1 ? 0 : su + 1;
+      sd = sd == NUB - 1 ? 0 : sd + 1;
 #pragma unroll
       for (int x = 0; x < NX; ++x) asm volatile("" : "+v"(acc[x]));
+      W4STAMP(2, g);
       if (dma) {
         if (wave < 4) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      W4STAMP(4, g);
       __syncthreads();   // (B)
+      W4STAMP(3, g);
     }
 
     if constexpr (DBG & 32) {
@@ -511,6 +590,9 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
                                                i * HW * 4 + r * WO * 4, 0);
   }
+#ifdef WINO4_STAMP
+  stamp_flush();
+#endif
 }
 
 // ---- packing: W (Cout, Cin, 3, 3) -> U = G g G^T in [cog][chunk][xi/2 18][cb 4][k 4][co 16][xi&1]
@@ -546,23 +628,22 @@ __global__ void pack_wino4_kernel(const float* __restrict__ w, int cin, int cout
 
 template <int WO, int ACT, int DBG>
 hipError_t launch_wo4d(const ConvArgs& a, int B, hipStream_t s, int cus) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<WO, ACT, DBG>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)WLDS);
-    attr = true;
-  }
+  static std::atomic<unsigned long long> attr{0};
+  set_max_lds_once((const void*)conv_wino4_kernel<WO, ACT, DBG>, (int)WLDS_LAUNCH, attr);
   const int base = wino4_tile_items(a.Cout, a.Wo, B);
   const int ksp = wino4_ksplit(a.Cin, a.Cout, a.Wo, B) && a.ksplit_buf ? 2 : 1;
   const int nitems = base * ksp;
   const int grid = nitems < cus ? nitems : cus;
-  conv_wino4_kernel<WO, ACT, DBG><<<grid, WT, WLDS, s>>>(a, nitems, ksp);
+  conv_wino4_kernel<WO, ACT, DBG><<<grid, WT, WLDS_LAUNCH, s>>>(a, nitems, ksp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ksp == 1) return e;
   const size_t n = (size_t)B * a.Cout * WO * WO;
   return launch_add_inplace(a.out, a.ksplit_buf, n, s);
 }
 
+#ifdef ERTD_DIAG
+// ablation variants (results wrong): only in a diagnostic build of the library
+// (tools/build_variant.sh ... "-DERTD_DIAG"), never in the shipped one
 int wino4_dbg() {
   static int v = [] {
     const char* e = getenv("ERTD_WINO4_DBG");
@@ -570,9 +651,11 @@ int wino4_dbg() {
   }();
   return v;
 }
+#endif
 
 template <int WO, int ACT>
 hipError_t launch_wo4(const ConvArgs& a, int B, hipStream_t s, int cus) {
+#ifdef ERTD_DIAG
   if constexpr (WO == 64 && ACT == ACT_GN_SILU) {
     switch (wino4_dbg()) {
       case 1: return launch_wo4d<WO, ACT, 1>(a, B, s, cus);
@@ -587,6 +670,7 @@ hipError_t launch_wo4(const ConvArgs& a, int B, hipStream_t s, int cus) {
       default: break;
     }
   }
+#endif
   return launch_wo4d<WO, ACT, 0>(a, B, s, cus);
 }
 
@@ -602,6 +686,14 @@ hipError_t launch_act4(const ConvArgs& a, int B, hipStream_t s, int cus) {
 }
 
 }  // namespace
+
+#ifdef WINO4_STAMP
+extern "C" int ertd_diag_wino4_stamps(unsigned* host, size_t n) {
+  const size_t cap = sizeof(g_w4stamps) / sizeof(unsigned);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4stamps), (n < cap ? n : cap) * sizeof(unsigned), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 int wino4_tile_items(int cout, int wo, int B) { return (wo / 4) * (wo / 4) * B / 32 * (cout / 64); }
 

@@ -107,22 +107,25 @@ __global__ __launch_bounds__(256) void dense_kernel(DenseArgs a) {
   const int o = blockIdx.x * 256 + tid;
   if (o >= a.O) return;
   float acc = 0.f;
-  // 16 weight loads in flight per batch (K % 16 == 0, checked at launch): a
-  // load per k-step consumed at once waited a full memory latency each
-  for (int k0 = 0; k0 < K; k0 += 16) {
+  // 16 weight loads in flight per batch: a load per k-step consumed at once
+  // waited a full memory latency each; the K % 16 tail continues the same
+  // k-ordered chain (any ch the config check accepts, e.g. ch = 8 or 24)
+  const int K16 = K & ~15;
+  for (int k0 = 0; k0 < K16; k0 += 16) {
     float w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = a.wt[(size_t)(k0 + j) * a.O + o];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc = fmaf(xin[k0 + j], w[j], acc);
   }
+  for (int k = K16; k < K; ++k) acc = fmaf(xin[k], a.wt[(size_t)k * a.O + o], acc);
   float v = acc + a.bias[o];
   if (a.add) v = v + a.add[(size_t)(a.add_bcast ? 0 : b) * a.add_stride + o];
   a.y[(size_t)b * a.y_stride + o] = v;
 }
 
 hipError_t launch_dense(int din, const DenseArgs& a, int B, hipStream_t s) {
-  if (a.K % 16) return hipErrorInvalidValue;
+  if (a.K < 1 || a.O < 1) return hipErrorInvalidValue;
   dim3 grid((a.O + 255) / 256, B);
   const size_t lds = (size_t)a.K * sizeof(float);
   if (din == DIN_PLAIN) dense_kernel<DIN_PLAIN><<<grid, 256, lds, s>>>(a);

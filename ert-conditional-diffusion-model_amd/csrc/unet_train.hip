@@ -694,20 +694,19 @@ int ertd_channel_slice(const float* src, int B, int Cs, int c0, int Cd, int HW, 
   return rcode(hipGetLastError());
 }
 
+size_t ertd_mse_loss_ws_bytes(void) { return MSE_WG * sizeof(double); }
+
 int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss, float* dout,
-                  void* stream) {
-  if (!eps || !noise || !loss || n < 1) return ERTD_EINVAL;
+                  void* ws, size_t ws_bytes, void* stream) {
+  if (!eps || !noise || !loss || n < 1 || !ws) return ERTD_EINVAL;
+  if (ws_bytes < ertd_mse_loss_ws_bytes()) return ERTD_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
   const size_t per = (((size_t)n + MSE_WG - 1) / MSE_WG + 255) / 256 * 256;
   const int np = (int)(((size_t)n + per - 1) / per);
-  double* part = nullptr;
-  hipError_t e = hipMallocAsync((void**)&part, MSE_WG * sizeof(double), s);
-  if (e != hipSuccess) return (int)e;
+  double* part = (double*)ws;   // caller-owned float64 partials (fixed-order final sum)
   mse_part_kernel<<<np, 256, 0, s>>>(eps, noise, (size_t)n, per, part, dout);
   mse_final_kernel<<<1, 256, 0, s>>>(part, np, (size_t)n, loss);
-  e = hipGetLastError();
-  hipFreeAsync(part, s);
-  return rcode(e);
+  return rcode(hipGetLastError());
 }
 
 // the reference condition encoder with saved activations: partial (B,S,64),

@@ -347,12 +347,8 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
 
 template <int MODE, int KS, int HO, int ACT>
 hipError_t launch_t(const WgArgs& a, size_t lds, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)wgrad_conv_kernel<MODE, KS, HO, ACT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<unsigned long long> attr{0};
+  set_max_lds_once((const void*)wgrad_conv_kernel<MODE, KS, HO, ACT>, 160 * 1024, attr);
   wgrad_conv_kernel<MODE, KS, HO, ACT><<<(unsigned)(a.ntiles * a.nsplit), 256, lds, s>>>(a);
   return hipGetLastError();
 }

@@ -75,7 +75,7 @@ SIGNATURES = {
                              _F, _F, _F, _VP, _VP, _SZ, _VP]),
     "ertd_postprocess": (_I, [_VP, ctypes.c_longlong, _I, ctypes.c_double, ctypes.c_double, _VP,
                               _VP, _VP, _VP, _VP, _VP]),
-    "ertd_conv2d_workspace_bytes": (_SZ, [_I, _I, _I, _I]),
+    "ertd_conv2d_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "ertd_conv2d": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP,
                          _I, _VP, _SZ, _VP]),
     "ertd_group_norm_stats": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _VP]),
@@ -117,7 +117,8 @@ SIGNATURES = {
     "ertd_softmax_backward": (_I, [_VP, _VP, _LL, _I, _F, _VP, _VP]),
     "ertd_eltwise": (_I, [_I, _VP, _VP, _VP, _LL, _F, _I, _VP]),
     "ertd_channel_slice": (_I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I, _VP]),
-    "ertd_mse_loss": (_I, [_VP, _VP, _LL, _VP, _VP, _VP]),
+    "ertd_mse_loss_ws_bytes": (_SZ, []),
+    "ertd_mse_loss": (_I, [_VP, _VP, _LL, _VP, _VP, _VP, _SZ, _VP]),
     "ertd_conv_wgrad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
     "ertd_conv_input_grad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
     "ertd_conv_input_grad": (_I, [_VP, _I, _I, _VP, _I, _I, _I, _I, _VP, _I, _VP, ctypes.c_size_t, _VP]),

@@ -77,14 +77,17 @@ def gather_members(local: torch.Tensor, n_members: int, group=None) -> torch.Ten
 def sample_ensemble(model, condition: Optional[torch.Tensor], n_members: int, T: int, betas,
                     alphas, alpha_bar, *, seed: int, num_steps=None, temperature: float = 1.0,
                     mode: str = "hoisted", L: Optional[int] = None, device=None, group=None,
-                    gather: bool = False,
+                    gather: bool,
                     _sampler: Optional[Callable] = None) -> torch.Tensor:
     """n_members realisations x_0 (unconstrained space) for ONE condition.
 
     condition: (14, L) or (1, 14, L) on the source rank (others may pass None
-    and give L).  Returns this rank's (hi-lo, P) shard (global members
-    member_range(n_members, world, rank)); with ``gather=True`` (opt-in, one
-    all_gather after sampling) the whole (n_members, P) ensemble on every rank.  ``_sampler`` replaces the device sampler in the
+    and give L).  ``gather`` has no default (round 2 changed the old
+    gather-by-default behaviour; a caller must now say which result it
+    wants): False returns this rank's (hi-lo, P) shard (global members
+    member_range(n_members, world, rank)), True adds one all_gather after
+    sampling and returns the whole (n_members, P) ensemble on every rank.
+    With one rank both are the whole ensemble.  ``_sampler`` replaces the device sampler in the
     CPU (gloo) tests of this host logic; the product always uses
     ertdiff.sample_model.
     """

@@ -235,10 +235,16 @@ class ConditionalUNet(nn.Module):
         requiring grad (the reference train loop, ERT_Conditional_Diffusion.py:
         314-318), the call runs the train-mode forward (saved activations) and
         loss.backward() runs the HIP backward (ertdiff.unet_train.UNetForwardFn);
-        otherwise (no_grad, return_cond_emb, or bf16 precision, which has no
-        backward) the inference forward (ertd_unet_forward)."""
-        if (torch.is_grad_enabled() and not return_cond_emb and self.precision == "fp32" and
+        otherwise (no_grad, return_cond_emb) the inference forward
+        (ertd_unet_forward).  The bf16-operand precision has no backward: under
+        autograd it raises instead of returning a tensor that silently does
+        not require grad."""
+        if (torch.is_grad_enabled() and not return_cond_emb and
                 (x.requires_grad or any(p.requires_grad for p in self.parameters()))):
+            if self.precision != "fp32":
+                raise RuntimeError(
+                    "ertdiff: the bf16-operand U-Net has no backward; call it under torch.no_grad() "
+                    "for inference (sample_model does) or model.set_precision('fp32') to train")
             from .unet_train import UNetForwardFn
             dev = _lib.require_device(x, t, condition, self.conv_in.weight)
             self._check_call(x, t, condition)
@@ -438,8 +444,10 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, *, mode: s
     Ho = H // 2 if mode == "down" else (2 * H if mode == "up" else H)
     out = torch.empty(B, Cout, Ho, Ho, dtype=torch.float32, device=dev)
     prec = _PRECISIONS[precision]
-    n = _lib.lib().ertd_conv2d_workspace_bytes(Cin, Cout, ks, prec)
-    ws = torch.empty(max(n, 256), dtype=torch.uint8, device=dev)
+    n = _lib.lib().ertd_conv2d_workspace_bytes(Cin, Cout, ks, prec, B, H, _MODES2D[mode])
+    if n == 0:
+        raise RuntimeError("ertdiff: unsupported conv2d geometry")
+    ws = torch.empty(n, dtype=torch.uint8, device=dev)
     w = _lib.f32c(weight, "weight")
     bb = _lib.f32c(bias, "bias")
     eb = None if ebias is None else _lib.f32c(ebias, "ebias")

@@ -94,7 +94,7 @@ class _K:
         Cout, Cin, ks, _ = w.shape
         Ho = H // 2 if mode == MODE_S2 else (2 * H if mode == MODE_UP else H)
         out = self.empty(B, Cout, Ho, Ho)
-        n = self.lib.ertd_conv2d_workspace_bytes(Cin, Cout, ks, PREC_FP32)
+        n = self.lib.ertd_conv2d_workspace_bytes(Cin, Cout, ks, PREC_FP32, B, H, mode)
         ws = self.ws(n)
         _lib.check(self.lib.ertd_conv2d(
             x.data_ptr(), Ca, _p(xb), Cb, B, H, w.data_ptr(), b.data_ptr(), Cout, ks, mode, _p(gn), act,
@@ -346,12 +346,11 @@ def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, g
 
 
 def _encoder_pack(model: ConditionalUNet, k: _K, W):
-    """The condition encoder's conv weights in the reference-path packing."""
+    """The condition encoder's conv weights in the reference-path packing: one
+    buffer per tape (a second forward before this tape's backward must not
+    overwrite the packing its backward reads)."""
     n = k.lib.ertd_packed_floats()
-    pk = getattr(model, "_enc_train_pack", None)
-    if pk is None or pk.device != k.dev or pk.numel() != n:
-        pk = torch.empty(n, dtype=torch.float32, device=k.dev)
-        model._enc_train_pack = pk
+    pk = torch.empty(n, dtype=torch.float32, device=k.dev)
     _lib.check(k.lib.ertd_encoder_train_pack(W["condition_encoder.0.weight"].data_ptr(),
                                              W["condition_encoder.2.weight"].data_ptr(),
                                              pk.data_ptr(), k.s), "encoder_train_pack")
@@ -627,12 +626,24 @@ class UNetForwardFn(torch.autograd.Function):
     def forward(ctx, model, x, t, cond, *params):
         eps, tape = unet_train_forward(model, x, t, cond)
         ctx.model, ctx.tape = model, tape
+        # the tape holds x, cond and the parameters by reference (not through
+        # save_for_backward): record their version counters so an in-place
+        # change before backward raises instead of giving wrong gradients
+        ctx.versions = [(n, v, v._version) for n, v in
+                        [("x", x), ("condition", cond)] + list(model.named_parameters())]
         return eps
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         model, tape = ctx.model, ctx.tape
+        if tape is None:
+            raise RuntimeError("ertdiff: the U-Net's saved activations were freed by the first "
+                               "backward; a second backward (retain_graph=True) is not supported")
+        for n, v, ver in ctx.versions:
+            if v._version != ver:
+                raise RuntimeError(f"ertdiff: {n} was modified in place between the U-Net forward and "
+                                   "its backward (version counter changed); the gradients would be wrong")
         ctx.tape = None
         grads = unet_train_backward(model, tape, g.contiguous(), need_x=ctx.needs_input_grad[1])
         out = [grads[n].view_as(p) for n, p in model.named_parameters()]
@@ -725,8 +736,10 @@ def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *
         eps, tape = unet_train_forward(model, xn, tt, cond)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         deps = torch.empty_like(eps)
+        mws = tape["k"].ws(lib.ertd_mse_loss_ws_bytes())
         _lib.check(lib.ertd_mse_loss(eps.data_ptr(), noise.data_ptr(), eps.numel(), loss.data_ptr(),
-                                     deps.data_ptr(), _lib.stream_of(dev)), "mse_loss")
+                                     deps.data_ptr(), mws.data_ptr(), mws.numel(), _lib.stream_of(dev)),
+                   "mse_loss")
         grads = unet_train_backward(model, tape, deps)
         for nm, p in zip(names, params):
             p.grad = grads[nm].view_as(p)

@@ -245,15 +245,18 @@ typedef struct ertd_unet_config {
  *   0 stride 1 / 1 stride 2 (Downsample) / 2 nearest-x2 upsample then conv;
  *   act 0 none / 1 GroupNorm+SiLU / 2 GroupNorm, gn = (B, Cin) float2
  *   {scale, shift} from ertd_group_norm_stats; precision FP32 | BF16;
- *   H in {16,32,64,128} (Ho likewise); ws >= ertd_conv2d_workspace_bytes
- *   (the packed weights).  fp32 3x3 stride-1 convs with Cout % 64 == 0 run as
+ *   H in {16,32,64,128} (Ho likewise); ws >= ertd_conv2d_workspace_bytes(Cin,
+ *   Cout, ks, precision, B, H, mode): the packed weights plus the launch's
+ *   scratch (a Winograd K split's partial sums, the bf16 pre-transformed
+ *   input image), all caller-owned -- the call allocates nothing.  fp32 3x3 stride-1 convs with Cout % 64 == 0 run as
  *   Winograd F(4x4,3x3) (Cin, Ca % 4 == 0; H >= 32, or 16 when the tile items
  *   fill the device) or F(2x2,3x3) (Cin, Ca % 8 == 0), the rest as direct
  *   implicit GEMMs; ERTD_UNET_WINO=2 keeps F(2x2), 0 disables Winograd.
  * ertd_group_norm_stats: per (sample, channel) {gamma*rstd, beta-mean*gamma*rstd}
  *   of cat(x, x2) over `groups` groups (eps 1e-5), out (B, Ca+Cb) float2.
  * ertd_attention: qkv (B, 3C, N) -> out (B, C, N) = v softmax(q^T k / sqrt C)^T, N = 256. */
-size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision);
+size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision, int B, int H,
+                                   int mode);
 int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
                 const float* bias, int Cout, int ks, int mode, const float* gn, int act,
                 const float* ebias, int eb_stride, const float* res, float* out, int precision,
@@ -358,7 +361,8 @@ int ertd_unet_plan_destroy(ertd_unet_plan* plan);
  * ertd_eltwise: op 0 silu(x), 1 y silu'(x), 2 relu(x), 3 y [x > 0], 4 x + y, 5 alpha x.
  * ertd_channel_slice: dst (B, Cdst, HW) channels [d0, d0+Cd) (+)= src (B, Cs, HW) channels
  *   [c0, c0+Cd).
- * ertd_mse_loss: loss (1) = mean (eps - noise)^2, dout = 2 (eps - noise) / n (optional).
+ * ertd_mse_loss: loss (1) = mean (eps - noise)^2, dout = 2 (eps - noise) / n (optional);
+ *   ws >= ertd_mse_loss_ws_bytes() (float64 partial sums, caller-owned).
  * ertd_encoder_train_fwd / _bwd: the reference condition encoder (:133-142) with saved
  *   activations in ws (pool mean m (B, 64) out) / conv-parameter grads from g = dL/dm / L.
  * ertd_adam_multi: torch.optim.Adam step (no weight decay) over ntensors tensors.        */
@@ -394,8 +398,9 @@ int ertd_eltwise(int op, const float* x, const float* y, float* out, long long n
                  int accumulate, void* stream);
 int ertd_channel_slice(const float* src, int B, int Cs, int c0, int Cd, int HW, float* dst,
                        int Cdst, int d0, int accumulate, void* stream);
+size_t ertd_mse_loss_ws_bytes(void);
 int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss, float* dout,
-                  void* stream);
+                  void* ws, size_t ws_bytes, void* stream);
 /* ertd_conv_wgrad: dW (Cout, Ca+Cb, ks, ks) (+)= the weight gradient of
  *   y = conv(cat(x, x2)) (mode 0 stride 1 / 1 stride 2 / 2 nearest-x2 upsample,
  *   as ertd_conv2d) given dy (B, Cout, Ho, Ho): implicit GEMM on fp32 MFMA,

@@ -254,15 +254,28 @@ def sample(cond, W: Weights, cfg: UNetConfig, T: int, noise, num_steps=None, tem
     return (x, kept) if record else x
 
 
-def init_weights(cfg: UNetConfig, seed: int = 0) -> Weights:
+def init_weights(cfg: UNetConfig, seed: int = 0, affine: str = "ones") -> Weights:
     """Deterministic init: PyTorch's default uniform(+-1/sqrt(fan_in)) for
     conv/linear, GN weight 1 / bias 0; zero-init (as is usual) is NOT used so
-    every path carries signal in the parity tests."""
+    every path carries signal in the parity tests.
+
+    ``affine="random"``: every GroupNorm gamma = 1 + U(-0.5, 0.5) and beta =
+    U(-0.5, 0.5), distinct per channel (a trained model's state), from a
+    second generator -- every other tensor is the same as with "ones".  With
+    gamma = 1 / beta = 0 a test cannot see which gamma/beta tensor feeds which
+    GroupNorm, nor the channel order of a concatenated input's gamma."""
+    if affine not in ("ones", "random"):
+        raise ValueError("affine must be 'ones' or 'random'")
     g = torch.Generator().manual_seed(seed)
+    ga = torch.Generator().manual_seed(seed + 7919)
     W: Weights = {}
     for name, shape in layer_shapes(cfg):
         if ".norm" in name or name.startswith("norm_out"):
-            W[name] = torch.ones(shape) if name.endswith("weight") else torch.zeros(shape)
+            if affine == "random":
+                u = torch.rand(shape, generator=ga) - 0.5
+                W[name] = 1.0 + u if name.endswith("weight") else u
+            else:
+                W[name] = torch.ones(shape) if name.endswith("weight") else torch.zeros(shape)
             continue
         wshape = shape if name.endswith("weight") else None
         if name.endswith("weight"):

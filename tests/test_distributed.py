@@ -62,9 +62,9 @@ def _worker(rank, world, port, n_members, q, model_kind="mlp"):
         cond = torch.arange(14 * L, dtype=torch.float32).reshape(14, L) / 100 if rank == 0 else None
         out = sample_ensemble(model, cond, n_members, 10, None, None, None, seed=3, L=L,
                               device=torch.device("cpu"), gather=True, _sampler=fake_sampler)
-        # default: no gather collective, each rank returns its own shard
+        # gather=False: no gather collective, each rank returns its own shard
         shard = sample_ensemble(model, cond, n_members, 10, None, None, None, seed=3, L=L,
-                                device=torch.device("cpu"), _sampler=fake_sampler)
+                                device=torch.device("cpu"), gather=False, _sampler=fake_sampler)
         q.put((rank, out.numpy(), shard.numpy()))
     finally:
         dist.destroy_process_group()

@@ -26,6 +26,13 @@ def _pair(name, dev, seed=0):
     return m, W
 
 
+def _model_from_spec(name, W, dev, precision="fp32"):
+    """The GPU model holding exactly the spec's weight dict (e.g. random GN affine)."""
+    m = ertdiff.ConditionalUNet.from_config(name, seed=0, precision=precision)
+    m.load_state_dict(W)
+    return m.to(dev).eval()
+
+
 @pytest.mark.parametrize("name,B,L,ts", [
     ("U1", 3, 257, [0, 17, 999]),
     ("U2", 2, 4693, [5, 640]),
@@ -45,6 +52,28 @@ def test_unet_forward_vs_oracle(name, B, L, ts, cuda_dev):
     assert RN.rel_l2(cemb.cpu().double().numpy(), rc.double().numpy()) < 1e-5
     err = RN.rel_l2(out.cpu().double().numpy(), ref.double().numpy())
     record_error(f"unet_forward_{name}_fp32", err)
+    assert err < 1e-5, err
+
+
+def test_unet_u2_b64_forward_headline_path_random_affine(cuda_dev):
+    """The exact headline kernel path (configs[1]: U2, B = 64, L = 4693): at
+    B = 64 the Winograd layers run unsplit (F(4x4) ksp = 1 at 64x64 / 32x32,
+    unsplit F(2x2) at 16x16) -- the variants the bench times -- against the
+    spec, with trained-model-like GroupNorm gamma/beta (random per channel),
+    so a gamma/beta tensor wired to the wrong GroupNorm, or a concatenated
+    input's gamma in the wrong channel order, fails here."""
+    name, B, L = "U2", 64, 4693
+    cfg = U.CONFIGS[name]
+    W = U.init_weights(cfg, 11, affine="random")
+    m = _model_from_spec(name, W, cuda_dev)
+    x = torch.from_numpy(synth_normal((B, cfg.param_dim), 141))
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 142))
+    t = torch.arange(B) * 997 % 1000
+    with torch.no_grad():
+        out = m(x.to(cuda_dev), t.to(cuda_dev), cond.to(cuda_dev)).cpu()
+        ref = U.forward(x, t, cond, W, cfg)
+    err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
+    record_error("unet_forward_U2_B64_L4693_affine_random", err)
     assert err < 1e-5, err
 
 
@@ -82,10 +111,12 @@ def _run_golden_chain(kat, key, dev):
     """Replays the golden case on the GPU as consecutive plan segments ending at
     each recorded step count; returns {count: x}."""
     name = {"u2": "U2", "u3": "U3"}[key[:2]]
-    wseed, B, L, cseed, nseed, bf16 = (int(v) for v in kat[f"{key}_meta"])
+    meta = [int(v) for v in kat[f"{key}_meta"]]
+    wseed, B, L, cseed, nseed, bf16 = meta[:6]
+    aff = meta[6] if len(meta) > 6 else 0
     T = int(kat["T"])
-    m = ertdiff.ConditionalUNet.from_config(name, seed=wseed,
-                                            precision="bf16" if bf16 else "fp32").to(dev).eval()
+    W = U.init_weights(U.CONFIGS[name], wseed, affine="random" if aff else "ones")
+    m = _model_from_spec(name, W, dev, precision="bf16" if bf16 else "fp32")
     P = m.param_dim
     cond = torch.from_numpy(synth_uniform((B, 14, L), cseed)).to(dev)
     noise = torch.from_numpy(synth_normal((T, B, P), nseed)).to(dev)
@@ -139,6 +170,17 @@ def test_unet_u3_fp32_sampler_full_chain_vs_golden(unet_sampler_kat, cuda_dev):
         assert err < SAMPLER_TOL, (k, err)
 
 
+@pytest.mark.parametrize("key", ["u2_fp32_aff", "u3_fp32_aff"])
+def test_unet_sampler_full_chain_random_affine_vs_golden(key, unet_sampler_kat, cuda_dev):
+    """Full T = 1000 chains (U2; U3 with mid attention) whose GroupNorms carry
+    random per-channel gamma/beta: <= 1e-4 at every recorded step."""
+    xs = _run_golden_chain(unet_sampler_kat, key, cuda_dev)
+    for k, x in xs.items():
+        err = RN.rel_l2(x, unet_sampler_kat[f"{key}_x{k}"].astype(np.float64))
+        record_error(f"unet_sampler_{key}_step{k}", err)
+        assert err < SAMPLER_TOL, (k, err)
+
+
 def test_unet_sampler_vs_oracle(cuda_dev):
     name, B, L, T = "U1", 2, 129, 10
     m, W = _pair(name, cuda_dev, seed=3)
@@ -189,6 +231,39 @@ def test_unet_member_sharding_invariance(cuda_dev):
     hi = ertdiff.sample_model(m, cond, T, *sched, P, cuda_dev, noise="philox", seed=2,
                               shared_condition=True, n_members=2, member_offset=2)
     assert torch.equal(full, torch.cat([lo, hi]))
+
+
+def test_configs3_ensemble_1024_members_sharded(cuda_dev):
+    """BASELINE configs[3]: ONE condition, 1024 U2 members sharded over 8
+    GPUs by member_range (the reference's realisation loops,
+    ERT_Conditional_Diffusion.py:398-410, :1052-1069), Philox keyed by the
+    global member id.  On one device: the 1024-member shared-condition run
+    (stride 0) is bitwise equal to the concatenation of the 8 member_range
+    shards and to the run with the condition materialised per member (stride
+    14 * L) -- i.e. what each rank computes is exactly its slice of the
+    single-GPU ensemble.  T = 4 steps of the T = 1000 schedule."""
+    from ertdiff.ensemble import member_range
+    name, n, L, T, steps, world, seed = "U2", 1024, 4693, 1000, 4, 8, 77
+    m = ertdiff.ConditionalUNet.from_config(name, seed=12).to(cuda_dev).eval()
+    P = m.param_dim
+    cond = torch.from_numpy(synth_uniform((1, 14, L), 151)).to(cuda_dev)
+    sched = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    kw = dict(num_steps=steps, noise="philox", seed=seed)
+    full = ertdiff.sample_model(m, cond, T, *sched, P, cuda_dev, shared_condition=True, n_members=n,
+                                **kw)
+    shards = []
+    for r in range(world):
+        lo, hi = member_range(n, world, r)
+        shards.append(ertdiff.sample_model(m, cond, T, *sched, P, cuda_dev, shared_condition=True,
+                                           n_members=hi - lo, member_offset=lo, **kw))
+    assert torch.equal(full, torch.cat(shards))
+    del shards
+    mat = cond.expand(n, 14, L).contiguous()
+    per = ertdiff.sample_model(m, mat, T, *sched, P, cuda_dev, **kw)
+    assert torch.equal(full, per)
+    assert bool(torch.isfinite(full).all())
+    # the members differ (each its own Philox stream)
+    assert float((full[0] - full[1]).abs().max()) > 0
 
 
 @pytest.mark.parametrize("name,B,L,ts", [("U1", 3, 129, [0, 17, 999]), ("U3", 2, 257, [999, 5]),

@@ -88,6 +88,31 @@ def test_conv2d(Ca, Cb, Cout, H, ks, mode, act, precision, cuda_dev):
     assert err < (1e-4 if precision == "bf16" else 1e-5), err
 
 
+# The exact variants the headline (U2, B = 64) and the train step (B = 32) run:
+# (Cin, Cout, H) per Winograd level at B = 32 and 64, with bias, per-sample
+# embedding add and residual.  At B = 64: F(4x4) ksp = 1 at 64x64 and 32x32,
+# unsplit F(2x2) at 16x16; at B = 32 the 32x32 F(4x4) and 16x16 F(2x2) layers
+# split their K in two halves (tile items < CUs).
+HEADLINE_CASES = [(64, 64, 64), (128, 128, 32), (384, 128, 32), (256, 256, 16), (512, 256, 16)]
+
+
+@pytest.mark.parametrize("B", [32, 64])
+@pytest.mark.parametrize("Cin,Cout,H", HEADLINE_CASES)
+def test_conv2d_headline_variants(Cin, Cout, H, B, cuda_dev):
+    seed = Cin + Cout + H + B
+    x = _rand((B, Cin, H, H), seed)
+    w = _rand((Cout, Cin, 3, 3), seed + 1, 1.0 / np.sqrt(9 * Cin))
+    b = _rand((Cout,), seed + 2, 0.1)
+    gn = torch.stack([_rand((B, Cin), seed + 3, 0.3) + 1.0, _rand((B, Cin), seed + 4, 0.2)], -1)
+    eb, res = _rand((B, Cout), seed + 5), _rand((B, Cout, H, H), seed + 6)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), act="gn_silu", gn=gn.to(cuda_dev),
+                 ebias=eb.to(cuda_dev), res=res.to(cuda_dev)).cpu()
+    ref = _ref_conv(x, w, b, "same", "gn_silu", gn, False) + eb[:, :, None, None] + res
+    err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
+    record_error(f"conv2d_headline_{Cin}_{Cout}_{H}_B{B}", err)
+    assert err < 1e-5, err
+
+
 def test_conv2d_wino4_16x16_two_sample_blocks(cuda_dev):
     """Winograd F(4x4,3x3) at 16x16 (taken only when its tile items fill the
     CUs without a K split: B=128, Cout=256 -> 256 items): a 32-tile block holds

@@ -224,3 +224,67 @@ def test_unet_sampler_golden_fixture_shape(unet_sampler_kat):
         b = kat[f"u3_fp32_x{r}"].astype(np.float64)
         assert np.isfinite(a).all() and np.isfinite(b).all()
         assert np.linalg.norm(a - b) / np.linalg.norm(b) < 2e-3
+
+
+def test_shipped_library_has_no_diagnostic_variants():
+    """The wrong-result ablation variants (ERTD_*_DBG knobs) exist only in a
+    diagnostic build (-DERTD_DIAG): an inherited environment variable cannot
+    change what the shipped library computes."""
+    data = open(_lib.LIB_PATH, "rb").read()
+    for knob in (b"ERTD_WINO4_DBG", b"ERTD_WINO_DBG", b"ERTD_BF16_DBG"):
+        assert knob not in data, knob
+
+
+def test_conv2d_workspace_covers_launch_scratch():
+    """ertd_conv2d allocates nothing: its workspace query includes the K-split
+    partial of a Winograd layer with fewer tile items than CUs and the bf16
+    pre-transformed input image (caller-owned, include/ertdiff.h)."""
+    lib = _lib.load()
+    fp32, bf16 = _lib.PREC_FP32, _lib.PREC_BF16
+    # 128 -> 128 at 32x32, B = 32: 128 tile items < 256 CUs -> K split
+    small = lib.ertd_conv2d_workspace_bytes(128, 128, 3, fp32, 64, 32, 0)
+    split = lib.ertd_conv2d_workspace_bytes(128, 128, 3, fp32, 32, 32, 0)
+    assert split >= 32 * 128 * 32 * 32 * 4
+    assert split > small - 64 * 128 * 32 * 32 * 4     # the B = 64 layer needs no split buffer
+    # bf16 3x3 stride-1 conv: the [B][C/16][H][W][16] bf16 image (C*H*W*2 bytes per sample)
+    img = lib.ertd_conv2d_workspace_bytes(64, 64, 3, bf16, 8, 64, 0)
+    assert img >= 8 * 64 * 64 * 64 * 2
+    assert lib.ertd_conv2d_workspace_bytes(64, 64, 3, fp32, 0, 64, 0) == 0      # B < 1
+    assert lib.ertd_conv2d_workspace_bytes(64, 64, 1, fp32, 2, 64, 1) == 0      # 1x1 stride 2
+    assert lib.ertd_mse_loss_ws_bytes() >= 8
+    assert lib.ertd_mse_loss(None, None, 4, None, None, None, 0, None) == _lib.ERTD_EINVAL
+
+
+def test_bf16_unet_under_autograd_raises():
+    """A bf16-operand U-Net has no backward: forward under autograd raises a
+    RuntimeError that says so (before any device work) instead of returning
+    a tensor that silently does not require grad."""
+    m = ertdiff.ConditionalUNet.from_config("U1", seed=0, precision="bf16")
+    x, t, c = torch.zeros(1, 1024), torch.zeros(1, dtype=torch.long), torch.zeros(1, 14, 9)
+    with pytest.raises(RuntimeError, match="no backward"):
+        m(x, t, c)
+    with torch.no_grad():          # inference goes on to the device path (and raises off-GPU)
+        with pytest.raises(RuntimeError, match="(?!no backward)"):
+            m(x, t, c)
+
+
+def test_sample_ensemble_gather_is_explicit():
+    """sample_ensemble(gather=...) has no default (round 2 changed it from
+    True to False, which silently changed the return shape at N > 1)."""
+    from ertdiff.ensemble import sample_ensemble
+    with pytest.raises(TypeError):
+        sample_ensemble(None, torch.zeros(14, 5), 4, 10, None, None, None, seed=0,
+                        device=torch.device("cpu"), _sampler=lambda *a, **k: None)
+
+
+def test_unet_spec_random_affine_init():
+    """oracle init_weights(affine="random"): distinct per-channel GroupNorm
+    gamma/beta, every other tensor identical to the default init."""
+    from oracle import unet_torch as U
+    cfg = U.CONFIGS["U1"]
+    a, r = U.init_weights(cfg, 3), U.init_weights(cfg, 3, affine="random")
+    for k in a:
+        if ".norm" in k or k.startswith("norm_out"):
+            assert not torch.equal(a[k], r[k]) and r[k].unique().numel() == r[k].numel(), k
+        else:
+            assert torch.equal(a[k], r[k]), k
