@@ -278,8 +278,8 @@ def test_unet_bf16_forward(name, B, L, ts, cuda_dev):
     x = torch.from_numpy(synth_normal((B, cfg.param_dim), 111))
     cond = torch.from_numpy(synth_uniform((B, 14, L), 112))
     t = torch.tensor(ts)
-    out = m(x.to(cuda_dev), t.to(cuda_dev), cond.to(cuda_dev)).cpu().double().numpy()
-    with torch.no_grad():
+    with torch.no_grad():      # bf16 has no backward: forward under autograd raises
+        out = m(x.to(cuda_dev), t.to(cuda_dev), cond.to(cuda_dev)).cpu().double().numpy()
         ref16 = U.forward(x, t, cond, W, cfg, bf16=True).double().numpy()
         ref32 = U.forward(x, t, cond, W, cfg).double().numpy()
     e16, e32 = RN.rel_l2(out, ref16), RN.rel_l2(out, ref32)
