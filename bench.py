@@ -95,6 +95,8 @@ def parse():
     ap.add_argument("--no-hbm-kernels", action="store_true",
                     help="skip the per-kernel GB/s of the HBM-bound U-Net kernels")
     ap.add_argument("--unet-train-steps", type=int, default=5)
+    ap.add_argument("--no-conv-kernels", action="store_true",
+                    help="skip the per-conv-kernel timing (GB/s and TF/s vs roofline)")
     ap.add_argument("--no-strip-roofline", action="store_true")
     ap.add_argument("--no-steps-schedule", action="store_true",
                     help="skip the secondary per-step-schedule timing")
@@ -354,6 +356,77 @@ def bench_hbm_kernels(dev, reps=50):
     return out
 
 
+# The U-Net's conv kernels at the headline's shapes (U2, B = 64): (kernel, layer,
+# Ca, Cb, Cout, H (source), ks, mode, act, emb, residual, executed / direct FLOP)
+CONV_KERNEL_CASES = [
+    ("conv_wino4_kernel", "d0r0.conv1 64->64 @64x64, GN+SiLU, +emb", 64, 0, 64, 64, 3, 0, 1, True, False, 1 / 4),
+    ("conv_wino4_kernel", "d0r0.conv2 64->64 @64x64, GN+SiLU, +residual", 64, 0, 64, 64, 3, 0, 1, False, True,
+     1 / 4),
+    ("conv_wino4_kernel", "u1r0.conv1 256+128->128 @32x32 (skip concat), GN+SiLU, +emb", 256, 128, 128, 32, 3,
+     0, 1, True, False, 1 / 4),
+    ("conv_wino_kernel", "mid1.conv1 256->256 @16x16 F(2x2), GN+SiLU, +emb", 256, 0, 256, 16, 3, 0, 1, True,
+     False, 4 / 9),
+    ("conv_kernel<3,MODE_S2>", "d0.down 64->64 64x64 -> 32x32 (stride 2)", 64, 0, 64, 64, 3, 1, 0, False, False,
+     1.0),
+    ("conv_kernel<2,MODE_UPP>", "u1.up 128->128 32x32 -> 64x64 (sub-pixel Upsample)", 128, 0, 128, 32, 3, 2, 0,
+     False, False, 4 / 9),
+    ("conv_kernel<1>", "u0r0.skip 128+64->64 @64x64 (1x1, concat)", 128, 64, 64, 64, 1, 0, 0, False, False, 1.0),
+    ("conv_in_kernel", "conv_in 1->64 @64x64", 1, 0, 64, 64, 3, 0, 0, False, False, 1.0),
+    ("conv_out_kernel", "conv_out 64->1 @64x64, GN+SiLU", 64, 0, 1, 64, 3, 0, 1, False, False, 1.0),
+]
+
+
+def bench_conv_kernels(dev, B=64, reps=20):
+    """Each conv kernel of the headline alone at its U2 B=64 shape, through
+    ertd_conv2d_run (weights packed once before timing): HIP-event duration;
+    algorithmic HBM bytes (input read once, output written once, residual
+    read, weights) as GB/s vs 8 TB/s; executed MFMA FLOP vs the fp32 peak;
+    time-based roofline fraction t_roof / t with t_roof = max(bytes / 8 TB/s,
+    executed FLOP / 157.3 TF/s)."""
+    lib = _lib.lib()
+    s = _lib.stream_of(dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    out = {}
+    for kern, layer, Ca, Cb, Cout, H, ks, mode, act, emb, res, ex in CONV_KERNEL_CASES:
+        Cin = Ca + Cb
+        Ho = H // 2 if mode == 1 else (2 * H if mode == 2 else H)
+        x = torch.randn(B, Ca, H, H, device=dev, generator=g)
+        x2 = torch.randn(B, Cb, H, H, device=dev, generator=g) if Cb else None
+        w = torch.randn(Cout, Cin, ks, ks, device=dev, generator=g) / (Cin * ks * ks) ** 0.5
+        b = torch.zeros(Cout, device=dev)
+        gn = torch.stack([torch.ones(B, Cin, device=dev), torch.zeros(B, Cin, device=dev)], -1) if act else None
+        eb = torch.randn(B, Cout, device=dev, generator=g) if emb else None
+        r = torch.randn(B, Cout, Ho, Ho, device=dev, generator=g) if res else None
+        y = torch.empty(B, Cout, Ho, Ho, device=dev)
+        n = lib.ertd_conv2d_workspace_bytes(Cin, Cout, ks, 0, B, H, mode)
+        ws = torch.empty(n, dtype=torch.uint8, device=dev)
+        args = (x.data_ptr(), Ca, None if x2 is None else x2.data_ptr(), Cb, B, H)
+        tail = (Cout, ks, mode, None if gn is None else gn.data_ptr(), act,
+                None if eb is None else eb.data_ptr(), Cout, None if r is None else r.data_ptr(),
+                y.data_ptr(), 0, ws.data_ptr(), n, s)
+        _lib.check(lib.ertd_conv2d(*args, w.data_ptr(), b.data_ptr(), *tail), "conv2d")
+        us = _time_op(lambda: _lib.check(lib.ertd_conv2d_run(*args, b.data_ptr(), *tail), "conv2d_run"),
+                      reps, dev)
+        nbytes = 4 * (B * Cin * H * H + B * Cout * Ho * Ho * (2 if res else 1) + w.numel()
+                      + (B * Cin * 2 if act else 0))
+        alg = 2 * Cout * Cin * ks * ks * Ho * Ho * B
+        exf = alg * ex
+        gbs = nbytes / (us * 1e-6) / 1e9
+        tf = exf / (us * 1e-6) / 1e12
+        t_roof = max(nbytes / (PEAK_HBM_GBS * 1e9), exf / (PEAK_FP32_TFLOPS * 1e12))
+        out[layer] = {"kernel": kern, "avg_us": round(us, 2), "hbm_bytes": int(nbytes),
+                      "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+                      "executed_flop": int(exf), "executed_tflops": round(tf, 2),
+                      "mfma_frac": round(tf / PEAK_FP32_TFLOPS, 4),
+                      "algorithmic_tflops": round(alg / (us * 1e-6) / 1e12, 2),
+                      "bound": "hbm" if nbytes / (PEAK_HBM_GBS * 1e9) > exf / (PEAK_FP32_TFLOPS * 1e12)
+                      else "mfma",
+                      "roofline_frac": round(t_roof / (us * 1e-6), 4)}
+        del x, x2, w, y, ws, r
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000, rank=0, world=1):
     """The reference train step (:309-320) on the U-Net denoiser: q_sample, the
     HIP forward with saved activations, the hand-written HIP backward, MSE and
@@ -542,11 +615,12 @@ def bench_reference(a, rank, world, dev):
     return out
 
 
-def cpu_unet_baseline(name, seconds, B, T):
+def cpu_unet_baseline(name, seconds, B, T, threads=None):
     """The U-Net spec (oracle/unet_torch.py) on PyTorch-CPU, bounded sample."""
     from oracle import unet_torch as U
     _tune_cpu_allocator()
-    cpu_model, affinity, threads = _host_cpus()
+    cpu_model, affinity, thr = _host_cpus()
+    threads = threads or thr
     torch.set_num_threads(threads)
     cfg = U.CONFIGS[name]
     W = U.init_weights(cfg, 0)
@@ -573,6 +647,47 @@ def cpu_unet_baseline(name, seconds, B, T):
                       f"(oracle/unet_torch.py, {name}), B={B}, cond (B,14,{L_MEAS}) fp32, "
                       f"torch {torch.__version__} CPU, {threads} threads",
             "seconds": round(el, 2)}
+
+
+def cpu_unet_train_baseline(name, seconds, B, T=1000, threads=None):
+    """The U-Net train step (the reference loop :309-320 around the spec:
+    q_sample, forward, MSELoss, autograd backward, torch.optim.Adam) on
+    PyTorch-CPU, fp32, bounded sample."""
+    from oracle import unet_torch as U
+    _tune_cpu_allocator()
+    cpu_model, affinity, thr = _host_cpus()
+    threads = threads or thr
+    torch.set_num_threads(threads)
+    cfg = U.CONFIGS[name]
+    W = {k: v.requires_grad_(True) for k, v in U.init_weights(cfg, 0).items()}
+    opt = torch.optim.Adam(list(W.values()), lr=1e-4)
+    g = torch.Generator().manual_seed(11)
+    x0 = torch.randn(B, cfg.param_dim, generator=g)
+    cond = torch.rand(B, 14, L_MEAS, generator=g)
+    ab = torch.cumprod(1.0 - torch.linspace(1e-4, 0.02, T), 0)
+
+    def step(i):
+        t = torch.randint(0, T, (B,), generator=g)
+        noise = torch.randn(B, cfg.param_dim, generator=g)
+        a = ab[t].unsqueeze(1)
+        xn = a.sqrt() * x0 + (1 - a).sqrt() * noise
+        loss = torch.nn.functional.mse_loss(U.forward(xn, t, cond, W, cfg), noise)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    step(0)
+    t0 = time.perf_counter()
+    step(1)
+    per = time.perf_counter() - t0
+    n = int(max(2, seconds / max(per, 1e-6)))
+    t0 = time.perf_counter()
+    for i in range(n):
+        step(i)
+    el = time.perf_counter() - t0
+    return {"value": round(n / el, 4), "unit": "train steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model, "affinity_cpus": affinity,
+            "sample": f"{n} train steps of the spec ({name}, B={B}, fp32, autograd + torch.optim.Adam), "
+                      f"torch {torch.__version__} CPU, {threads} threads", "seconds": round(el, 2)}
 
 
 def time_unet(model, cond, B, steps, warmup, T, seed, offset, world, dev, shared=False):
@@ -614,7 +729,7 @@ def time_unet(model, cond, B, steps, warmup, T, seed, offset, world, dev, shared
     return el, ev_s, plan
 
 
-def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev):
+def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev, cpu_seconds=None):
     """A further BASELINE config (not the headline): same timing discipline,
     reported under extra.  Weak scaling over member shards like the headline."""
     from ertdiff.unet import CONFIGS, unet_flops
@@ -642,6 +757,12 @@ def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev):
     if tr:
         out["hbm_gbs_step_avg"] = round(tr / step_s / 1e9, 1)
         out["hbm_frac_step_avg"] = round(tr / step_s / 1e9 / PEAK_HBM_GBS, 4)
+    if cpu_seconds and rank == 0 and world == 1:
+        # the CPU reference path has no bf16: the fp32 spec at the same batch
+        cpu = cpu_unet_baseline(name, cpu_seconds, B, T)
+        cpu["sample"] += " (fp32: the CPU path has no bf16 operands)"
+        out["cpu_baseline"] = cpu
+        out["vs_cpu_baseline"] = round(out["value"] / cpu["value"], 1)
     return out
 
 
@@ -767,18 +888,45 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_unet_baseline(a.unet, a.cpu_unet_seconds, B, T)
         extra["vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        # thread scaling of the CPU path on this box's CPU share (OMP_NUM_THREADS;
+        # the box allots 16 CPUs per GPU): the same sample at half the threads
+        half = max(1, cpu["cores"] // 2)
+        if half < cpu["cores"]:
+            c2 = cpu_unet_baseline(a.unet, a.cpu_unet_seconds / 2, B, T, threads=half)
+            cpu["thread_scaling"] = {f"{half}_threads": c2["value"], f"{cpu['cores']}_threads": cpu["value"],
+                                     "speedup": round(cpu["value"] / c2["value"], 3)}
+            torch.set_num_threads(cpu["cores"])
     del timed
+    if not a.no_conv_kernels:
+        ck = bench_conv_kernels(dev)
+        extra["conv_kernels"] = ck
+        dom = ck["d0r0.conv1 64->64 @64x64, GN+SiLU, +emb"]
+        roof["dominant"] = {"kernel": "conv_wino4_kernel (Winograd F(4x4,3x3), 18 of the 52 convs, 1.9 of "
+                                      "4.8 ms of conv time per step)",
+                            "layer": "d0r0.conv1 64->64 @64x64, B=64, GN+SiLU prologue, +emb epilogue",
+                            "achieved": dom["executed_tflops"], "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                            "frac": dom["mfma_frac"], "avg_us": dom["avg_us"],
+                            "executed_flop_per_launch": dom["executed_flop"],
+                            "timing": "HIP events around 20 launches through ertd_conv2d_run (no packing)",
+                            "hbm_gbs": dom["hbm_gbs"], "hbm_frac": dom["hbm_frac"]}
     if not a.no_u3:
-        extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev)
+        extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev,
+                                                     None if a.no_cpu_baseline else a.cpu_unet_seconds)
     if not a.no_ensemble:
         extra["configs3_ensemble"] = bench_ensemble(a.ensemble, "U2", a.ensemble_steps, 2, T, rank,
                                                     world, dev)
     if not a.no_u5:
-        extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev)
+        extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev,
+                                                     None if a.no_cpu_baseline else a.cpu_unet_seconds)
     if not a.no_hbm_kernels:
         extra["hbm_kernels"] = bench_hbm_kernels(dev)
     if not a.no_unet_train:
-        extra["unet_train"] = bench_unet_train(dev, steps=a.unet_train_steps, rank=rank, world=world)
+        ut = bench_unet_train(dev, steps=a.unet_train_steps, rank=rank, world=world)
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            ct = cpu_unet_train_baseline("U2", a.cpu_unet_seconds, 32)
+            ut["cpu_baseline"] = ct
+            ut["vs_cpu_baseline"] = round(ut["unet_train_steps_per_s"] / ct["value"], 1)
+        extra["unet_train"] = ut
     if not a.no_kde:
         extra["kde_mode"] = bench_kde(dev, world, rank, cpu=not a.no_cpu_baseline)
     if not a.no_reference:

@@ -47,7 +47,45 @@ struct ConvArgs {
                          // fewer tile items than CUs split its K (input channels) in two halves
   const float* wpk_wino4;// fp32 3x3 stride-1 at W >= 32: Winograd F(4x4,3x3) weights
                          // (launch_pack_conv_wino4), preferred over wpk_wino where eligible
+  float2* gnp;           // optional (B, Cout, np): GroupNorm partials of the OUTPUT (after
+                         // bias / emb / residual), np = conv_gn_parts(...) (0: the dispatched
+                         // kernel emits none and gnp must be null)
 };
+
+// GroupNorm statistics without a second read of the activation: the fp32
+// Winograd convs emit, per (sample, channel, part of n = HW/np pixels), the
+// partial {sum, M2 = sum (x - sum/n)^2} of their output from the epilogue
+// registers; launch_gn_partials computes the same from a tensor (the outputs
+// of the other kernels); launch_gn_finalize combines a group's parts in a
+// fixed order in float64 (Chan's parallel formula) into the conv prologue's
+// {scale, shift} (and {mean, rstd}) -- the 35 full-tensor reads of
+// gn_stats_kernel per U2 step become 5.
+struct GnPartArgs {
+  const float2* pa; int npa; int Ca;   // (B, Ca, npa) partials of channels [0, Ca)
+  const float2* pb; int npb; int Cb;   // (B, Cb, npb) of channels [Ca, Ca+Cb), or null
+  int HW, groups;
+  const float* gamma; const float* beta;
+  float2* out;           // (B, Ca+Cb) {gamma*rstd, beta - mean*gamma*rstd}
+  float2* mr;            // optional (B, groups) {mean, rstd}
+};
+hipError_t launch_gn_finalize(const GnPartArgs& a, int B, hipStream_t s);
+// x (B, C, HW) -> (B, C, np) partials of 256 pixels: HW == 256 np
+hipError_t launch_gn_partials(const float* x, int C, int HW, int np, float2* out, int B, hipStream_t s);
+// parts per (sample, channel) the kernel launch_conv would dispatch emits into
+// ConvArgs::gnp (0 = none: the Winograd layers without a K split do)
+int conv_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B);
+int wino_gn_parts(const ConvArgs& a, int B);
+
+// sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), the same bits in
+// every lane of the row (fixed pairing: quad swaps, then the half-row and row
+// mirrors; fp32 addition is commutative)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
 // bf16-operand variant (unet_conv_bf16.hip): same arguments, wpk packed by

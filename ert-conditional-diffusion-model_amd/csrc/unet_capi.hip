@@ -204,11 +204,19 @@ struct Walk {
   bool dry;
   hipError_t err = hipSuccess;
 
+  // dry (sizing) walks hand out distinct fake addresses -- never dereferenced,
+  // but tensors are keyed by address (GroupNorm partials): a shared null would
+  // merge their records and under-count the workspace
   float* alloc(size_t floats) {
-    float* p = dry ? nullptr : (float*)(ws + used);
+    float* p = dry ? reinterpret_cast<float*>((uintptr_t)4096 + used) : (float*)(ws + used);
     used += (floats * sizeof(float) + 255) / 256 * 256;
+    if (!dry && cap && used > cap) {   // never launch past the caller's workspace
+      if (err == hipSuccess) err = hipErrorOutOfMemory;
+      return (float*)ws;
+    }
     return p;
   }
+  size_t cap = 0;        // real walks: the caller's workspace bytes (checked by alloc)
   const float* P(const std::string& n) const { return pk + L->off.at(n); }
   void chk(hipError_t e) {
     if (err == hipSuccess && e != hipSuccess) err = e;
@@ -235,8 +243,43 @@ struct Walk {
     return v;
   }
 
+  // fp32: GroupNorm partials per activation tensor (unet.h, GnPartArgs) --
+  // emitted by the Winograd convs' epilogues, else computed once by a
+  // partials pass (conv_in, Downsample, Upsample outputs) -- so a GroupNorm
+  // costs a finalize over B x C x np partials instead of a read of the tensor
+  struct PartRec {
+    float2* p;
+    int np;
+  };
+  std::map<const float*, PartRec> parts;
+  static bool gn_fuse_env() {
+    static const bool v = [] {
+      const char* e = getenv("ERTD_UNET_GNFUSE");
+      return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+  }
+  bool gn_parts_on() const { return c->precision == ERTD_PREC_FP32 && gn_fuse_env(); }
+  const PartRec& parts_of(const float* X, int C, int HW) {
+    auto it = parts.find(X);
+    if (it != parts.end()) return it->second;
+    const int np = HW / 256;   // gn_stats only takes this path when HW % 256 == 0
+    float2* p = (float2*)alloc((size_t)B * C * np * 2);
+    if (!dry) chk(launch_gn_partials(X, C, HW, np, p, B, s));
+    return parts[X] = PartRec{p, np};
+  }
+
   void gn_stats(const float* A, int Ca, const float* Bs, int Cb, int HW, const std::string& n,
                 bool fusable = false) {
+    if (gn_parts_on() && HW % 256 == 0) {
+      const PartRec ra = parts_of(A, Ca, HW);
+      const PartRec rb = Cb > 0 ? parts_of(Bs, Cb, HW) : PartRec{nullptr, 0};
+      if (dry) return;
+      GnPartArgs g{ra.p, ra.np, Ca, rb.p, rb.np, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"),
+                   gnbuf, nullptr};
+      chk(launch_gn_finalize(g, B, s));
+      return;
+    }
     if (dry) return;
     GnArgs g{A, Bs, Ca, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"), gnbuf};
     if (fusable && c->precision == ERTD_PREC_BF16 && fuse_gn_env() &&
@@ -251,7 +294,7 @@ struct Walk {
   // conv over input (A: Ca ch, Bs: Cb ch) at source size Hs x Ws
   float* conv(const std::string& n, int ks, int mode, int act, const float* A, int Ca,
               const float* Bs, int Cb, int Hs, int Ws, const float* ebias, const float* res,
-              float* out = nullptr) {
+              float* out = nullptr, bool gn_out = true) {
     const Param* wp = nullptr;
     for (const Param& p : L->params)
       if (p.name == n + ".weight") { wp = &p; break; }
@@ -261,16 +304,31 @@ struct Walk {
     if (mode == MODE_UP) { Ho = Hs * 2; Wo = Ws * 2; }
     if (!out) out = alloc((size_t)B * Cout * Ho * Wo);
     // fp32 Winograd layers with fewer tile items than CUs split their K
-    float* kbuf = nullptr;
-    if (c->precision == ERTD_PREC_FP32 && ks == 3 && mode == MODE_S1 &&
-        (L->offw.count(n + ".weight") || L->offw4.count(n + ".weight")) &&
-        conv_wino_ok(Cin, Ca, Cout, Wo) && wino_ksplit_wanted(Cin, Cout, Wo, B))
-      kbuf = alloc((size_t)B * Cout * Ho * Wo);
+    const bool want_split = c->precision == ERTD_PREC_FP32 && ks == 3 && mode == MODE_S1 &&
+                            (L->offw.count(n + ".weight") || L->offw4.count(n + ".weight")) &&
+                            conv_wino_ok(Cin, Ca, Cout, Wo) && wino_ksplit_wanted(Cin, Cout, Wo, B);
+    float* kbuf = want_split ? alloc((size_t)B * Cout * Ho * Wo) : nullptr;
     // bf16 stride-1 convs stage a pre-transformed bf16 copy of their input
     float* bimg = nullptr;
     if (c->precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
         ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
       bimg = alloc((conv_bf16_image_bytes(Ca + Cb, B, Ho, Wo) + 3) / 4);
+    // fp32: GroupNorm partials of the output, when the dispatched kernel emits
+    // them (the geometry-only part of the dispatch: sentinel pointers in dry runs)
+    float2* gnp = nullptr;
+    if (gn_parts_on() && gn_out) {
+      ConvArgs q{};
+      q.Ca = Ca; q.Cb = Cb; q.Cin = Cin; q.Cout = Cout;
+      q.Hs = Hs; q.Ws = Ws; q.Ho = Ho; q.Wo = Wo;
+      q.wpk_wino = L->offw.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
+      q.wpk_wino4 = L->offw4.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
+      q.ksplit_buf = want_split ? reinterpret_cast<float*>(16) : nullptr;
+      const int np = conv_gn_parts(ks, mode, act, q, B);
+      if (np > 0) {
+        gnp = (float2*)alloc((size_t)B * Cout * np * 2);
+        parts[out] = PartRec{gnp, np};
+      }
+    }
     if (dry) return out;
     if (Cin != Ca + Cb) {
       chk(hipErrorInvalidValue);
@@ -293,6 +351,7 @@ struct Walk {
     a.Hs = Hs; a.Ws = Ws; a.Ho = Ho; a.Wo = Wo;
     a.bimg = bimg;
     a.ksplit_buf = kbuf;
+    a.gnp = gnp;
     if (has_pend) {
       has_pend = false;
       if (bimg && ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) {
@@ -559,6 +618,7 @@ struct SampleCall {
   int head(hipStream_t s) const {
     const Layout Lo = layout_with_freq(c);
     Walk w{c, &Lo, packed, (char*)ws, 0, B, s, false};
+    w.cap = ws_bytes;
     const Fixed f = fixed(w, L);
     const int r = prologue(w, f, cond, cond_stride, L);
     if (r != ERTD_OK) return r;
@@ -569,6 +629,7 @@ struct SampleCall {
            hipEvent_t evj = nullptr, hipEvent_t eve = nullptr) const {
     const Layout Lo = layout_with_freq(c);
     Walk w{c, &Lo, packed, (char*)ws, 0, B, s, false};
+    w.cap = ws_bytes;
     w.s2 = s2;
     w.evf = evf;
     w.evj = evj;
@@ -667,12 +728,15 @@ size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision, int
   return std::max(a.total(), b.total());
 }
 
-int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
+namespace {
+// ertd_conv2d: pack (unless `pack` is false: ws already holds this shape's
+// packing from an earlier call) and launch
+int conv2d_impl(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
                 const float* bias, int Cout, int ks, int mode, const float* gn, int act,
                 const float* ebias, int eb_stride, const float* res, float* out, int precision,
-                void* ws, size_t ws_bytes, void* stream) {
+                void* ws, size_t ws_bytes, void* stream, bool pack) {
   const int Cin = Ca + Cb;
-  if (!x || !w || !bias || !out || !ws || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
+  if (!x || (pack && !w) || !bias || !out || !ws || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
       !conv2d_geom_ok(Cin, Cout, ks, precision, B, H, mode) || act < ACT_NONE || act > ACT_GN ||
       (act != ACT_NONE && !gn))
     return ERTD_EINVAL;
@@ -690,7 +754,7 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   const bool wino = wino4 || (precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
                               conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho_));
   hipError_t e = hipSuccess;
-  if (!wino)
+  if (!wino && pack)
     e = precision == ERTD_PREC_BF16 ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s)
         : (ks == 3 && mode == MODE_UP) ? launch_pack_conv_up(w, Cin, Cout, pk, s)
                                        : launch_pack_conv(w, Cin, Cout, ks, pk, s);
@@ -704,8 +768,8 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   a.Wo = a.Ho;
   if (wino) {
     float* pw = pk + a64(std::max(conv_packed_floats(Cin, Cout, ks), conv_packed_floats_up(Cin, Cout)));
-    if ((e = wino4 ? launch_pack_conv_wino4(w, Cin, Cout, pw, s)
-                   : launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess)
+    if (pack && (e = wino4 ? launch_pack_conv_wino4(w, Cin, Cout, pw, s)
+                           : launch_pack_conv_wino(w, Cin, Cout, pw, s)) != hipSuccess)
       return (int)e;
     if (wino4) a.wpk_wino4 = pw; else a.wpk_wino = pw;
     a.ksplit_buf = kbuf;
@@ -714,6 +778,23 @@ int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   e = precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
                                   : launch_conv(ks, mode, act, a, B, s);
   return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
+}
+}  // namespace
+
+int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
+                const float* bias, int Cout, int ks, int mode, const float* gn, int act,
+                const float* ebias, int eb_stride, const float* res, float* out, int precision,
+                void* ws, size_t ws_bytes, void* stream) {
+  return conv2d_impl(x, Ca, x2, Cb, B, H, w, bias, Cout, ks, mode, gn, act, ebias, eb_stride, res, out,
+                     precision, ws, ws_bytes, stream, true);
+}
+
+int ertd_conv2d_run(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* bias,
+                    int Cout, int ks, int mode, const float* gn, int act, const float* ebias,
+                    int eb_stride, const float* res, float* out, int precision, void* ws,
+                    size_t ws_bytes, void* stream) {
+  return conv2d_impl(x, Ca, x2, Cb, B, H, nullptr, bias, Cout, ks, mode, gn, act, ebias, eb_stride, res,
+                     out, precision, ws, ws_bytes, stream, false);
 }
 
 // dX (B, Cin, H, H) (+)= the input gradient of y = conv(x) (Cout, Cin, ks, ks; mode as
@@ -789,6 +870,23 @@ int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B
     return ERTD_EINVAL;
   GnArgs g{x, x2, Ca, Cb, HW, groups, gamma, beta, (float2*)out};
   return rcode(launch_gn_stats(g, B, (hipStream_t)stream));
+}
+
+int ertd_group_norm_partials(const float* x, int C, int B, int HW, int np, float* parts, void* stream) {
+  if (!x || !parts || C < 1 || B < 1 || np < 1 || HW != np * 256) return ERTD_EINVAL;
+  return rcode(launch_gn_partials(x, C, HW, np, (float2*)parts, B, (hipStream_t)stream));
+}
+
+int ertd_group_norm_finalize(const float* pa, int npa, int Ca, const float* pb, int npb, int Cb, int B,
+                             int HW, int groups, const float* gamma, const float* beta, float* out,
+                             float* mr, void* stream) {
+  const int C = Ca + Cb;
+  if (!pa || !gamma || !beta || !out || B < 1 || Ca < 1 || Cb < 0 || npa < 1 || HW < 1 || groups < 1 ||
+      C % groups || HW % npa || (Cb > 0 && (!pb || npb < 1 || HW % npb)))
+    return ERTD_EINVAL;
+  GnPartArgs g{(const float2*)pa, npa, Ca, (const float2*)pb, npb, Cb, HW, groups, gamma, beta,
+               (float2*)out, (float2*)mr};
+  return rcode(launch_gn_finalize(g, B, (hipStream_t)stream));
 }
 
 int ertd_group_norm_act_bf16(const float* x, int Ca, const float* x2, int Cb, int B, int H,
@@ -926,6 +1024,7 @@ int ertd_unet_forward(const ertd_unet_config* c, const float* packed, const floa
   const Layout Lo = layout_with_freq(c);
   if (ws_bytes_for(c, Lo, B, L) > ws_bytes) return ERTD_ENOSPC;
   Walk w{c, &Lo, packed, (char*)ws, 0, B, (hipStream_t)stream, false};
+  w.cap = ws_bytes;
   const Fixed f = fixed(w, L);
   int r = prologue(w, f, cond, cond_stride, L);
   if (r != ERTD_OK) return r;

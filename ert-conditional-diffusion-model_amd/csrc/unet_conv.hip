@@ -451,8 +451,16 @@ static hipError_t launch_t(const ConvArgs& a, int B, hipStream_t s) {
   return launch_w<KS, MODE, ACT, 1>(a, B, s);
 }
 
+int conv_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B) {
+  if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN) return 0;   // conv_out
+  if (conv_in_ok(a, ks, mode, act)) return 0;
+  if (ks == 3 && mode == MODE_S1 && wino_dispatchable(a, B)) return wino_gn_parts(a, B);
+  return 0;
+}
+
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
+  if (a.gnp && conv_gn_parts(ks, mode, act, a, B) == 0) return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)

@@ -491,6 +491,35 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
     }
     store_tile(0, y[0]);
     store_tile(1, y[1]);
+    // GroupNorm partials of the stored output: the 16 lanes of a DPP row hold
+    // 2 x 16 tiles x 4 px = 128 pixels of sample itm.b for the same 4 channels
+    if (a.gnp && ksp == 1) {
+      float2 pr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sm = ((y[0][i][0][0] + y[0][i][0][1]) + (y[0][i][1][0] + y[0][i][1][1])) +
+                   ((y[1][i][0][0] + y[1][i][0][1]) + (y[1][i][1][0] + y[1][i][1][1]));
+        sm = row16_sum(sm);
+        const float mu = sm * (1.0f / 128.0f);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+              const float d = y[j][i][r][x] - mu;
+              q = __builtin_fmaf(d, d, q);
+            }
+        pr[i] = make_float2(sm, row16_sum(q));
+      }
+      if ((ln & 15) == 0) {
+        constexpr int np = TPR * TPR / 32;
+        const int part = 2 * itm.tblk + tbp;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.gnp[((size_t)itm.b * a.Cout + co0 + i) * np + part] = pr[i];
+      }
+    }
   }
 }
 
@@ -673,6 +702,21 @@ hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, 
   pack_wino_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cout, cin / WKC, total, dst,
                                                                     flipT);
   return hipGetLastError();
+}
+
+// parts per (sample, channel) of the GroupNorm partials the dispatched
+// Winograd kernel emits (none when it splits its K: the halves are summed by
+// a separate pass after the epilogue)
+int wino_gn_parts(const ConvArgs& a, int B) {
+  if (!wino_dispatchable(a, B)) return 0;
+  if (a.wpk_wino4 && wino4_ok(a.Cin, a.Ca, a.Cout, a.Wo, B)) {
+    if (a.ksplit_buf && wino4_ksplit(a.Cin, a.Cout, a.Wo, B)) return 0;
+    return (a.Wo / 4) * (a.Wo / 4) / 16;
+  }
+  const int base = (a.Wo / 2) * (a.Wo / 2) / 64 * (a.Cout / 64) * B;
+  const int nchunk = a.Cin / WKC;
+  if (a.ksplit_buf && nchunk % 2 == 0 && nchunk >= 4 && base < ksplit_items() * cu_count()) return 0;
+  return (a.Wo / 2) * (a.Wo / 2) / 32;
 }
 
 hipError_t launch_conv_wino(int act, const ConvArgs& a, int B, hipStream_t s) {

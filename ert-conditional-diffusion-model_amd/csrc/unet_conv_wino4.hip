@@ -583,6 +583,35 @@ __global__ __launch_bounds__(WT) void conv_wino4_kernel(ConvArgs a, int nitems, 
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[i][r] = y[i][r] + rv[i][r];
     }
+    // GroupNorm partials of the output: the 16 lanes of a DPP row hold 16 tiles
+    // x 16 px = 256 pixels of one sample for the same 4 channels.  Before the
+    // output stores: anything after them that reloads a spilled value waits
+    // (shared vmcnt) for every store of the item
+    if (a.gnp && ksp == 1) {
+      float2 pr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sm = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm += (y[i][r][0] + y[i][r][1]) + (y[i][r][2] + y[i][r][3]);
+        sm = row16_sum(sm);
+        const float mu = sm * (1.0f / 256.0f);
+        float q = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const float d = y[i][r][x] - mu;
+            q = __builtin_fmaf(d, d, q);
+          }
+        pr[i] = make_float2(sm, row16_sum(q));
+      }
+      if ((ln & 15) == 0) {
+        const int np = TS / 16, part = (flatw % TS) / 16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.gnp[((size_t)smpl * a.Cout + co0 + i) * np + part] = pr[i];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll

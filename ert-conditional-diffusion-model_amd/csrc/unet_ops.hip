@@ -83,6 +83,129 @@ hipError_t launch_gn_stats(const GnArgs& a, int B, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---- GroupNorm statistics from partials (unet.h, GnPartArgs) ---------------------
+// Partials of a tensor, parts of n = 256 pixels: one wave per 4 parts of one
+// (sample, channel) plane, one float4 per lane and part, every load issued
+// before the arithmetic; a butterfly over the wave (the same bits in every
+// lane) gives the part sum, then the squared deviations from the part mean
+// of the same registers.
+__global__ __launch_bounds__(256) void gn_partials_kernel(const float* __restrict__ x, int np,
+                                                          float2* __restrict__ out, long long nplanes) {
+  const long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);   // global wave
+  const int lane = threadIdx.x & 63;
+  const int groups4 = (np + 3) / 4;
+  const long long plane = w / groups4;
+  if (plane >= nplanes) return;
+  const int p0 = (int)(w - plane * groups4) * 4;
+  const float4* src = reinterpret_cast<const float4*>(x + plane * (long long)np * 256);
+  float4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = p0 + j < np ? src[(p0 + j) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (p0 + j >= np) break;
+    float sm = (v[j].x + v[j].y) + (v[j].z + v[j].w);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
+    const float mu = sm * (1.0f / 256.0f);
+    const float dx = v[j].x - mu, dy = v[j].y - mu, dz = v[j].z - mu, dw = v[j].w - mu;
+    float m2 = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, dw * dw)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m2 += __shfl_xor(m2, o);
+    if (lane == 0) out[plane * np + p0 + j] = make_float2(sm, m2);
+  }
+}
+
+hipError_t launch_gn_partials(const float* x, int C, int HW, int np, float2* out, int B, hipStream_t s) {
+  if (C < 1 || np < 1 || HW != np * 256) return hipErrorInvalidValue;
+  const long long nplanes = (long long)B * C;
+  const long long waves = nplanes * ((np + 3) / 4);
+  gn_partials_kernel<<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(x, np, out, nplanes);
+  return hipGetLastError();
+}
+
+// One wave per (sample, group): lanes take the group's (channel, part)
+// items k = lane, lane + 64, ... (channel-major, possibly across both tensors
+// of a skip concatenation), float64 sums reduced by a butterfly in a fixed
+// order: mean = sum S / N, then M2 = sum_p [M2_p + n_p (S_p / n_p - mean)^2]
+// (Chan et al.), var = M2 / N (biased, as GroupNorm); {scale, shift} as
+// gn_stats_kernel.
+__global__ __launch_bounds__(256) void gn_finalize_kernel(GnPartArgs a, int B) {
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wv >= B * a.groups) return;
+  const int b = wv / a.groups, g = wv - b * a.groups;
+  const int C = a.Ca + a.Cb, cpg = C / a.groups, c0 = g * cpg;
+  // items of the group: channels [c0, c0+cpg); channel c has np(c) parts
+  const int nA = c0 < a.Ca ? (a.Ca - c0 < cpg ? a.Ca - c0 : cpg) : 0;   // channels in tensor A
+  const int itemsA = nA * a.npa, items = itemsA + (cpg - nA) * (a.Cb > 0 ? a.npb : 0);
+  auto item = [&](int k, double& n) -> float2 {
+    if (k < itemsA) {
+      const int c = c0 + k / a.npa, p = k - (k / a.npa) * a.npa;
+      n = (double)(a.HW / a.npa);
+      return a.pa[((size_t)b * a.Ca + c) * a.npa + p];
+    }
+    const int kk = k - itemsA;
+    const int c = c0 + nA + kk / a.npb - a.Ca, p = kk - (kk / a.npb) * a.npb;
+    n = (double)(a.HW / a.npb);
+    return a.pb[((size_t)b * a.Cb + c) * a.npb + p];
+  };
+  // at most 4 items per lane held in registers (groups up to 256 items)
+  float2 it[4];
+  double nn[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = lane + 64 * j;
+    nn[j] = 0.0;
+    it[j] = k < items ? item(k, nn[j]) : make_float2(0.f, 0.f);
+  }
+  double S = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) S += (double)it[j].x;
+  for (int k = lane + 256; k < items; k += 64) {   // wider groups (one group over 512 channels)
+    double n;
+    S += (double)item(k, n).x;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) S += __shfl_xor(S, o);
+  const double N = (double)cpg * a.HW;
+  const double mean = S / N;
+  double M2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (nn[j] > 0.0) {
+      const double d = (double)it[j].x / nn[j] - mean;
+      M2 += (double)it[j].y + nn[j] * d * d;
+    }
+  for (int k = lane + 256; k < items; k += 64) {
+    double n;
+    const float2 q = item(k, n);
+    const double d = (double)q.x / n - mean;
+    M2 += (double)q.y + n * d * d;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) M2 += __shfl_xor(M2, o);
+  double var = M2 / N;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
+  if (a.mr && lane == 0) a.mr[(size_t)b * a.groups + g] = make_float2((float)mean, rstd);
+  for (int cl = lane; cl < cpg; cl += 64) {
+    const int c = c0 + cl;
+    const float scale = rstd * a.gamma[c];
+    const float shift = -scale * (float)mean + a.beta[c];
+    a.out[(size_t)b * C + c] = make_float2(scale, shift);
+  }
+}
+
+hipError_t launch_gn_finalize(const GnPartArgs& a, int B, hipStream_t s) {
+  const int C = a.Ca + a.Cb;
+  if (!a.pa || a.npa < 1 || a.Ca < 1 || (a.Cb > 0 && (!a.pb || a.npb < 1)) || a.groups < 1 ||
+      C % a.groups || a.HW % a.npa || (a.Cb > 0 && a.HW % a.npb))
+    return hipErrorInvalidValue;
+  const int n = B * a.groups;   // one wave each
+  gn_finalize_kernel<<<(n + 3) / 4, 256, 0, s>>>(a, B);
+  return hipGetLastError();
+}
+
 // ---- dense layers of the embedding path --------------------------------------------
 // One workgroup per (256 outputs, sample); the input row is formed once in LDS
 // (plain, SiLU, or the reference's sinusoid of t), then each thread runs one

@@ -75,6 +75,10 @@ SIGNATURES = {
                              _F, _F, _F, _VP, _VP, _SZ, _VP]),
     "ertd_postprocess": (_I, [_VP, ctypes.c_longlong, _I, ctypes.c_double, ctypes.c_double, _VP,
                               _VP, _VP, _VP, _VP, _VP]),
+    "ertd_conv2d_run": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP, _I,
+                             _VP, _SZ, _VP]),
+    "ertd_group_norm_partials": (_I, [_VP, _I, _I, _I, _I, _VP, _VP]),
+    "ertd_group_norm_finalize": (_I, [_VP, _I, _I, _VP, _I, _I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP]),
     "ertd_conv2d_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "ertd_conv2d": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP,
                          _I, _VP, _SZ, _VP]),

@@ -254,17 +254,35 @@ typedef struct ertd_unet_config {
  *   implicit GEMMs; ERTD_UNET_WINO=2 keeps F(2x2), 0 disables Winograd.
  * ertd_group_norm_stats: per (sample, channel) {gamma*rstd, beta-mean*gamma*rstd}
  *   of cat(x, x2) over `groups` groups (eps 1e-5), out (B, Ca+Cb) float2.
- * ertd_attention: qkv (B, 3C, N) -> out (B, C, N) = v softmax(q^T k / sqrt C)^T, N = 256. */
+ * ertd_attention: qkv (B, 3C, N) -> out (B, C, N) = v softmax(q^T k / sqrt C)^T, N = 256.
+ * ertd_group_norm_partials: parts (B, C, np, 2) = per (sample, channel, part of n = 256
+ *   pixels) {sum, sum (x - sum/n)^2} of x (B, C, HW); HW = 256 np.  The fp32
+ *   Winograd convs of the U-Net walk emit the same partials of their output from the
+ *   epilogue, so a GroupNorm does not re-read its input.
+ * ertd_group_norm_finalize: out (B, Ca+Cb) {scale, shift} exactly as ertd_group_norm_stats
+ *   (and mr (B, groups) {mean, rstd}, optional) from the partials of the two concatenated
+ *   inputs (pb = null when Cb = 0), combined per group in a fixed order in float64.  */
 size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision, int B, int H,
                                    int mode);
 int ertd_conv2d(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
                 const float* bias, int Cout, int ks, int mode, const float* gn, int act,
                 const float* ebias, int eb_stride, const float* res, float* out, int precision,
                 void* ws, size_t ws_bytes, void* stream);
+/* ertd_conv2d_run: the same conv reusing the packing a previous ertd_conv2d call with the
+ * same (Ca, Cb, B, H, Cout, ks, mode, act, precision) and weights left at the head of ws
+ * (no weight read, no pack kernel: the conv kernel alone, e.g. for per-kernel timing). */
+int ertd_conv2d_run(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* bias,
+                    int Cout, int ks, int mode, const float* gn, int act, const float* ebias,
+                    int eb_stride, const float* res, float* out, int precision, void* ws,
+                    size_t ws_bytes, void* stream);
 int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B, int HW,
                           int groups, const float* gamma, const float* beta, float* out,
                           void* stream);
 int ertd_attention(const float* qkv, int B, int C, int N, float* out, void* stream);
+int ertd_group_norm_partials(const float* x, int C, int B, int HW, int np, float* parts, void* stream);
+int ertd_group_norm_finalize(const float* pa, int npa, int Ca, const float* pb, int npb, int Cb, int B,
+                             int HW, int groups, const float* gamma, const float* beta, float* out,
+                             float* mr, void* stream);
 /* ertd_act_bf16: img [B][ceil(C/16)][Ho][Ho][16] bf16 (RNE) of act(cat(x, x2)*ss.x + ss.y)
  *   (act 0 none / 1 GN+SiLU / 2 GN; ss (B, C, 2) as ertd_group_norm_stats) or, with up = 1
  *   (act 0), of the nearest-x2 upsample of cat(x, x2) (Ho = 2H): the bf16 path's standalone

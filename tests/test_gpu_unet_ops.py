@@ -181,6 +181,42 @@ def test_group_norm_stats(Ca, Cb, H, G, cuda_dev):
     assert RN.rel_l2(y.double().numpy(), ref.double().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("Ca,Cb,H,G,npa,npb", [(64, 0, 64, 32, 16, 0), (128, 64, 32, 32, 4, 4),
+                                               (192, 64, 64, 32, 16, 16), (256, 256, 16, 32, 1, 1),
+                                               (512, 0, 16, 1, 1, 0), (100, 92, 32, 32, 4, 4)])
+def test_group_norm_from_partials(Ca, Cb, H, G, npa, npb, cuda_dev):
+    """GroupNorm statistics from per-part {sum, M2} partials (what the fp32
+    Winograd convs emit from their epilogue): finalize == ertd_group_norm_stats
+    within 1e-6, and the normalized tensor == torch's group_norm within 1e-5,
+    for groups straddling the skip concatenation and parts of different sizes."""
+    from ertdiff import _lib
+    lib = _lib.lib()
+    B = 3
+    x = (_rand((B, Ca, H, H), 51, 2.0) + 0.5).to(cuda_dev)
+    x2 = (_rand((B, Cb, H, H), 52) - 0.3).to(cuda_dev) if Cb else None
+    gamma, beta = (_rand((Ca + Cb,), 53) + 1).to(cuda_dev), _rand((Ca + Cb,), 54).to(cuda_dev)
+    s = _lib.stream_of(cuda_dev)
+    pa = torch.empty(B, Ca, npa, 2, device=cuda_dev)
+    assert lib.ertd_group_norm_partials(x.data_ptr(), Ca, B, H * H, npa, pa.data_ptr(), s) == 0
+    pb = None
+    if Cb:
+        pb = torch.empty(B, Cb, npb, 2, device=cuda_dev)
+        assert lib.ertd_group_norm_partials(x2.data_ptr(), Cb, B, H * H, npb, pb.data_ptr(), s) == 0
+    ss = torch.empty(B, Ca + Cb, 2, device=cuda_dev)
+    mr = torch.empty(B, G, 2, device=cuda_dev)
+    assert lib.ertd_group_norm_finalize(pa.data_ptr(), npa, Ca, None if pb is None else pb.data_ptr(), npb,
+                                        Cb, B, H * H, G, gamma.data_ptr(), beta.data_ptr(), ss.data_ptr(),
+                                        mr.data_ptr(), s) == 0
+    ref_ss = group_norm_stats(x, G, gamma, beta, x2=x2)
+    assert torch.allclose(ss, ref_ss, rtol=1e-6, atol=1e-6)
+    xin = (x if x2 is None else torch.cat([x, x2], 1)).cpu()
+    y = xin * ss.cpu()[..., 0][:, :, None, None] + ss.cpu()[..., 1][:, :, None, None]
+    ref = F.group_norm(xin, G, gamma.cpu(), beta.cpu(), eps=1e-5)
+    err = RN.rel_l2(y.double().numpy(), ref.double().numpy())
+    record_error(f"gn_from_partials_{Ca}_{Cb}_{H}_{G}", err)
+    assert err < 1e-5, err
+
+
 @pytest.mark.parametrize("Ca,Cb,H,silu", [(64, 0, 64, True), (128, 64, 32, True),
                                           (256, 128, 16, True), (192, 0, 32, False),
                                           (512, 0, 16, True), (64, 0, 16, True)])
@@ -268,3 +304,25 @@ def test_act_bf16_image(Ca, Cb, H, act, up, cuda_dev):
     got_f, ref_f = got.view(torch.bfloat16).float(), ref.view(torch.bfloat16).float()
     ulp = (ref_f.abs() * 2.0 ** -7).clamp_min(1e-6)
     assert bool(((got_f - ref_f).abs() <= ulp).all())
+
+
+def test_conv2d_run_reuses_packing(cuda_dev):
+    """ertd_conv2d_run (the conv kernel alone on a packing an earlier
+    ertd_conv2d left in the workspace) == ertd_conv2d bit for bit."""
+    from ertdiff import _lib
+    lib = _lib.lib()
+    B, C, H = 4, 64, 32
+    x = _rand((B, C, H, H), 61).to(cuda_dev)
+    w = _rand((C, C, 3, 3), 62, 1.0 / np.sqrt(9 * C)).to(cuda_dev)
+    b = _rand((C,), 63, 0.1).to(cuda_dev)
+    gn = torch.stack([_rand((B, C), 64, 0.3) + 1.0, _rand((B, C), 65, 0.2)], -1).to(cuda_dev)
+    y1, y2 = torch.empty(B, C, H, H, device=cuda_dev), torch.empty(B, C, H, H, device=cuda_dev)
+    n = lib.ertd_conv2d_workspace_bytes(C, C, 3, 0, B, H, 0)
+    ws = torch.empty(n, dtype=torch.uint8, device=cuda_dev)
+    s = _lib.stream_of(cuda_dev)
+    assert lib.ertd_conv2d(x.data_ptr(), C, None, 0, B, H, w.data_ptr(), b.data_ptr(), C, 3, 0,
+                           gn.data_ptr(), 1, None, 0, None, y1.data_ptr(), 0, ws.data_ptr(), n, s) == 0
+    assert lib.ertd_conv2d_run(x.data_ptr(), C, None, 0, B, H, b.data_ptr(), C, 3, 0, gn.data_ptr(), 1,
+                               None, 0, None, y2.data_ptr(), 0, ws.data_ptr(), n, s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
