@@ -430,11 +430,14 @@ def bench_conv_kernels(dev, B=64, reps=20):
 def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000, rank=0, world=1):
     """The reference train step (:309-320) on the U-Net denoiser: q_sample, the
     HIP forward with saved activations, the hand-written HIP backward, MSE and
-    the multi-tensor Adam kernel (ertdiff.unet_train_step), fp32, batch B per
-    GPU.  N > 1: data parallel (identical replicas, each rank its own shard of
-    the global batch, gradients averaged by one bucketed RCCL all-reduce per
-    step); weak scaling, time = max over ranks."""
-    from ertdiff.unet_train import unet_train_step
+    the multi-tensor Adam kernel, fp32, batch B per GPU -- through
+    ertdiff.UNetTrainPlan (the device work of a step captured once as a graph,
+    Adam launched after each replay); the eager host walk (unet_train_step)
+    timed beside it.  N > 1: data parallel (identical replicas, each rank its own
+    shard of the global batch, gradients averaged by one bucketed RCCL
+    all-reduce per step); weak scaling, time = max over ranks."""
+    from ertdiff.unet import CONFIGS, unet_flops
+    from ertdiff.unet_train import UNetTrainPlan, unet_train_step
     model = ertdiff.ConditionalUNet.from_config(name, seed=0).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     g = torch.Generator(device=dev).manual_seed(11 + rank)
@@ -442,31 +445,53 @@ def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000, rank=0, wo
     x0 = torch.randn(B, P_, device=dev, generator=g)
     cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
     _, _, ab = ertdiff.get_diffusion_schedule(T, device=dev)
-    ts = torch.randint(0, T, (steps + warmup, B), device=dev, generator=g)
-    ns = torch.randn(steps + warmup, B, P_, device=dev, generator=g)
+    n_eager = 3
+    ts = torch.randint(0, T, (steps + warmup + n_eager, B), device=dev, generator=g)
+    ns = torch.randn(steps + warmup + n_eager, B, P_, device=dev, generator=g)
+
+    def timed(fn, i0, n):
+        torch.cuda.synchronize(dev)
+        barrier(world)
+        t0 = time.perf_counter()
+        for i in range(n):
+            loss = fn(i0 + i)
+        torch.cuda.synchronize(dev)
+        barrier(world)
+        el = time.perf_counter() - t0
+        if world > 1:
+            e = torch.tensor([el], device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el, loss
+
+    def eager(i):
+        return unet_train_step(model, opt, x0, cond, T, ab, t=ts[i], noise=ns[i], return_tensor=True)
+    eager(0)
+    el_e, _ = timed(eager, 1, n_eager - 1)
+    plan = UNetTrainPlan(model, opt, B, L_MEAS, T, ab)
+
+    def graphed(i):
+        return plan.step(x0, cond, t=ts[i], noise=ns[i], return_tensor=True)
     for i in range(warmup):
-        unet_train_step(model, opt, x0, cond, T, ab, t=ts[i], noise=ns[i], return_tensor=True)
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    t0 = time.perf_counter()
-    for i in range(steps):
-        loss = unet_train_step(model, opt, x0, cond, T, ab, t=ts[warmup + i], noise=ns[warmup + i],
-                               return_tensor=True)
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    el = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([el], device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        el = float(e.item())
+        graphed(n_eager + i)
+    el, loss = timed(graphed, n_eager + warmup, steps)
+    step_s = el / steps
+    fl = unet_flops(**CONFIGS[name])
+    # forward + input gradient + weight gradient of every conv (algorithmic, direct count)
+    conv_tf = 3 * fl["conv"] * B / step_s / 1e12
     return {"unet_train_steps_per_s": round(steps / el, 3), "model": name, "batch_per_gpu": B,
             "global_batch": B * world, "samples_per_s": round(steps * B * world / el, 1),
-            "ms_per_step": round(el / steps * 1e3, 2), "steps": steps, "warmup": warmup,
+            "ms_per_step": round(step_s * 1e3, 2), "steps": steps, "warmup": warmup,
+            "eager_ms_per_step": round(el_e / (n_eager - 1) * 1e3, 2),
+            "conv_tflops_alg": round(conv_tf, 2), "conv_frac_fp32_peak": round(conv_tf / PEAK_FP32_TFLOPS, 4),
+            "flop_basis": "3 x the direct-convolution FLOP of the U-Net forward (forward, input "
+                          "gradient, weight gradient) x B per step; Winograd layers execute fewer",
             "final_loss_rank0": round(float(loss), 5), "dtype": "f32",
             "scaling": "weak" if world > 1 else None,
             "parallelism": f"dp{world} (one bucketed RCCL all-reduce of the gradients per step)"
             if world > 1 else "1 GPU",
-            "note": "wall clock around the steps (host walk + HIP kernels), max over ranks"}
+            "note": "wall clock around the steps (graph replay + eager Adam; eager = the Python "
+                    "walk of unet_train_step), max over ranks"}
 
 
 def _host_cpus():
@@ -743,7 +768,9 @@ def bench_unet_extra(name, B, precision, steps, warmup, T, rank, world, dev, cpu
     del plan
     step_s = el / steps
     conv_tf = fl["conv"] * B / step_s / 1e12
-    peak = PEAK_FP32_TFLOPS if precision == "fp32" else PEAK_BF16_TFLOPS
+    # split bf16 runs three bf16 MFMAs per product: its effective conv peak is a third
+    peak = {"fp32": PEAK_FP32_TFLOPS, "bf16": PEAK_BF16_TFLOPS,
+            "bf16x3": round(PEAK_BF16_TFLOPS / 3, 1)}[precision]
     out = {"config": f"{name} B={B} per GPU, {precision}, T={T}", "value": round(world * steps / el, 3),
             "unit": "denoising-steps/sec", "scaling": "weak", "ms_per_step": round(step_s * 1e3, 4),
             "conv_tflops": round(conv_tf, 2), "conv_peak_tflops": peak,
@@ -912,12 +939,16 @@ def main():
     if not a.no_u3:
         extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev,
                                                      None if a.no_cpu_baseline else a.cpu_unet_seconds)
+        # split-bf16 operands: the same config inside the north star's 1e-4
+        # (tests/test_gpu_unet.py::test_unet_bf16x3_sampler_full_chain_vs_fp32_golden)
+        extra["configs2_u3_bf16x3"] = bench_unet_extra("U3", 256, "bf16x3", 20, 3, T, rank, world, dev)
     if not a.no_ensemble:
         extra["configs3_ensemble"] = bench_ensemble(a.ensemble, "U2", a.ensemble_steps, 2, T, rank,
                                                     world, dev)
     if not a.no_u5:
         extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev,
                                                      None if a.no_cpu_baseline else a.cpu_unet_seconds)
+        extra["configs4_u5_bf16x3"] = bench_unet_extra("U5", 64, "bf16x3", 10, 2, T, rank, world, dev)
     if not a.no_hbm_kernels:
         extra["hbm_kernels"] = bench_hbm_kernels(dev)
     if not a.no_unet_train:

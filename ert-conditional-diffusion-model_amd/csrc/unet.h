@@ -50,6 +50,8 @@ struct ConvArgs {
   float2* gnp;           // optional (B, Cout, np): GroupNorm partials of the OUTPUT (after
                          // bias / emb / residual), np = conv_gn_parts(...) (0: the dispatched
                          // kernel emits none and gnp must be null)
+  int split;             // bf16 kernels: 1 = split-bf16 operands (hi + lo planes: weights
+                         // packed with split = true, images of conv_bf16_image_bytes(.., true))
 };
 
 // GroupNorm statistics without a second read of the activation: the fp32
@@ -91,18 +93,22 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
 // bf16-operand variant (unet_conv_bf16.hip): same arguments, wpk packed by
 // launch_pack_conv_bf16
 hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
-size_t conv_packed_floats_bf16(int cin, int cout, int ks);
+// split: the split-bf16 layouts (two bf16 planes, hi and lo = RNE(x - hi))
+size_t conv_packed_floats_bf16(int cin, int cout, int ks, bool split = false);
 hipError_t launch_act_bf16(const ConvArgs& a, int act, bool up, int B, hipStream_t s);
-size_t conv_bf16_image_bytes(int cin, int B, int H, int W);
+size_t conv_bf16_image_bytes(int cin, int B, int H, int W, bool split = false);
 hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, float* dst,
-                                 hipStream_t s);
+                                 hipStream_t s, bool split = false);
+// weight packing a conv_in / conv_out launch reads: 0 fp32, 1 bf16 (the staged
+// input is rounded to bf16 too), 2 split bf16 (weight = hi + lo, fp32 input)
+enum PackKind { PK_F32 = 0, PK_BF16 = 1, PK_SPLIT = 2 };
 // Cout = 1, 3x3 stride 1 (conv_out; unet_conv_out.hip): per-pixel fp32 fma
-// chains, weights read from either packing (bf16: staged input rounded too)
-hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStream_t s);
+// chains, weights read from the model's packing
+hipError_t launch_conv_out(int act, const ConvArgs& a, int B, int pk, hipStream_t s);
 // Cin = 1, 3x3 stride 1, no activation / emb / residual (conv_in; unet_conv_out.hip):
 // one thread per output pixel, every output channel's 9-tap fp32 fma chain
 bool conv_in_ok(const ConvArgs& a, int ks, int mode, int act);
-hipError_t launch_conv_in(const ConvArgs& a, int B, bool bf16, hipStream_t s);
+hipError_t launch_conv_in(const ConvArgs& a, int B, int pk, hipStream_t s);
 // fp32 3x3 stride-1 convs by Winograd F(2x2,3x3) (unet_conv_wino.hip): eligible
 // shapes (Cin, Ca multiples of 8, Cout of 64, W in 16..128; ERTD_UNET_WINO=0
 // disables), the U = G g G^T packing (0 floats: shape not eligible), launch
@@ -148,7 +154,8 @@ hipError_t launch_gn_stats(const GnArgs& a, int B, hipStream_t s);
 // launch_gn_stats and the [B][C/16][H][W][16] image; shapes gated by
 // gn_act_bf16_fits (C/16 whole, <= 64 activations per thread)
 bool gn_act_bf16_fits(int C, int groups, int HW);
-hipError_t launch_gn_act_bf16(const GnArgs& a, bool silu, void* bimg, int B, hipStream_t s);
+hipError_t launch_gn_act_bf16(const GnArgs& a, bool silu, void* bimg, int B, hipStream_t s,
+                              bool split = false);
 
 // y[b][o] = bias[o] (+ add[b][o]) + sum_k Wt[k][o] * in(b, k)
 enum DenseIn { DIN_PLAIN = 0, DIN_SILU = 1, DIN_SINUSOID = 2 };

@@ -42,7 +42,9 @@ bool cfg_ok(const ertd_unet_config* c) {
     if (c->ch_mult[i] < 1 || C % c->groups) return false;
   }
   if (c->ch % c->groups) return false;
-  if (c->precision != ERTD_PREC_FP32 && c->precision != ERTD_PREC_BF16) return false;
+  if (c->precision != ERTD_PREC_FP32 && c->precision != ERTD_PREC_BF16 &&
+      c->precision != ERTD_PREC_BF16X3)
+    return false;
   if (c->attn) {
     const int Cm = c->ch * c->ch_mult[c->n_levels - 1];
     const int r = c->image >> (c->n_levels - 1);
@@ -52,6 +54,9 @@ bool cfg_ok(const ertd_unet_config* c) {
 }
 
 int temb(const ertd_unet_config* c) { return 4 * c->ch; }
+
+// the bf16-operand conv kernels (plain or split): bf16 packings and images
+bool bf_prec(int p) { return p == ERTD_PREC_BF16 || p == ERTD_PREC_BF16X3; }
 
 std::vector<Param> enumerate(const ertd_unet_config* c) {
   std::vector<Param> P;
@@ -169,8 +174,9 @@ Layout layout(const ertd_unet_config* c) {
     if (ends_with(p.name, ".emb.weight") || ends_with(p.name, ".emb.bias")) continue;
     L.off[p.name] = o;
     if (p.shape.size() == 4)
-      o += a64(c->precision == ERTD_PREC_BF16
-                   ? conv_packed_floats_bf16(p.shape[1], p.shape[0], p.shape[2])
+      o += a64(bf_prec(c->precision)
+                   ? conv_packed_floats_bf16(p.shape[1], p.shape[0], p.shape[2],
+                                             c->precision == ERTD_PREC_BF16X3)
                    : (ends_with(p.name, ".upsample.weight")
                           ? conv_packed_floats_up(p.shape[1], p.shape[0])
                           : conv_packed_floats(p.shape[1], p.shape[0], p.shape[2])));
@@ -282,7 +288,7 @@ struct Walk {
     }
     if (dry) return;
     GnArgs g{A, Bs, Ca, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"), gnbuf};
-    if (fusable && c->precision == ERTD_PREC_BF16 && fuse_gn_env() &&
+    if (fusable && bf_prec(c->precision) && fuse_gn_env() &&
         gn_act_bf16_fits(Ca + Cb, c->groups, HW)) {
       pend = g;
       has_pend = true;
@@ -310,9 +316,10 @@ struct Walk {
     float* kbuf = want_split ? alloc((size_t)B * Cout * Ho * Wo) : nullptr;
     // bf16 stride-1 convs stage a pre-transformed bf16 copy of their input
     float* bimg = nullptr;
-    if (c->precision == ERTD_PREC_BF16 && ks == 3 && Cout > 1 &&
+    const bool split = c->precision == ERTD_PREC_BF16X3;
+    if (bf_prec(c->precision) && ks == 3 && Cout > 1 &&
         ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
-      bimg = alloc((conv_bf16_image_bytes(Ca + Cb, B, Ho, Wo) + 3) / 4);
+      bimg = alloc((conv_bf16_image_bytes(Ca + Cb, B, Ho, Wo, split) + 3) / 4);
     // fp32: GroupNorm partials of the output, when the dispatched kernel emits
     // them (the geometry-only part of the dispatch: sentinel pointers in dry runs)
     float2* gnp = nullptr;
@@ -352,17 +359,18 @@ struct Walk {
     a.bimg = bimg;
     a.ksplit_buf = kbuf;
     a.gnp = gnp;
+    a.split = split ? 1 : 0;
     if (has_pend) {
       has_pend = false;
       if (bimg && ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) {
-        chk(launch_gn_act_bf16(pend, true, bimg, B, s));
+        chk(launch_gn_act_bf16(pend, true, bimg, B, s, split));
         a.bimg_ready = 1;
       } else {
         chk(launch_gn_stats(pend, B, s));
       }
     }
-    chk(c->precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
-                                       : launch_conv(ks, mode, act, a, B, s));
+    chk(bf_prec(c->precision) ? launch_conv_bf16(ks, mode, act, a, B, s)
+                              : launch_conv(ks, mode, act, a, B, s));
     return out;
   }
 
@@ -689,28 +697,28 @@ struct Conv2dWs {
 bool conv2d_geom_ok(int cin, int cout, int ks, int precision, int B, int H, int mode) {
   return cin >= 1 && cout >= 1 && (ks == 1 || ks == 3) && B >= 1 && H >= 1 && mode >= MODE_S1 &&
          mode <= MODE_UP && !(ks == 1 && mode != MODE_S1) &&
-         (precision == ERTD_PREC_FP32 || precision == ERTD_PREC_BF16);
+         (precision == ERTD_PREC_FP32 || bf_prec(precision));
 }
 
 Conv2dWs conv2d_ws(int cin, int ca, int cout, int ks, int precision, int B, int H, int mode, int act) {
   Conv2dWs w;
-  size_t f = precision == ERTD_PREC_BF16 ? conv_packed_floats_bf16(cin, cout, ks)
-                                         : conv_packed_floats(cin, cout, ks);
+  const bool bf = bf_prec(precision), split = precision == ERTD_PREC_BF16X3;
+  size_t f = bf ? conv_packed_floats_bf16(cin, cout, ks, split) : conv_packed_floats(cin, cout, ks);
   // fp32 3x3 convs may be Upsample convs (sub-pixel packing)
-  if (precision != ERTD_PREC_BF16 && ks == 3 && conv_packed_floats_up(cin, cout) > f)
+  if (!bf && ks == 3 && conv_packed_floats_up(cin, cout) > f)
     f = conv_packed_floats_up(cin, cout);
   // ... and stride-1 ones carry the Winograd packing behind the direct one
-  if (precision != ERTD_PREC_BF16 && ks == 3)
+  if (!bf && ks == 3)
     f = a64(f) + std::max(conv_packed_floats_wino(cin, cout), conv_packed_floats_wino4(cin, cout));
   w.pack_floats = f;
   const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
-  if (precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && cout > 1 &&
+  if (!bf && ks == 3 && mode == MODE_S1 && cout > 1 &&
       (conv_packed_floats_wino(cin, cout) > 0 || conv_packed_floats_wino4(cin, cout) > 0) &&
       conv_wino_ok(cin, ca, cout, Ho) && wino_ksplit_wanted(cin, cout, Ho, B))
     w.kbuf_floats = (size_t)B * cout * Ho * Ho;
-  if (precision == ERTD_PREC_BF16 && ks == 3 && cout > 1 &&
+  if (bf && ks == 3 && cout > 1 &&
       ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
-    w.bimg_bytes = conv_bf16_image_bytes(cin, B, Ho, Ho);
+    w.bimg_bytes = conv_bf16_image_bytes(cin, B, Ho, Ho, split);
   return w;
 }
 
@@ -749,13 +757,14 @@ int conv2d_impl(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   void* bimg = need.bimg_bytes ? (void*)(pk + a64(need.pack_floats) + a64(need.kbuf_floats)) : nullptr;
   // the Winograd path reads only its own packing: skip the direct one then
   const int Ho_ = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
-  const bool wino4 = precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
+  const bool bf = bf_prec(precision), split = precision == ERTD_PREC_BF16X3;
+  const bool wino4 = !bf && ks == 3 && mode == MODE_S1 && Cout > 1 &&
                      conv_packed_floats_wino4(Cin, Cout) > 0 && wino4_ok(Cin, Ca, Cout, Ho_, B);
-  const bool wino = wino4 || (precision != ERTD_PREC_BF16 && ks == 3 && mode == MODE_S1 && Cout > 1 &&
+  const bool wino = wino4 || (!bf && ks == 3 && mode == MODE_S1 && Cout > 1 &&
                               conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho_));
   hipError_t e = hipSuccess;
   if (!wino && pack)
-    e = precision == ERTD_PREC_BF16 ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s)
+    e = bf ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s, split)
         : (ks == 3 && mode == MODE_UP) ? launch_pack_conv_up(w, Cin, Cout, pk, s)
                                        : launch_pack_conv(w, Cin, Cout, ks, pk, s);
   if (e != hipSuccess) return (int)e;
@@ -775,8 +784,8 @@ int conv2d_impl(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
     a.ksplit_buf = kbuf;
   }
   a.bimg = bimg;
-  e = precision == ERTD_PREC_BF16 ? launch_conv_bf16(ks, mode, act, a, B, s)
-                                  : launch_conv(ks, mode, act, a, B, s);
+  a.split = split ? 1 : 0;
+  e = bf ? launch_conv_bf16(ks, mode, act, a, B, s) : launch_conv(ks, mode, act, a, B, s);
   return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
 }
 }  // namespace
@@ -989,9 +998,9 @@ int ertd_unet_pack(const ertd_unet_config* c, const float* const* params, const 
       e = hipMemcpyAsync(packed + L.ball + col, src, p.numel() * sizeof(float),
                          hipMemcpyDeviceToDevice, s);
     } else if (p.shape.size() == 4) {
-      e = c->precision == ERTD_PREC_BF16
+      e = bf_prec(c->precision)
               ? launch_pack_conv_bf16(src, p.shape[1], p.shape[0], p.shape[2],
-                                      packed + L.off.at(p.name), s)
+                                      packed + L.off.at(p.name), s, c->precision == ERTD_PREC_BF16X3)
               : (ends_with(p.name, ".upsample.weight")
                      ? launch_pack_conv_up(src, p.shape[1], p.shape[0], packed + L.off.at(p.name), s)
                      : launch_pack_conv(src, p.shape[1], p.shape[0], p.shape[2],
@@ -1078,7 +1087,7 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
   // chain vs 152.6 forked); the bf16 path keeps it (U3 B=256: 94.0 vs 93.1).
   // ERTD_UNET_SIDE=0/1 overrides (A/B).
   const char* sv = getenv("ERTD_UNET_SIDE");
-  const bool side = sv ? atoi(sv) != 0 : c->precision == ERTD_PREC_BF16;
+  const bool side = sv ? atoi(sv) != 0 : bf_prec(c->precision);
   if (e == hipSuccess && side) {
     e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evf, hipEventDisableTiming);

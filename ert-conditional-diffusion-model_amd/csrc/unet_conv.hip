@@ -41,6 +41,7 @@
 // the summed weights.  grid.x = 4 classes x pixel tiles; the epilogue
 // scatters each class to its output parity.
 #include <cstdlib>
+#include <type_traits>
 
 #include "unet.h"
 
@@ -73,8 +74,9 @@ struct ConvGeom {
   static constexpr int WST = MODE == MODE_S2 ? 2 * WO : WO;   // staged image width
   static constexpr int R = BM / WO;                   // output rows per workgroup
   static constexpr int IR = KS == 1 ? R : (KS == 2 ? R + 1 : (MODE == MODE_S2 ? 2 * R + 1 : R + 2));
-  static constexpr int IP = WST + 2;                  // LDS row pitch (zero column each side)
-  static constexpr int CP = IR * IP;                  // channel pitch
+  // 1x1: the chunk image is [channel][BM pixels] (no halo, no row pitch)
+  static constexpr int IP = KS == 1 ? BM : WST + 2;   // LDS row pitch (zero column each side)
+  static constexpr int CP = KS == 1 ? BM : IR * IP;   // channel pitch
   static constexpr int CKK = conv_ck(KS);             // input channels per chunk
   static constexpr int CH = CKK / 2;                  // channels per lane half
   static constexpr int HP = CH * CP + (MODE == MODE_S2 ? 1 : 0);  // lane-half pitch
@@ -84,12 +86,14 @@ struct ConvGeom {
   static constexpr int WB = (BN / 32) * TW;           // weight floats per buffer
   static constexpr int RSTEP = NTHR / WST;            // staged rows per thread pass
   static constexpr int NROWS = CKK * IR;
-  static constexpr int NIT = (NROWS + RSTEP - 1) / RSTEP;
+  static constexpr int NIT = KS == 1 ? CKK * BM / 4 / NTHR      // 1x1: float4s per thread
+                                     : (NROWS + RSTEP - 1) / RSTEP;
   static constexpr int NGL = WB / 256;                // 16-B-per-lane DMA instructions per chunk
   static constexpr size_t LDS = (size_t)(2 * XB + 2 * WB) * sizeof(float);
   static_assert(BM % WO == 0, "tile must hold whole output rows");
   static_assert(WST <= NTHR, "staged row wider than the workgroup");
   static_assert(WB % 256 == 0, "weight slice must be whole DMA instructions");
+  static_assert(KS != 1 || (CKK * BM / 4) % NTHR == 0, "1x1: whole float4s per thread");
 };
 
 // STG = input staging schedule: 0 = rows loaded one chunk ahead, LDS stores
@@ -124,7 +128,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   if constexpr (ACT != ACT_NONE) {
     for (int c = tid; c < Cin; c += NTHR) gtab[c] = a.gn[(size_t)b * Cin + c];
   }
-  for (int r = tid; r < 2 * CK * G::IR; r += NTHR) {  // rows of [buf][c][row]
+  for (int r = tid; KS != 1 && r < 2 * CK * G::IR; r += NTHR) {  // rows of [buf][c][row]
     const int buf = r / (CK * G::IR), rem = r - buf * (CK * G::IR);
     const int c = rem / G::IR, rr = rem - c * G::IR;
     float* row = xim + buf * G::XB + (c / G::CH) * G::HP + (c % G::CH) * G::CP + rr * G::IP;
@@ -143,10 +147,26 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
   const int sx = MODE == MODE_UP ? (col >> 1) : col;
   constexpr size_t plane = (size_t)HS * HS;
 
-  float stg[G::NIT];
+  // 1x1: a chunk is 32 channel rows of BM contiguous pixels -- float4 loads
+  // and ds_write_b128 (4 per thread at BM = 128), no halo, no row arithmetic
+  using StgT = std::conditional_t<KS == 1, float4, float>;
+  StgT stg[G::NIT];
   // branch-free: out-of-image / padded-channel elements load a valid address
   // and are replaced by zero
   auto load_chunk = [&](int k) {
+    if constexpr (KS == 1) {
+#pragma unroll
+      for (int it = 0; it < G::NIT; ++it) {
+        const int q = tid + it * NTHR;                 // float4 of the chunk
+        const int c = q / (G::BM / 4), p4 = q - c * (G::BM / 4);
+        const int cg = k * CK + c;
+        const int cgc = cg < Cin ? cg : 0;
+        const float* src = cgc < Ca ? a.srcA + ((size_t)b * Ca + cgc) * plane
+                                    : a.srcB + ((size_t)b * a.Cb + (cgc - Ca)) * plane;
+        stg[it] = *reinterpret_cast<const float4*>(src + p0 + 4 * p4);
+      }
+      return;
+    } else {
 #pragma unroll
     for (int it = 0; it < G::NIT; ++it) {
       const int fr = rs0 + it * G::RSTEP;
@@ -160,9 +180,33 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
                                   : a.srcB + ((size_t)b * a.Cb + (cgc - Ca)) * plane;
       stg[it] = src[sy * HS + sx];   // raw; the zero select happens in store_chunk
     }
+    }
   };
   // one staged element: GroupNorm(+SiLU) and the LDS write (element it of chunk k)
   auto store_elem = [&](int it, int k, float* img) {
+    if constexpr (KS == 1) {
+      const int q = tid + it * NTHR;
+      const int c = q / (G::BM / 4), p4 = q - c * (G::BM / 4);
+      const int cg = k * CK + c;
+      float4 v = stg[it];
+      if constexpr (ACT != ACT_NONE) {
+        const float2 g = gtab[cg < Cin ? cg : 0];
+        v.x = fmaf(v.x, g.x, g.y);
+        v.y = fmaf(v.y, g.x, g.y);
+        v.z = fmaf(v.z, g.x, g.y);
+        v.w = fmaf(v.w, g.x, g.y);
+        if constexpr (ACT == ACT_GN_SILU) {
+          v.x = v.x * __builtin_amdgcn_rcpf(1.0f + __expf(-v.x));
+          v.y = v.y * __builtin_amdgcn_rcpf(1.0f + __expf(-v.y));
+          v.z = v.z * __builtin_amdgcn_rcpf(1.0f + __expf(-v.z));
+          v.w = v.w * __builtin_amdgcn_rcpf(1.0f + __expf(-v.w));
+        }
+      }
+      if (cg >= Cin) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      // channel c of the chunk is lane half c / CH's channel c % CH
+      *reinterpret_cast<float4*>(img + (c / G::CH) * G::HP + (c % G::CH) * G::CP + 4 * p4) = v;
+      return;
+    } else {
     const int fr = rs0 + it * G::RSTEP;
     if (fr < G::NROWS) {
       const int c = fr / G::IR, r = fr - c * G::IR;
@@ -176,6 +220,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
         if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
       }
       img[(c / G::CH) * G::HP + (c % G::CH) * G::CP + r * G::IP + col + 1] = ok ? v : 0.f;
+    }
     }
   };
   auto store_chunk = [&](int k, float* img) {
@@ -218,7 +263,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
     const int pl = wpx * 32 * TPX + t * 32 + l32;
     const int oyl = pl / WO, ox = pl - oyl * WO;
     int rb, cb;
-    if constexpr (KS == 1) { rb = oyl; cb = ox + 1; }
+    if constexpr (KS == 1) { rb = 0; cb = pl; }
     else if constexpr (KS == 2) { rb = oyl; cb = ox + pb; }
     else if constexpr (MODE == MODE_S2) { rb = 2 * oyl; cb = 2 * ox; }
     else { rb = oyl; cb = ox; }
@@ -415,7 +460,14 @@ static hipError_t launch_p(const ConvArgs& a, int B, hipStream_t s) {
   // measured per layer (U2 B=64, profiles/r01_unet_layers.txt era): TPX=2 wins
   // for the 3x3 stride-1 and sub-pixel Upsample convs (32x32 level -7..-9 %,
   // -270 us per step in all), TPX=1 for 1x1 (8x at 64x64) and stride 2
-  if (tpx == 0) tpx = ((KS == 3 && MODE == MODE_S1) || MODE == MODE_UPP) ? 2 : 1;
+  // 1x1 since its float4 staging: TPX = 2 (U2 B=64 205.5 vs 202.9 steps/s, same box)
+  if (tpx == 0) tpx = ((KS == 3 && MODE == MODE_S1) || MODE == MODE_UPP || KS == 1) ? 2 : 1;
+  // ERTD_UNET_TPX1=1|2 picks the 1x1 convs' wave tile alone (A/B); 0 = the above
+  static const int t1 = [] {
+    const char* e = getenv("ERTD_UNET_TPX1");
+    return e ? atoi(e) : 0;
+  }();
+  if (KS == 1 && t1 > 0) tpx = t1;
   (void)wg2;
   if constexpr (32 * (4 / WCO) >= WO) {
     if (tpx == 1) return launch_g<KS, MODE, ACT, WCO, WO, 1>(a, B, s);
@@ -464,8 +516,8 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)
-    return launch_conv_out(act, a, B, false, s);
-  if (conv_in_ok(a, ks, mode, act)) return launch_conv_in(a, B, false, s);
+    return launch_conv_out(act, a, B, PK_F32, s);
+  if (conv_in_ok(a, ks, mode, act)) return launch_conv_in(a, B, PK_F32, s);
   if (ks == 3 && mode == MODE_S1 && wino_dispatchable(a, B))
     return launch_conv_wino(act, a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_t<3, MODE_S1, ACT_NONE>(a, B, s);

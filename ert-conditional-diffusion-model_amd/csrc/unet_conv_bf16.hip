@@ -28,13 +28,23 @@ __device__ __forceinline__ unsigned bf16_bits(float v) {  // round to nearest ev
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 
+// the split-bf16 low part: bf16 RNE of v - hi (exact in fp32)
+__device__ __forceinline__ unsigned bf16_lo_bits(float v, unsigned hi) {
+  return bf16_bits(v - __uint_as_float(hi << 16));
+}
+
 __device__ __forceinline__ unsigned lds_addr_h(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
 __host__ __device__ constexpr int convh_ck(int ks) { return ks == 3 ? 16 : 32; }
 
-template <int KS, int MODE, int WO, int TPX>
+// SP = operand planes: 1 = bf16, 2 = split bf16 (x = hi + lo, both bf16 RNE;
+// every product as lo_a*hi_b + hi_a*lo_b + hi_a*hi_b on the MFMA, fp32
+// accumulate: ~2^-16 relative per product instead of bf16's 2^-8).  A split
+// pixel record is [16 hi][16 lo] bf16 (64 B), a split weight slice [hi steps]
+// [lo steps] per (co tile, chunk).
+template <int KS, int MODE, int WO, int TPX, int SP = 1>
 struct GeomH {
   static constexpr int BM = 128 * TPX;               // output pixels per workgroup
   static constexpr int BN = 64;                      // output channels per workgroup
@@ -46,9 +56,10 @@ struct GeomH {
   static constexpr int NG = CKB / 16;                 // 16-channel groups per chunk
   static constexpr int TAPS = KS * KS;
   static constexpr int SPC = TAPS * NG;               // k-steps per chunk
-  static constexpr int GB = IR * IP * 32;             // bytes per 16-channel group image
+  static constexpr int PB = 32 * SP;                  // bytes per staged pixel record
+  static constexpr int GB = IR * IP * PB;             // bytes per 16-channel group image
   static constexpr int XB = NG * GB;                  // input image bytes per buffer
-  static constexpr int TWB = SPC * 64 * 16;           // weight bytes per 32-co tile and chunk
+  static constexpr int TWB = SPC * 64 * 16 * SP;      // weight bytes per 32-co tile and chunk
   static constexpr int WBB = 2 * TWB;                 // 2 tiles per workgroup
   static constexpr int RSTEP = NTHR / WST;
   static constexpr int NR = 2 * NG * IR;              // (half-group, row) rows of 8-channel pixels
@@ -67,9 +78,9 @@ struct GeomH {
 // DBG (diagnostics only, ERTD_BF16_DBG, 3x3 PRE path; results wrong): bit 0
 // skips the epilogue's stores and residual loads, bit 1 the MFMAs, bit 2 the
 // row DMA, bit 3 the weight DMA
-template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE, int DBG = 0>
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE, int DBG = 0, int SP = 1>
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void conv_bf16_kernel(ConvArgs a) {
-  using G = GeomH<KS, MODE, WO, TPX>;
+  using G = GeomH<KS, MODE, WO, TPX, SP>;
   extern __shared__ __attribute__((aligned(16))) char smemh[];
   char* wim = smemh;                          // [2][WBB]
   char* xim = smemh + 2 * G::WBB;             // [2][XB]
@@ -113,9 +124,9 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
     const int buf = rest / (G::NG * G::IR), rem = rest - buf * (G::NG * G::IR);
     const int g = rem / G::IR, rr = rem - g * G::IR;
     u32x4* px = reinterpret_cast<u32x4*>(xim + buf * G::XB + g * G::GB +
-                                         (rr * G::IP + (side ? G::IP - 1 : 0)) * 32);
-    px[0] = u32x4{0u, 0u, 0u, 0u};
-    px[1] = u32x4{0u, 0u, 0u, 0u};
+                                         (rr * G::IP + (side ? G::IP - 1 : 0)) * G::PB);
+#pragma unroll
+    for (int q = 0; q < 2 * SP; ++q) px[q] = u32x4{0u, 0u, 0u, 0u};
   }
 
   const int col = tid % G::WST;
@@ -152,10 +163,10 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
       const int hg = fr / G::IR, r = fr - hg * G::IR;
       const int iy = row0 + r;
       const bool rowok = iy >= 0 && iy < HST;
-      unsigned w[4];
+      unsigned w[4], wl[4];
 #pragma unroll
       for (int j2 = 0; j2 < 4; ++j2) {
-        unsigned bits[2];
+        unsigned bits[2], lbits[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int j = 2 * j2 + e;
@@ -168,11 +179,14 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
             if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
           }
           bits[e] = ok ? bf16_bits(v) : 0u;
+          if constexpr (SP == 2) lbits[e] = ok ? bf16_lo_bits(v, bits[e]) : 0u;
         }
         w[j2] = bits[0] | (bits[1] << 16);
+        if constexpr (SP == 2) wl[j2] = lbits[0] | (lbits[1] << 16);
       }
-      *reinterpret_cast<u32x4*>(img + (hg >> 1) * G::GB + (r * G::IP + col + 1) * 32 +
-                                (hg & 1) * 16) = u32x4{w[0], w[1], w[2], w[3]};
+      char* px = img + (hg >> 1) * G::GB + (r * G::IP + col + 1) * G::PB + (hg & 1) * 16;
+      *reinterpret_cast<u32x4*>(px) = u32x4{w[0], w[1], w[2], w[3]};
+      if constexpr (SP == 2) *reinterpret_cast<u32x4*>(px + 32) = u32x4{wl[0], wl[1], wl[2], wl[3]};
     }
   };
 
@@ -202,7 +216,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
 
   // PRE: chunk k's rows of the pre-transformed image -> img (LDS-DMA, 16 B per
   // lane, one instruction per 1 KB of a row; a 16-pixel row is half a wave)
-  constexpr int RB = G::WST * 32;                          // bytes per image row
+  constexpr int RB = G::WST * G::PB;                       // bytes per image row
   constexpr int IPR = RB >= 1024 ? RB / 1024 : 1;          // DMA instructions per row
   const int G16 = (Cin + 15) / 16;
   auto dma_rows = [&](int k, char* img) {
@@ -217,7 +231,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
       const char* src = reinterpret_cast<const char*>(a.bimg) +
                         (((size_t)b * G16 + gg) * HST + iy) * RB + part * 1024 + lane * 16;
       const unsigned dst = __builtin_amdgcn_readfirstlane(
-          lds_addr_h(img + g * G::GB + (r * G::IP + 1) * 32 + part * 1024));
+          lds_addr_h(img + g * G::GB + (r * G::IP + 1) * G::PB + part * 1024));
       unsigned keep;
       asm volatile(
           "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
@@ -237,7 +251,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
     if constexpr (KS == 1) { rb = oyl; cb = ox + 1; }
     else if constexpr (MODE == MODE_S2) { rb = 2 * oyl; cb = 2 * ox; }
     else { rb = oyl; cb = ox; }
-    lbase[t] = (rb * G::IP + cb) * 32 + h * 16;
+    lbase[t] = (rb * G::IP + cb) * G::PB + h * 16;
   }
   const int abase = lane * 16;
 
@@ -282,15 +296,29 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
       const int g = s / G::TAPS, tap = s % G::TAPS;
       int off;
       if constexpr (KS == 1) off = g * G::GB;
-      else off = g * G::GB + ((tap / 3) * G::IP + (tap % 3)) * 32;
+      else off = g * G::GB + ((tap / 3) * G::IP + (tap % 3)) * G::PB;
       const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(wb + s * 1024 + abase);
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(wb + G::TWB + s * 1024 + abase);
+      bf16x8 a0l{}, a1l{};
+      if constexpr (SP == 2) {
+        a0l = *reinterpret_cast<const bf16x8*>(wb + (G::SPC + s) * 1024 + abase);
+        a1l = *reinterpret_cast<const bf16x8*>(wb + G::TWB + (G::SPC + s) * 1024 + abase);
+      }
 #pragma unroll
       for (int t = 0; t < TPX; ++t) {
         const bf16x8 bv = *reinterpret_cast<const bf16x8*>(xb + lbase[t] + off);
         if constexpr (DBG & 2) {
           acc[0][t][0] += (float)a0[0] * (float)bv[0];
           acc[1][t][0] += (float)a1[1] * (float)bv[1];
+        } else if constexpr (SP == 2) {
+          // the two cross terms first (small), then hi*hi
+          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(xb + lbase[t] + off + 32);
+          acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0l, bv, acc[0][t], 0, 0, 0);
+          acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1l, bv, acc[1][t], 0, 0, 0);
+          acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl, acc[0][t], 0, 0, 0);
+          acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl, acc[1][t], 0, 0, 0);
+          acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bv, acc[0][t], 0, 0, 0);
+          acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bv, acc[1][t], 0, 0, 0);
         } else {
           acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bv, acc[0][t], 0, 0, 0);
           acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bv, acc[1][t], 0, 0, 0);
@@ -381,7 +409,8 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
 // tile and halo row of every conv workgroup.
 // UPS: nearest x2 upsample folded in (output pixel (y, x) reads source
 // (y/2, x/2)), so an Upsample conv becomes a stride-1 conv on the image.
-template <int ACT, bool UPS = false>
+// SP = 2: split-bf16 records [16 hi][16 lo] (64 B per pixel)
+template <int ACT, bool UPS = false, int SP = 1>
 __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G16, int HW) {
   // UPS: four horizontally adjacent output pixels per thread -- one float2 of
   // the source row per channel plane, four 32-B records stored contiguously
@@ -415,17 +444,18 @@ __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G1
       }
     }
   }
-  u32x4* dst = reinterpret_cast<u32x4*>(static_cast<char*>(a.bimg) + (size_t)i4 * 32 * PX);
+  u32x4* dst = reinterpret_cast<u32x4*>(static_cast<char*>(a.bimg) + (size_t)i4 * 32 * SP * PX);
 #pragma unroll
   for (int k = 0; k < PX; ++k) {
-    unsigned w[8];
+    unsigned w[8], wl[8];
 #pragma unroll
     for (int j2 = 0; j2 < 8; ++j2) {
-      unsigned bits[2];
+      unsigned bits[2], lbits[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int c = g * 16 + 2 * j2 + e;
         bits[e] = 0u;
+        lbits[e] = 0u;
         if (c < Cin) {
           float x = v[2 * j2 + e][k];
           if constexpr (ACT != ACT_NONE) {
@@ -434,12 +464,18 @@ __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G1
             if constexpr (ACT == ACT_GN_SILU) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
           }
           bits[e] = bf16_bits(x);
+          if constexpr (SP == 2) lbits[e] = bf16_lo_bits(x, bits[e]);
         }
       }
       w[j2] = bits[0] | (bits[1] << 16);
+      wl[j2] = lbits[0] | (lbits[1] << 16);
     }
-    dst[2 * k] = u32x4{w[0], w[1], w[2], w[3]};
-    dst[2 * k + 1] = u32x4{w[4], w[5], w[6], w[7]};
+    dst[2 * SP * k] = u32x4{w[0], w[1], w[2], w[3]};
+    dst[2 * SP * k + 1] = u32x4{w[4], w[5], w[6], w[7]};
+    if constexpr (SP == 2) {
+      dst[4 * k + 2] = u32x4{wl[0], wl[1], wl[2], wl[3]};
+      dst[4 * k + 3] = u32x4{wl[4], wl[5], wl[6], wl[7]};
+    }
   }
 }
 
@@ -460,7 +496,7 @@ __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G1
 // instead of two.
 __host__ __device__ constexpr int ga_gcd(int a, int b) { return b == 0 ? a : ga_gcd(b, a % b); }
 
-template <bool SILU, int NREC, int NB>
+template <bool SILU, int NREC, int NB, int SP = 1>
 __global__ __launch_bounds__(1024) void gn_act_bf16_kernel(GnArgs g, void* bimg) {
   constexpr int NCH = NB * 16;
   __shared__ double2 part[8][16];   // [group in set][wave]
@@ -522,15 +558,15 @@ __global__ __launch_bounds__(1024) void gn_act_bf16_kernel(GnArgs g, void* bimg)
     g.out[(size_t)b * C + cg] = make_float2(scale, shift);
   }
   __syncthreads();
-  char* base = static_cast<char*>(bimg) + ((size_t)b * (C / 16) + (size_t)set * NB) * HW * 32;
+  char* base = static_cast<char*>(bimg) + ((size_t)b * (C / 16) + (size_t)set * NB) * HW * 32 * SP;
 #pragma unroll
   for (int blk = 0; blk < NB; ++blk) {
 #pragma unroll
     for (int k = 0; k < NREC; ++k) {
-      unsigned u[8];
+      unsigned u[8], ul[8];
 #pragma unroll
       for (int j2 = 0; j2 < 8; ++j2) {
-        unsigned bits[2];
+        unsigned bits[2], lbits[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int c = blk * 16 + 2 * j2 + e;
@@ -538,12 +574,18 @@ __global__ __launch_bounds__(1024) void gn_act_bf16_kernel(GnArgs g, void* bimg)
           float x = fmaf(v[c][k], t.x, t.y);
           if constexpr (SILU) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
           bits[e] = bf16_bits(x);
+          lbits[e] = SP == 2 ? bf16_lo_bits(x, bits[e]) : 0u;
         }
         u[j2] = bits[0] | (bits[1] << 16);
+        ul[j2] = lbits[0] | (lbits[1] << 16);
       }
-      u32x4* dst = reinterpret_cast<u32x4*>(base + ((size_t)blk * HW + tid + k * nthr) * 32);
+      u32x4* dst = reinterpret_cast<u32x4*>(base + ((size_t)blk * HW + tid + k * nthr) * 32 * SP);
       dst[0] = u32x4{u[0], u[1], u[2], u[3]};
       dst[1] = u32x4{u[4], u[5], u[6], u[7]};
+      if constexpr (SP == 2) {
+        dst[2] = u32x4{ul[0], ul[1], ul[2], ul[3]};
+        dst[3] = u32x4{ul[4], ul[5], ul[6], ul[7]};
+      }
     }
   }
 }
@@ -570,38 +612,40 @@ bool gn_act_bf16_fits(int C, int groups, int HW) {
   return ga_plan(C, groups, HW, &r, &n);
 }
 
-template <bool SILU>
+template <bool SILU, int SP>
 static hipError_t launch_ga(const GnArgs& g, int nrec, int nb, void* bimg, int B, hipStream_t s) {
   const int C = g.Ca + g.Cb;
   dim3 grid((unsigned)(C / (16 * nb)), (unsigned)B);
   const int thr = g.HW / nrec;
-  if (nb == 3) gn_act_bf16_kernel<SILU, 1, 3><<<grid, thr, 0, s>>>(g, bimg);
-  else if (nrec == 1) gn_act_bf16_kernel<SILU, 1, 1><<<grid, thr, 0, s>>>(g, bimg);
-  else if (nrec == 2) gn_act_bf16_kernel<SILU, 2, 1><<<grid, thr, 0, s>>>(g, bimg);
-  else gn_act_bf16_kernel<SILU, 4, 1><<<grid, thr, 0, s>>>(g, bimg);
+  if (nb == 3) gn_act_bf16_kernel<SILU, 1, 3, SP><<<grid, thr, 0, s>>>(g, bimg);
+  else if (nrec == 1) gn_act_bf16_kernel<SILU, 1, 1, SP><<<grid, thr, 0, s>>>(g, bimg);
+  else if (nrec == 2) gn_act_bf16_kernel<SILU, 2, 1, SP><<<grid, thr, 0, s>>>(g, bimg);
+  else gn_act_bf16_kernel<SILU, 4, 1, SP><<<grid, thr, 0, s>>>(g, bimg);
   return hipGetLastError();
 }
 
-hipError_t launch_gn_act_bf16(const GnArgs& g, bool silu, void* bimg, int B, hipStream_t s) {
+hipError_t launch_gn_act_bf16(const GnArgs& g, bool silu, void* bimg, int B, hipStream_t s, bool split) {
   int nrec, nb;
   if (!bimg || !ga_plan(g.Ca + g.Cb, g.groups, g.HW, &nrec, &nb)) return hipErrorInvalidValue;
-  return silu ? launch_ga<true>(g, nrec, nb, bimg, B, s) : launch_ga<false>(g, nrec, nb, bimg, B, s);
+  if (split)
+    return silu ? launch_ga<true, 2>(g, nrec, nb, bimg, B, s) : launch_ga<false, 2>(g, nrec, nb, bimg, B, s);
+  return silu ? launch_ga<true, 1>(g, nrec, nb, bimg, B, s) : launch_ga<false, 1>(g, nrec, nb, bimg, B, s);
 }
 
-size_t conv_bf16_image_bytes(int cin, int B, int H, int W) {
-  return (size_t)B * ((cin + 15) / 16) * H * W * 32;
+size_t conv_bf16_image_bytes(int cin, int B, int H, int W, bool split) {
+  return (size_t)B * ((cin + 15) / 16) * H * W * 32 * (split ? 2 : 1);
 }
 
-template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false, int DBG = 0>
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false, int DBG = 0, int SP = 1>
 static hipError_t launch_hgd(const ConvArgs& a, int B, hipStream_t s) {
-  using G = GeomH<KS, MODE, WO, TPX>;
+  using G = GeomH<KS, MODE, WO, TPX, SP>;
   const size_t lds = G::LDS + 64 * sizeof(float2) + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE, DBG>,
+    (void)hipFuncSetAttribute((const void*)conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE, DBG, SP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((unsigned)(WO * WO / G::BM), (unsigned)((a.Cout + G::BN - 1) / G::BN), (unsigned)B);
-  conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE, DBG><<<grid, NTHR, lds, s>>>(a);
+  conv_bf16_kernel<KS, MODE, ACT, WO, TPX, PRE, DBG, SP><<<grid, NTHR, lds, s>>>(a);
   return hipGetLastError();
 }
 
@@ -617,10 +661,10 @@ static int bf16_dbg() {
 }
 #endif
 
-template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false>
+template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false, int SP = 1>
 static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
 #ifdef ERTD_DIAG
-  if constexpr (KS == 3 && PRE && WO == 64 && TPX == 2) {
+  if constexpr (KS == 3 && PRE && WO == 64 && TPX == 2 && SP == 1) {
     switch (bf16_dbg()) {
       case 1: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 1>(a, B, s);
       case 2: return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 2>(a, B, s);
@@ -633,7 +677,7 @@ static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
     }
   }
 #endif
-  return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 0>(a, B, s);
+  return launch_hgd<KS, MODE, ACT, WO, TPX, PRE, 0, SP>(a, B, s);
 }
 
 // ERTD_UNET_BF16_PRE=0 keeps the register staging for stride-1 convs (diagnostics)
@@ -655,66 +699,73 @@ static int convh_tpx_override() {
   return v;
 }
 
-template <int KS, int TP>
+template <int KS, int TP, int SP>
 static hipError_t launch_pre_w(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
-    case 16: return launch_hg<KS, MODE_S1, ACT_NONE, 16, TP, true>(a, B, s);
-    case 32: return launch_hg<KS, MODE_S1, ACT_NONE, 32, TP, true>(a, B, s);
-    case 64: return launch_hg<KS, MODE_S1, ACT_NONE, 64, TP, true>(a, B, s);
-    case 128: return launch_hg<KS, MODE_S1, ACT_NONE, 128, TP, true>(a, B, s);
+    case 16: return launch_hg<KS, MODE_S1, ACT_NONE, 16, TP, true, SP>(a, B, s);
+    case 32: return launch_hg<KS, MODE_S1, ACT_NONE, 32, TP, true, SP>(a, B, s);
+    case 64: return launch_hg<KS, MODE_S1, ACT_NONE, 64, TP, true, SP>(a, B, s);
+    case 128: return launch_hg<KS, MODE_S1, ACT_NONE, 128, TP, true, SP>(a, B, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 // TPX = 4 (512-pixel tiles, 64 co x 128 px per wave: 6 LDS operand reads per
-// 8 MFMAs instead of 4 per 4) where two workgroups still fit a CU (W = 32, 64)
-template <int KS>
+// 8 MFMAs instead of 4 per 4) where two workgroups still fit a CU (W = 32, 64);
+// split bf16 (twice the LDS) fits one
+template <int KS, int SP>
 static hipError_t launch_pre_w4(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
-    case 32: return launch_hg<KS, MODE_S1, ACT_NONE, 32, 4, true>(a, B, s);
-    case 64: return launch_hg<KS, MODE_S1, ACT_NONE, 64, 4, true>(a, B, s);
-    default: return launch_pre_w<KS, 2>(a, B, s);
+    case 32: return launch_hg<KS, MODE_S1, ACT_NONE, 32, 4, true, SP>(a, B, s);
+    case 64: return launch_hg<KS, MODE_S1, ACT_NONE, 64, 4, true, SP>(a, B, s);
+    default: return launch_pre_w<KS, 2, SP>(a, B, s);
   }
 }
 
-// stride-1 (or upsample) conv through the pre-transformed image: transform,
-// then the conv as stride 1 on the image
-static hipError_t launch_conv_pre(int ks, int mode, int act, const ConvArgs& a, int B,
-                                  hipStream_t s) {
+template <int SP>
+static hipError_t launch_act_img(const ConvArgs& a, int act, bool up, int B, hipStream_t s) {
   const int HW = a.Wo * a.Wo, G16 = (a.Cin + 15) / 16;
   const long long n = (long long)B * G16 * HW;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   const unsigned blocks4 = (unsigned)((n / 4 + 255) / 256);   // the UPS kernel: 4 pixels per thread
-  if (a.bimg_ready) {
-    // image already written by gn_act_bf16_kernel
-  } else if (mode == MODE_UP) act_bf16_kernel<ACT_NONE, true><<<blocks4, 256, 0, s>>>(a, B, G16, HW);
-  else if (act == ACT_GN_SILU) act_bf16_kernel<ACT_GN_SILU><<<blocks, 256, 0, s>>>(a, B, G16, HW);
-  else if (act == ACT_GN) act_bf16_kernel<ACT_GN><<<blocks, 256, 0, s>>>(a, B, G16, HW);
-  else act_bf16_kernel<ACT_NONE><<<blocks, 256, 0, s>>>(a, B, G16, HW);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  ConvArgs c = a;
-  c.Hs = c.Ws = a.Wo;   // the image is at the output resolution
-  if (ks == 1) return launch_pre_w<1, 1>(c, B, s);
-  if (convh_tpx_override() == 1) return launch_pre_w<3, 1>(c, B, s);
-  if (convh_tpx_override() == 2) return launch_pre_w<3, 2>(c, B, s);
-  return launch_pre_w4<3>(c, B, s);   // U3 B=256: 101.5 -> 103.1 steps/s over TPX = 2
+  if (up) act_bf16_kernel<ACT_NONE, true, SP><<<blocks4, 256, 0, s>>>(a, B, G16, HW);
+  else if (act == ACT_GN_SILU) act_bf16_kernel<ACT_GN_SILU, false, SP><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else if (act == ACT_GN) act_bf16_kernel<ACT_GN, false, SP><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  else act_bf16_kernel<ACT_NONE, false, SP><<<blocks, 256, 0, s>>>(a, B, G16, HW);
+  return hipGetLastError();
 }
 
-template <int KS, int MODE, int ACT, int TP>
+// stride-1 (or upsample) conv through the pre-transformed image: transform,
+// then the conv as stride 1 on the image
+template <int SP>
+static hipError_t launch_conv_pre(int ks, int mode, int act, const ConvArgs& a, int B,
+                                  hipStream_t s) {
+  if (!a.bimg_ready) {   // else: image already written by gn_act_bf16_kernel
+    const hipError_t e = launch_act_img<SP>(a, act, mode == MODE_UP, B, s);
+    if (e != hipSuccess) return e;
+  }
+  ConvArgs c = a;
+  c.Hs = c.Ws = a.Wo;   // the image is at the output resolution
+  if (ks == 1) return launch_pre_w<1, 1, SP>(c, B, s);
+  if (convh_tpx_override() == 1) return launch_pre_w<3, 1, SP>(c, B, s);
+  if (convh_tpx_override() == 2) return launch_pre_w<3, 2, SP>(c, B, s);
+  return launch_pre_w4<3, SP>(c, B, s);   // U3 B=256: 101.5 -> 103.1 steps/s over TPX = 2
+}
+
+template <int KS, int MODE, int ACT, int TP, int SP>
 static hipError_t launch_hwt(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
-    case 16: return launch_hg<KS, MODE, ACT, 16, TP>(a, B, s);
-    case 32: return launch_hg<KS, MODE, ACT, 32, TP>(a, B, s);
-    case 64: return launch_hg<KS, MODE, ACT, 64, TP>(a, B, s);
+    case 16: return launch_hg<KS, MODE, ACT, 16, TP, false, SP>(a, B, s);
+    case 32: return launch_hg<KS, MODE, ACT, 32, TP, false, SP>(a, B, s);
+    case 64: return launch_hg<KS, MODE, ACT, 64, TP, false, SP>(a, B, s);
     case 128:
-      if constexpr (MODE != MODE_S2) return launch_hg<KS, MODE, ACT, 128, TP>(a, B, s);
+      if constexpr (MODE != MODE_S2) return launch_hg<KS, MODE, ACT, 128, TP, false, SP>(a, B, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int KS, int MODE, int ACT>
+template <int KS, int MODE, int ACT, int SP>
 static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
   // TPX = 2 (256-pixel tiles) except stride 2 / 1x1 (staging registers)
   if constexpr (KS == 1) {
@@ -723,62 +774,64 @@ static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
       const char* e = getenv("ERTD_UNET_BF16_TPX1");
       return e ? atoi(e) : 1;
     }();
-    if (t1 == 2) return launch_hwt<KS, MODE, ACT, 2>(a, B, s);
-    return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
+    if (t1 == 2) return launch_hwt<KS, MODE, ACT, 2, SP>(a, B, s);
+    return launch_hwt<KS, MODE, ACT, 1, SP>(a, B, s);
   } else if constexpr (MODE == MODE_S2) {
-    return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
+    return launch_hwt<KS, MODE, ACT, 1, SP>(a, B, s);
   } else {
-    if (convh_tpx_override() == 1) return launch_hwt<KS, MODE, ACT, 1>(a, B, s);
-    return launch_hwt<KS, MODE, ACT, 2>(a, B, s);
+    if (convh_tpx_override() == 1) return launch_hwt<KS, MODE, ACT, 1, SP>(a, B, s);
+    return launch_hwt<KS, MODE, ACT, 2, SP>(a, B, s);
   }
 }
 
 // the standalone image transform (act(GN(x)) or the nearest-x2 upsample of x
 // -> the [B][C/16][H][W][16] bf16 image): ertd_act_bf16 (bench per-kernel GB/s)
 hipError_t launch_act_bf16(const ConvArgs& a, int act, bool up, int B, hipStream_t s) {
-  const int HW = a.Wo * a.Wo, G16 = (a.Cin + 15) / 16;
-  const long long n = (long long)B * G16 * HW;
-  const unsigned blocks = (unsigned)((n + 255) / 256);
-  if (up) act_bf16_kernel<ACT_NONE, true><<<(unsigned)((n / 4 + 255) / 256), 256, 0, s>>>(a, B, G16, HW);
-  else if (act == ACT_GN_SILU) act_bf16_kernel<ACT_GN_SILU><<<blocks, 256, 0, s>>>(a, B, G16, HW);
-  else if (act == ACT_GN) act_bf16_kernel<ACT_GN><<<blocks, 256, 0, s>>>(a, B, G16, HW);
-  else act_bf16_kernel<ACT_NONE><<<blocks, 256, 0, s>>>(a, B, G16, HW);
-  return hipGetLastError();
+  return a.split ? launch_act_img<2>(a, act, up, B, s) : launch_act_img<1>(a, act, up, B, s);
+}
+
+template <int SP>
+static hipError_t launch_conv_h(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
+  // the pre-transform pays where the staging VALU is heaviest: 3x3 convs with
+  // a GroupNorm(+SiLU) prologue and the Upsample convs (measured on U3 B=256:
+  // the extra read+write pass costs more than it saves for 1x1 convs)
+  if (a.bimg && convh_pre() == 1 && ks == 3 &&
+      ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
+    return launch_conv_pre<SP>(ks, mode, act, a, B, s);
+  if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_hw<3, MODE_S1, ACT_NONE, SP>(a, B, s);
+  if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_hw<3, MODE_S1, ACT_GN_SILU, SP>(a, B, s);
+  if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_hw<3, MODE_S2, ACT_NONE, SP>(a, B, s);
+  if (ks == 3 && mode == MODE_UP && act == ACT_NONE) return launch_hw<3, MODE_UP, ACT_NONE, SP>(a, B, s);
+  if (ks == 1 && mode == MODE_S1 && act == ACT_NONE) return launch_hw<1, MODE_S1, ACT_NONE, SP>(a, B, s);
+  if (ks == 1 && mode == MODE_S1 && act == ACT_GN) return launch_hw<1, MODE_S1, ACT_GN, SP>(a, B, s);
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;
-  if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)
-    return launch_conv_out(act, a, B, true, s);
-  if (conv_in_ok(a, ks, mode, act)) return launch_conv_in(a, B, true, s);
-  // the pre-transform pays where the staging VALU is heaviest: 3x3 convs with
-  // a GroupNorm(+SiLU) prologue and the Upsample convs (measured on U3 B=256:
-  // the extra read+write pass costs more than it saves for 1x1 convs)
-  if (a.bimg && convh_pre() == 1 && ks == 3 &&
-      ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE)))
-    return launch_conv_pre(ks, mode, act, a, B, s);
-  if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_hw<3, MODE_S1, ACT_NONE>(a, B, s);
-  if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_hw<3, MODE_S1, ACT_GN_SILU>(a, B, s);
-  if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_hw<3, MODE_S2, ACT_NONE>(a, B, s);
-  if (ks == 3 && mode == MODE_UP && act == ACT_NONE) return launch_hw<3, MODE_UP, ACT_NONE>(a, B, s);
-  if (ks == 1 && mode == MODE_S1 && act == ACT_NONE) return launch_hw<1, MODE_S1, ACT_NONE>(a, B, s);
-  if (ks == 1 && mode == MODE_S1 && act == ACT_GN) return launch_hw<1, MODE_S1, ACT_GN>(a, B, s);
-  return hipErrorInvalidValue;
+  // conv_in / conv_out are fp32-VALU kernels: bf16 rounds their operands,
+  // split bf16 reads hi + lo weights and keeps the activation fp32
+  const int pk = a.split ? 2 : 1;
+  if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN) return launch_conv_out(act, a, B, pk, s);
+  if (conv_in_ok(a, ks, mode, act)) return launch_conv_in(a, B, pk, s);
+  return a.split ? launch_conv_h<2>(ks, mode, act, a, B, s) : launch_conv_h<1>(ks, mode, act, a, B, s);
 }
 
 // ---- bf16 weight packing: W (Cout, Cin, ks, ks) fp32 -> [co_tile32][chunk][step][lane][8] bf16
-size_t conv_packed_floats_bf16(int cin, int cout, int ks) {
+// (split: [co_tile32][chunk][hi | lo][step][lane][8])
+size_t conv_packed_floats_bf16(int cin, int cout, int ks, bool split) {
   const int ck = convh_ck(ks);
   const size_t tiles = (size_t)((cout + 127) / 128) * 4;
   const size_t nchunk = (size_t)((cin + ck - 1) / ck);
   const size_t steps = (size_t)ks * ks * (ck / 16);
-  return tiles * nchunk * steps * 64 * 8 / 2;   // 8 bf16 per lane = 4 floats
+  return tiles * nchunk * steps * 64 * 8 / 2 * (split ? 2 : 1);   // 8 bf16 per lane = 4 floats
 }
 
 __global__ void pack_conv_bf16_kernel(const float* __restrict__ w, int cin, int cout, int ks,
-                                      int nchunk, size_t total, unsigned short* __restrict__ dst) {
+                                      int nchunk, int planes, size_t total,
+                                      unsigned short* __restrict__ dst) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // bf16 element
   if (i >= total) return;
   const int ck = convh_ck(ks), taps = ks * ks, spc = taps * (ck / 16);
@@ -787,6 +840,8 @@ __global__ void pack_conv_bf16_kernel(const float* __restrict__ w, int cin, int 
   size_t rest = i >> 9;
   const int s = (int)(rest % spc);
   rest /= spc;
+  const int hl = (int)(rest % planes);
+  rest /= planes;
   const int k = (int)(rest % nchunk);
   const int tile = (int)(rest / nchunk);
   const int g = s / taps, tap = s % taps;
@@ -795,15 +850,21 @@ __global__ void pack_conv_bf16_kernel(const float* __restrict__ w, int cin, int 
   float v = 0.f;
   if (co < cout && ci < cin) v = w[((size_t)co * cin + ci) * taps + tap];
   const uint32_t u = __float_as_uint(v);
-  dst[i] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  const uint32_t hi = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+  if (hl == 0) {
+    dst[i] = (unsigned short)hi;
+  } else {
+    const uint32_t r = __float_as_uint(v - __uint_as_float(hi << 16));
+    dst[i] = (unsigned short)((r + 0x7FFFu + ((r >> 16) & 1u)) >> 16);
+  }
 }
 
 hipError_t launch_pack_conv_bf16(const float* w, int cin, int cout, int ks, float* dst,
-                                 hipStream_t s) {
-  const size_t total = conv_packed_floats_bf16(cin, cout, ks) * 2;
+                                 hipStream_t s, bool split) {
+  const size_t total = conv_packed_floats_bf16(cin, cout, ks, split) * 2;
   const int nchunk = (cin + convh_ck(ks) - 1) / convh_ck(ks);
   pack_conv_bf16_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
-      w, cin, cout, ks, nchunk, total, reinterpret_cast<unsigned short*>(dst));
+      w, cin, cout, ks, nchunk, split ? 2 : 1, total, reinterpret_cast<unsigned short*>(dst));
   return hipGetLastError();
 }
 

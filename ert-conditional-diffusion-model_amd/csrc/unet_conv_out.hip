@@ -32,11 +32,15 @@ __device__ __forceinline__ float packed_w_f32(const float* w, int ci, int tap) {
   return w[((size_t)(ci >> 2) * 9 + (s >> 1)) * 128 + ((ci & 3) >> 1) * 64 + (s & 1)];
 }
 
-// W[0][ci][tap] in the bf16 packing (16-channel chunks, step = tap, k = 8*half + j)
-__device__ __forceinline__ float packed_w_bf16(const float* w, int ci, int tap) {
+// W[0][ci][tap] in the bf16 packing (16-channel chunks, step = tap, k = 8*half + j);
+// split bf16: [chunk][hi | lo][9 steps], the weight is hi + lo
+__device__ __forceinline__ float packed_w_bf16(const float* w, int ci, int tap, bool split) {
   const unsigned short* p = reinterpret_cast<const unsigned short*>(w);
-  const unsigned short v = p[((size_t)(ci >> 4) * 9 + tap) * 512 + ((ci >> 3) & 1) * 256 + (ci & 7)];
-  return __uint_as_float((unsigned)v << 16);
+  const size_t e = ((ci >> 3) & 1) * 256 + (ci & 7);
+  if (!split) return __uint_as_float((unsigned)p[((size_t)(ci >> 4) * 9 + tap) * 512 + e] << 16);
+  const float hi = __uint_as_float((unsigned)p[((size_t)(ci >> 4) * 18 + tap) * 512 + e] << 16);
+  const float lo = __uint_as_float((unsigned)p[((size_t)(ci >> 4) * 18 + 9 + tap) * 512 + e] << 16);
+  return hi + lo;
 }
 
 // Thread = 4 horizontally adjacent output pixels of one row; a workgroup owns
@@ -55,8 +59,9 @@ struct OutGeom {
   static_assert(WO % ROWS == 0 && NT <= 256 && NT % 64 == 0, "whole output rows per workgroup");
 };
 
-template <int ACT, int WO, int RWS, bool BF>
+template <int ACT, int WO, int RWS, int PK>
 __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
+  constexpr bool BF = PK == PK_BF16;   // round the staged input to bf16
   using G = OutGeom<WO, RWS>;
   constexpr int OCC = G::OCC;
   extern __shared__ __attribute__((aligned(16))) float smo[];
@@ -70,7 +75,7 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
 
   for (int i = tid; i < Cin * 9; i += G::NT) {
     const int ci = i / 9, tap = i - ci * 9;
-    wl[i] = BF ? packed_w_bf16(a.wpk, ci, tap) : packed_w_f32(a.wpk, ci, tap);
+    wl[i] = PK == PK_F32 ? packed_w_f32(a.wpk, ci, tap) : packed_w_bf16(a.wpk, ci, tap, PK == PK_SPLIT);
   }
   if constexpr (ACT != ACT_NONE) {
     for (int c = tid; c < Cin; c += G::NT) gtab[c] = a.gn[(size_t)b * Cin + c];
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
   *reinterpret_cast<float4*>(a.out + o) = v;
 }
 
-template <int ACT, int WO, int RWS, bool BF>
+template <int ACT, int WO, int RWS, int BF>
 hipError_t launch_co(const ConvArgs& a, int B, hipStream_t s) {
   using G = OutGeom<WO, RWS>;
   const size_t lds = ((size_t)G::OCC * G::CSZ + (((size_t)a.Cin * 9 + 1) & ~(size_t)1)) * sizeof(float) +
@@ -195,14 +200,14 @@ hipError_t launch_co(const ConvArgs& a, int B, hipStream_t s) {
 // 60.5 us, 4 rows (1024 one-wave workgroups) 70.5 us -- per-workgroup weight
 // gathers and the halo re-reads cost more than the lost occupancy; U3 B=256:
 // 163 us (the one-pixel-per-thread kernel before: 244 us).
-template <int ACT, int WO, bool BF>
+template <int ACT, int WO, int BF>
 hipError_t launch_co_r(const ConvArgs& a, int B, hipStream_t s) {
   constexpr int TPR = WO / 4;
   constexpr int R = (256 / TPR) < WO ? (256 / TPR) : WO;
   return launch_co<ACT, WO, R, BF>(a, B, s);
 }
 
-template <int ACT, bool BF>
+template <int ACT, int BF>
 hipError_t launch_co_w(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
     case 16: return launch_co_r<ACT, 16, BF>(a, B, s);
@@ -226,14 +231,19 @@ hipError_t launch_co_w(const ConvArgs& a, int B, hipStream_t s) {
 __device__ __forceinline__ float packed_w0_f32(const float* w, int co, int tap) {
   return w[((size_t)(co >> 5) * 9 + (tap >> 1)) * 128 + (co & 31) * 2 + (tap & 1)];
 }
-// ... and in the bf16 packing ([tile][chunk][9 steps][lane][8], lane = co & 31 for ci 0..7)
-__device__ __forceinline__ float packed_w0_bf16(const float* w, int co, int tap) {
+// ... and in the bf16 packing ([tile][chunk][9 steps][lane][8], lane = co & 31 for ci 0..7;
+// split: [tile][chunk][hi | lo][9 steps], the weight is hi + lo)
+__device__ __forceinline__ float packed_w0_bf16(const float* w, int co, int tap, bool split) {
   const unsigned short* p = reinterpret_cast<const unsigned short*>(w);
-  return __uint_as_float((unsigned)p[((size_t)(co >> 5) * 9 + tap) * 512 + (co & 31) * 8] << 16);
+  if (!split) return __uint_as_float((unsigned)p[((size_t)(co >> 5) * 9 + tap) * 512 + (co & 31) * 8] << 16);
+  const float hi = __uint_as_float((unsigned)p[((size_t)(co >> 5) * 18 + tap) * 512 + (co & 31) * 8] << 16);
+  const float lo = __uint_as_float((unsigned)p[((size_t)(co >> 5) * 18 + 9 + tap) * 512 + (co & 31) * 8] << 16);
+  return hi + lo;
 }
 
-template <int WO, bool BF>
+template <int WO, int PK>
 __global__ __launch_bounds__(256) void conv_in_kernel(ConvArgs a) {
+  constexpr bool BF = PK == PK_BF16;
   extern __shared__ __attribute__((aligned(16))) float smi[];
   float* wl = smi;                    // [Cout][9]
   float* bl = smi + a.Cout * 9;       // [Cout]
@@ -241,7 +251,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvArgs a) {
   const int Cout = a.Cout;
   for (int i = tid; i < Cout * 9; i += 256) {
     const int co = i / 9, tap = i - co * 9;
-    wl[i] = BF ? packed_w0_bf16(a.wpk, co, tap) : packed_w0_f32(a.wpk, co, tap);
+    wl[i] = PK == PK_F32 ? packed_w0_f32(a.wpk, co, tap) : packed_w0_bf16(a.wpk, co, tap, PK == PK_SPLIT);
   }
   for (int i = tid; i < Cout; i += 256) bl[i] = a.bias ? a.bias[i] : 0.f;
   constexpr int HW = WO * WO;
@@ -269,7 +279,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvArgs a) {
   }
 }
 
-template <int WO, bool BF>
+template <int WO, int BF>
 hipError_t launch_ci(const ConvArgs& a, int B, hipStream_t s) {
   const size_t lds = (size_t)a.Cout * 10 * sizeof(float);
   if (lds > 65536) return hipErrorInvalidValue;
@@ -285,23 +295,41 @@ bool conv_in_ok(const ConvArgs& a, int ks, int mode, int act) {
          (a.Wo == 16 || a.Wo == 32 || a.Wo == 64 || a.Wo == 128) && a.Cout <= 1024;
 }
 
-hipError_t launch_conv_in(const ConvArgs& a, int B, bool bf16, hipStream_t s) {
+template <int PK>
+static hipError_t launch_ci_w(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
-    case 16: return bf16 ? launch_ci<16, true>(a, B, s) : launch_ci<16, false>(a, B, s);
-    case 32: return bf16 ? launch_ci<32, true>(a, B, s) : launch_ci<32, false>(a, B, s);
-    case 64: return bf16 ? launch_ci<64, true>(a, B, s) : launch_ci<64, false>(a, B, s);
-    case 128: return bf16 ? launch_ci<128, true>(a, B, s) : launch_ci<128, false>(a, B, s);
+    case 16: return launch_ci<16, PK>(a, B, s);
+    case 32: return launch_ci<32, PK>(a, B, s);
+    case 64: return launch_ci<64, PK>(a, B, s);
+    case 128: return launch_ci<128, PK>(a, B, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_conv_out(int act, const ConvArgs& a, int B, bool bf16, hipStream_t s) {
+hipError_t launch_conv_in(const ConvArgs& a, int B, int pk, hipStream_t s) {
+  switch (pk) {
+    case PK_F32: return launch_ci_w<PK_F32>(a, B, s);
+    case PK_BF16: return launch_ci_w<PK_BF16>(a, B, s);
+    case PK_SPLIT: return launch_ci_w<PK_SPLIT>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int ACT>
+static hipError_t launch_co_pk(const ConvArgs& a, int B, int pk, hipStream_t s) {
+  switch (pk) {
+    case PK_F32: return launch_co_w<ACT, PK_F32>(a, B, s);
+    case PK_BF16: return launch_co_w<ACT, PK_BF16>(a, B, s);
+    case PK_SPLIT: return launch_co_w<ACT, PK_SPLIT>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_conv_out(int act, const ConvArgs& a, int B, int pk, hipStream_t s) {
   if (a.Cout != 1 || a.Ho != a.Wo || a.Hs != a.Ws || a.Ws != a.Wo || a.Cin != a.Ca + a.Cb)
     return hipErrorInvalidValue;
-  if (act == ACT_GN_SILU) return bf16 ? launch_co_w<ACT_GN_SILU, true>(a, B, s)
-                                      : launch_co_w<ACT_GN_SILU, false>(a, B, s);
-  if (act == ACT_NONE) return bf16 ? launch_co_w<ACT_NONE, true>(a, B, s)
-                                   : launch_co_w<ACT_NONE, false>(a, B, s);
+  if (act == ACT_GN_SILU) return launch_co_pk<ACT_GN_SILU>(a, B, pk, s);
+  if (act == ACT_NONE) return launch_co_pk<ACT_NONE>(a, B, pk, s);
   return hipErrorInvalidValue;
 }
 

@@ -124,12 +124,34 @@ hipError_t launch_gn_partials(const float* x, int C, int HW, int np, float2* out
   return hipGetLastError();
 }
 
+// float64 wave sum in a fixed order, the same bits in every lane: DPP row
+// sums (row16_sum's pairing on both halves of the double), then the four row
+// sums as (r0 + r1) + (r2 + r3) by readlane -- no LDS round trips (a
+// __shfl_xor butterfly on doubles is 12 dependent ds_bpermutes)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
 // One wave per (sample, group): lanes take the group's (channel, part)
 // items k = lane, lane + 64, ... (channel-major, possibly across both tensors
-// of a skip concatenation), float64 sums reduced by a butterfly in a fixed
-// order: mean = sum S / N, then M2 = sum_p [M2_p + n_p (S_p / n_p - mean)^2]
-// (Chan et al.), var = M2 / N (biased, as GroupNorm); {scale, shift} as
-// gn_stats_kernel.
+// of a skip concatenation), float64 sums reduced in a fixed order: mean =
+// sum S / N, then M2 = sum_p [M2_p + n_p (S_p / n_p - mean)^2] (Chan et al.),
+// var = M2 / N (biased, as GroupNorm); {scale, shift} as gn_stats_kernel.
+// Channel-major items of one tensor are contiguous in its (B, C, np) partials.
 __global__ __launch_bounds__(256) void gn_finalize_kernel(GnPartArgs a, int B) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (wv >= B * a.groups) return;
@@ -138,52 +160,50 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnPartArgs a, int B) {
   // items of the group: channels [c0, c0+cpg); channel c has np(c) parts
   const int nA = c0 < a.Ca ? (a.Ca - c0 < cpg ? a.Ca - c0 : cpg) : 0;   // channels in tensor A
   const int itemsA = nA * a.npa, items = itemsA + (cpg - nA) * (a.Cb > 0 ? a.npb : 0);
-  auto item = [&](int k, double& n) -> float2 {
-    if (k < itemsA) {
-      const int c = c0 + k / a.npa, p = k - (k / a.npa) * a.npa;
-      n = (double)(a.HW / a.npa);
-      return a.pa[((size_t)b * a.Ca + c) * a.npa + p];
-    }
-    const int kk = k - itemsA;
-    const int c = c0 + nA + kk / a.npb - a.Ca, p = kk - (kk / a.npb) * a.npb;
-    n = (double)(a.HW / a.npb);
-    return a.pb[((size_t)b * a.Cb + c) * a.npb + p];
+  // 1 / n_p: exact for the U-Net's power-of-two part sizes
+  const double ina = 1.0 / (double)(a.HW / a.npa), inb = a.Cb > 0 ? 1.0 / (double)(a.HW / a.npb) : 0.0;
+  const double na = (double)(a.HW / a.npa), nb = a.Cb > 0 ? (double)(a.HW / a.npb) : 0.0;
+  const float2* pa = a.pa + ((size_t)b * a.Ca + c0) * a.npa;              // item k < itemsA at pa[k]
+  const float2* pb = a.Cb > 0 ? a.pb + ((size_t)b * a.Cb + (c0 + nA - a.Ca)) * a.npb : nullptr;
+  auto item = [&](int k, bool& inB) -> float2 {
+    inB = k >= itemsA;
+    if (!inB) return pa[k];                       // channel-major items are contiguous
+    return pb[k - itemsA];
   };
   // at most 4 items per lane held in registers (groups up to 256 items)
   float2 it[4];
-  double nn[4];
+  bool ib[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = lane + 64 * j;
-    nn[j] = 0.0;
-    it[j] = k < items ? item(k, nn[j]) : make_float2(0.f, 0.f);
+    ib[j] = false;
+    it[j] = k < items ? item(k, ib[j]) : make_float2(0.f, 0.f);
   }
   double S = 0.0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) S += (double)it[j].x;
   for (int k = lane + 256; k < items; k += 64) {   // wider groups (one group over 512 channels)
-    double n;
-    S += (double)item(k, n).x;
+    bool q;
+    S += (double)item(k, q).x;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) S += __shfl_xor(S, o);
+  S = wave_sum_d(S);
   const double N = (double)cpg * a.HW;
   const double mean = S / N;
   double M2 = 0.0;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    if (nn[j] > 0.0) {
-      const double d = (double)it[j].x / nn[j] - mean;
-      M2 += (double)it[j].y + nn[j] * d * d;
+    if (lane + 64 * j < items) {
+      const double n = ib[j] ? nb : na;
+      const double d = (double)it[j].x * (ib[j] ? inb : ina) - mean;
+      M2 += (double)it[j].y + n * d * d;
     }
   for (int k = lane + 256; k < items; k += 64) {
-    double n;
-    const float2 q = item(k, n);
-    const double d = (double)q.x / n - mean;
-    M2 += (double)q.y + n * d * d;
+    bool q;
+    const float2 v = item(k, q);
+    const double d = (double)v.x * (q ? inb : ina) - mean;
+    M2 += (double)v.y + (q ? nb : na) * d * d;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) M2 += __shfl_xor(M2, o);
+  M2 = wave_sum_d(M2);
   double var = M2 / N;
   var = var > 0.0 ? var : 0.0;
   const float rstd = (float)(1.0 / sqrt(var + GN_EPS));

@@ -15,7 +15,7 @@ from .train import DiffusionForwardFn, train_step, validation_loss
 from .ensemble import member_range, sample_ensemble
 from .postproc import compact, postprocess, sample_realisations
 from .unet import ConditionalUNet, UNetSamplerPlan, sample_unet
-from .unet_train import unet_train_backward, unet_train_forward, unet_train_step
+from .unet_train import UNetTrainPlan, unet_train_backward, unet_train_forward, unet_train_step
 from .kde import ensemble_mode, kde_mode, mode_kde_calculation
 
 __all__ = [
@@ -26,5 +26,5 @@ __all__ = [
     "save_checkpoint", "STATE_KEYS", "train_step", "validation_loss", "DiffusionForwardFn",
     "sample_ensemble", "member_range", "postprocess", "sample_realisations", "compact",
     "ConditionalUNet", "UNetSamplerPlan", "sample_unet", "kde_mode", "ensemble_mode",
-    "mode_kde_calculation", "unet_train_step", "unet_train_forward", "unet_train_backward",
+    "mode_kde_calculation", "unet_train_step", "UNetTrainPlan", "unet_train_forward", "unet_train_backward",
 ]

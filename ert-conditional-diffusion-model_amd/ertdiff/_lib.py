@@ -28,7 +28,7 @@ ERTD_ENOGPU = -3
 ERTD_ETIMEOUT = -4
 OP_FORWARD, OP_SAMPLE, OP_TRAIN = 0, 1, 2
 MODE_HOISTED, MODE_FAITHFUL, MODE_FAITHFUL_STEPS = 0, 1, 2
-PREC_FP32, PREC_BF16 = 0, 1
+PREC_FP32, PREC_BF16, PREC_BF16X3 = 0, 1, 2
 HIDDEN = 128
 PMAX = 32
 CIN = 14

@@ -42,7 +42,11 @@ CONFIGS: Dict[str, dict] = {
 }
 
 
-_PRECISIONS = {"fp32": 0, "bf16": 1}
+# "bf16x3": split-bf16 conv operands (hi + lo bf16 planes, 3 bf16 MFMAs per
+# product, fp32 accumulate) -- the bf16 configs' MFMA path at ~2^-16 relative
+# per product, inside the north star's 1e-4 rel-L2
+_PRECISIONS = {"fp32": 0, "bf16": 1, "bf16x3": 2}
+_PRECISION_NAMES = {v: k for k, v in _PRECISIONS.items()}
 
 
 def make_config(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, attn=False,
@@ -184,11 +188,12 @@ class ConditionalUNet(nn.Module):
 
     @property
     def precision(self) -> str:
-        return "bf16" if self.cfg.precision == 1 else "fp32"
+        return _PRECISION_NAMES[self.cfg.precision]
 
     def set_precision(self, precision: str) -> None:
-        """fp32 convs (default) or bf16 conv operands with fp32 accumulation;
-        the packed weights are rebuilt on the next call."""
+        """fp32 convs (default), bf16 conv operands with fp32 accumulation, or
+        "bf16x3" split-bf16 operands; the packed weights are rebuilt on the
+        next call."""
         self.cfg.precision = _PRECISIONS[precision]
         self._packed = None
         self._packed_key = None

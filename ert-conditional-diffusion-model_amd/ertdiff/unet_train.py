@@ -698,6 +698,121 @@ def _adam_state(optimizer, params):
     return lr, b1, b2, eps, ms, vs, int(optimizer.state[params[0]]["step"].item())
 
 
+def _check_batch(model, x0, cond):
+    B = x0.size(0)
+    if x0.dim() != 2 or x0.shape[1] != model.param_dim:
+        raise RuntimeError(f"ertdiff: x0 must be (B, {model.param_dim}), got {tuple(x0.shape)}")
+    if cond.dim() != 3 or cond.shape[0] != B or cond.shape[1] != _lib.CIN:
+        raise RuntimeError(f"ertdiff: condition must be (B, 14, L), got {tuple(cond.shape)}")
+    return B
+
+
+def _default_group(process_group):
+    import torch.distributed as dist
+    if process_group is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.group.WORLD
+    return process_group
+
+
+def _adam_apply(optimizer, params, dev):
+    lr, b1, b2, ep, ms, vs, step = _adam_state(optimizer, params)
+    sizes = _arr([p.numel() for p in params], ctypes.c_longlong)
+    arrs = [_arr([x.data_ptr() for x in ts]) for ts in (params, [p.grad for p in params], ms, vs)]
+    _lib.check(_lib.lib().ertd_adam_multi(*arrs, sizes, len(params), step, lr, b1, b2, ep,
+                                          _lib.stream_of(dev)), "adam_multi")
+
+
+class UNetTrainPlan:
+    """unet_train_step for a fixed (B, L) with the device work captured ONCE
+    as a graph (torch.cuda.CUDAGraph = hipGraph): q_sample -> the forward walk
+    with its tape -> MSE -> the backward walk, ~900 kernel launches (every conv
+    packing included: the weights change every step, so each conv's forward and
+    flipped packings are re-made once per replay, from the parameters in place).
+    A step then costs one graph launch instead of the Python walk's per-launch
+    host overhead; the optional gradient all-reduce and the multi-tensor Adam
+    launch run eagerly after the replay (the Adam step count is host state).
+
+        plan = UNetTrainPlan(model, optimizer, B, L, T, alpha_bar)
+        loss = plan.step(x0, cond)            # == unet_train_step(...), bit for bit
+
+    The graph reads the parameters and writes the gradients by address: keep
+    the model's parameter tensors (Adam updates them in place) and build a new
+    plan after replacing them (load_state_dict copies into them: fine)."""
+
+    def __init__(self, model: ConditionalUNet, optimizer, B: int, L: int, T: int, alpha_bar,
+                 process_group=None, warmup: int = 1):
+        if model.precision != "fp32":
+            raise RuntimeError("ertdiff: the U-Net train step runs fp32 (set_precision('fp32'))")
+        self.model, self.optimizer, self.T = model, optimizer, int(T)
+        self.names = [nm for nm, _ in model.named_parameters()]
+        self.params = [p for _, p in model.named_parameters()]
+        dev = _lib.require_device(alpha_bar, self.params[0])
+        self.dev, self.B, self.L = dev, int(B), int(L)
+        self.group = process_group
+        self.alpha_bar = _lib.f32c(alpha_bar, "alpha_bar")
+        P = model.param_dim
+        self.x0 = torch.zeros(B, P, dtype=torch.float32, device=dev)
+        self.noise = torch.zeros(B, P, dtype=torch.float32, device=dev)
+        self.t = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.cond = torch.zeros(B, _lib.CIN, L, dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            # warm-up on a side stream (torch's capture recipe): lazily created
+            # state (cached frequency tables, per-device kernel attributes) is
+            # made outside the capture
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(max(1, warmup)):
+                    self._body()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize(dev)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                self.loss, self.grads, self._tape = self._body()
+        for nm, p in zip(self.names, self.params):
+            self.grads[nm] = self.grads[nm].view_as(p)
+
+    @torch.no_grad()
+    def _body(self):
+        from .model import q_sample
+        lib = _lib.lib()
+        xn = q_sample(self.x0, self.t, self.noise, self.alpha_bar)
+        eps, tape = unet_train_forward(self.model, xn, self.t, self.cond)
+        loss = torch.empty((), dtype=torch.float32, device=self.dev)
+        deps = torch.empty_like(eps)
+        mws = tape["k"].ws(lib.ertd_mse_loss_ws_bytes())
+        _lib.check(lib.ertd_mse_loss(eps.data_ptr(), self.noise.data_ptr(), eps.numel(), loss.data_ptr(),
+                                     deps.data_ptr(), mws.data_ptr(), mws.numel(), _lib.stream_of(self.dev)),
+                   "mse_loss")
+        grads = unet_train_backward(self.model, tape, deps)
+        return loss, grads, tape
+
+    @torch.no_grad()
+    def step(self, x0, cond, t=None, noise=None, return_tensor: bool = False):
+        """One optimizer step on (x0, cond): same contract as unet_train_step."""
+        B = _check_batch(self.model, x0, cond)
+        if B != self.B or cond.shape[2] != self.L:
+            raise RuntimeError(f"ertdiff: this plan was captured for B={self.B}, L={self.L}")
+        if t is None:
+            t = torch.randint(0, self.T, (B,), device=self.dev).long()
+        if noise is None:
+            noise = torch.randn_like(x0)
+        with torch.cuda.device(self.dev):
+            self.x0.copy_(x0)
+            self.cond.copy_(cond)
+            self.t.copy_(t)
+            self.noise.copy_(noise)
+            self.graph.replay()
+            for nm, p in zip(self.names, self.params):
+                p.grad = self.grads[nm]
+            group = _default_group(self.group)
+            if group is not None:
+                allreduce_mean([p.grad for p in self.params], group, _DeviceBucketOps(self._tape["k"]))
+            _adam_apply(self.optimizer, self.params, self.dev)
+        self.model._packed_key = None
+        return self.loss.clone() if return_tensor else self.loss.item()
+
+
 @torch.no_grad()
 def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *, t=None,
                     noise=None, return_tensor: bool = False, process_group=None):
@@ -717,11 +832,7 @@ def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *
     names = [nm for nm, _ in model.named_parameters()]
     params = [p for _, p in model.named_parameters()]
     dev = _lib.require_device(x0, cond, alpha_bar, params[0])
-    B = x0.size(0)
-    if x0.dim() != 2 or x0.shape[1] != model.param_dim:
-        raise RuntimeError(f"ertdiff: x0 must be (B, {model.param_dim}), got {tuple(x0.shape)}")
-    if cond.dim() != 3 or cond.shape[0] != B or cond.shape[1] != _lib.CIN:
-        raise RuntimeError(f"ertdiff: condition must be (B, 14, L), got {tuple(cond.shape)}")
+    B = _check_batch(model, x0, cond)
     if t is None:
         t = torch.randint(0, T, (B,), device=dev).long()
     if noise is None:
@@ -743,16 +854,9 @@ def unet_train_step(model: ConditionalUNet, optimizer, x0, cond, T, alpha_bar, *
         grads = unet_train_backward(model, tape, deps)
         for nm, p in zip(names, params):
             p.grad = grads[nm].view_as(p)
-        import torch.distributed as dist
-        group = process_group
-        if group is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            group = dist.group.WORLD
+        group = _default_group(process_group)
         if group is not None:
             allreduce_mean([p.grad for p in params], group, _DeviceBucketOps(tape["k"]))
-        lr, b1, b2, ep, ms, vs, step = _adam_state(optimizer, params)
-        sizes = _arr([p.numel() for p in params], ctypes.c_longlong)
-        arrs = [_arr([x.data_ptr() for x in ts]) for ts in (params, [p.grad for p in params], ms, vs)]
-        _lib.check(lib.ertd_adam_multi(*arrs, sizes, len(params), step, lr, b1, b2, ep,
-                                       _lib.stream_of(dev)), "adam_multi")
+        _adam_apply(optimizer, params, dev)
     model._packed_key = None      # parameters changed in place behind autograd's back: re-pack
     return loss if return_tensor else loss.item()

@@ -77,6 +77,10 @@ typedef struct ertd_weights {
 /* Encoder operand precision. */
 #define ERTD_PREC_FP32 0
 #define ERTD_PREC_BF16 1 /* bf16 conv operands, fp32 accumulate/state */
+/* U-Net only: split-bf16 conv operands -- x = hi + lo (two bf16 RNE planes),
+   products lo*hi + hi*lo + hi*hi on the bf16 MFMA, fp32 accumulate/state
+   (about 2^-16 relative per product: within the north star's 1e-4) */
+#define ERTD_PREC_BF16X3 2
 
 int ertd_version(void);
 const char* ertd_error_string(int code);
@@ -234,8 +238,9 @@ typedef struct ertd_unet_config {
   int num_res;     /* ResBlocks per level on the way down (num_res+1 up)    */
   int attn;        /* 1: mid-block attention (needs 16x16 and C % 256 == 0) */
   int groups;      /* GroupNorm groups (32)                                 */
-  int precision;   /* ERTD_PREC_FP32 (fp32 MFMA convs) or ERTD_PREC_BF16
-                      (bf16 conv operands, fp32 accumulate/activations)    */
+  int precision;   /* ERTD_PREC_FP32 (fp32 MFMA convs), ERTD_PREC_BF16
+                      (bf16 conv operands, fp32 accumulate/activations) or
+                      ERTD_PREC_BF16X3 (split-bf16 conv operands)          */
 } ertd_unet_config;
 
 /* Single U-Net operators (the SURVEY 8a' operator rows; used by per-operator
@@ -244,7 +249,7 @@ typedef struct ertd_unet_config {
  *   + bias (+ ebias[b][co], row stride eb_stride) (+ res), ks 1|3, mode
  *   0 stride 1 / 1 stride 2 (Downsample) / 2 nearest-x2 upsample then conv;
  *   act 0 none / 1 GroupNorm+SiLU / 2 GroupNorm, gn = (B, Cin) float2
- *   {scale, shift} from ertd_group_norm_stats; precision FP32 | BF16;
+ *   {scale, shift} from ertd_group_norm_stats; precision FP32 | BF16 | BF16X3;
  *   H in {16,32,64,128} (Ho likewise); ws >= ertd_conv2d_workspace_bytes(Cin,
  *   Cout, ks, precision, B, H, mode): the packed weights plus the launch's
  *   scratch (a Winograd K split's partial sums, the bf16 pre-transformed

@@ -107,16 +107,17 @@ SAMPLER_TOL = 1e-4
 BF16_SAMPLER_TOL = {"bf16_spec": 1e-3, "fp32_spec": 3e-3}
 
 
-def _run_golden_chain(kat, key, dev):
+def _run_golden_chain(kat, key, dev, precision=None):
     """Replays the golden case on the GPU as consecutive plan segments ending at
-    each recorded step count; returns {count: x}."""
-    name = {"u2": "U2", "u3": "U3"}[key[:2]]
+    each recorded step count; returns {count: x}.  precision: the model's (default:
+    the case's spec precision)."""
+    name = {"u2": "U2", "u3": "U3", "u5": "U5"}[key[:2]]
     meta = [int(v) for v in kat[f"{key}_meta"]]
     wseed, B, L, cseed, nseed, bf16 = meta[:6]
     aff = meta[6] if len(meta) > 6 else 0
     T = int(kat["T"])
     W = U.init_weights(U.CONFIGS[name], wseed, affine="random" if aff else "ones")
-    m = _model_from_spec(name, W, dev, precision="bf16" if bf16 else "fp32")
+    m = _model_from_spec(name, W, dev, precision=precision or ("bf16" if bf16 else "fp32"))
     P = m.param_dim
     cond = torch.from_numpy(synth_uniform((B, 14, L), cseed)).to(dev)
     noise = torch.from_numpy(synth_normal((T, B, P), nseed)).to(dev)
@@ -159,6 +160,40 @@ def test_unet_u3_bf16_sampler_full_chain_vs_golden(unet_sampler_kat, cuda_dev):
         assert e32 < BF16_SAMPLER_TOL["fp32_spec"], (k, e32)
 
 
+# split-bf16 operands (precision "bf16x3": hi + lo bf16 planes, three bf16
+# MFMAs per product, fp32 accumulate) at the north star's output tolerance:
+# the bf16 configs' networks over full T = 1000 chains against the FP32 spec.
+BF16X3_SAMPLER_TOL = 1e-4
+
+
+@pytest.mark.parametrize("key", ["u3_fp32", "u3_fp32_aff", "u5_fp32_aff"])
+def test_unet_bf16x3_sampler_full_chain_vs_fp32_golden(key, unet_sampler_kat, cuda_dev):
+    """configs[2] (U3) / configs[4] (U5) networks at split-bf16 operands over a
+    full T = 1000 chain: <= 1e-4 rel-L2 vs the fp32 spec at every recorded step."""
+    xs = _run_golden_chain(unet_sampler_kat, key, cuda_dev, precision="bf16x3")
+    for k, x in xs.items():
+        err = RN.rel_l2(x, unet_sampler_kat[f"{key}_x{k}"].astype(np.float64))
+        record_error(f"unet_sampler_{key}_bf16x3_vs_fp32spec_step{k}", err)
+        assert err < BF16X3_SAMPLER_TOL, (k, err)
+
+
+def test_unet_u5_sampler_full_chain_vs_golden(unet_sampler_kat, cuda_dev):
+    """configs[4]'s network (U5: 128x128, 4 levels, ch 128, mid attention; random
+    GN affine) over a full T = 1000 chain: fp32 <= 1e-4 vs the fp32 spec; plain
+    bf16 operands within the bf16 budget of the same spec."""
+    key = "u5_fp32_aff"
+    xs = _run_golden_chain(unet_sampler_kat, key, cuda_dev)
+    for k, x in xs.items():
+        err = RN.rel_l2(x, unet_sampler_kat[f"{key}_x{k}"].astype(np.float64))
+        record_error(f"unet_sampler_U5_fp32_step{k}", err)
+        assert err < SAMPLER_TOL, (k, err)
+    xs = _run_golden_chain(unet_sampler_kat, key, cuda_dev, precision="bf16")
+    for k, x in xs.items():
+        err = RN.rel_l2(x, unet_sampler_kat[f"{key}_x{k}"].astype(np.float64))
+        record_error(f"unet_sampler_U5_bf16_vs_fp32spec_step{k}", err)
+        assert err < BF16_SAMPLER_TOL["fp32_spec"], (k, err)
+
+
 def test_unet_u3_fp32_sampler_full_chain_vs_golden(unet_sampler_kat, cuda_dev):
     """U3 (mid attention) at fp32 over the same chain: <= 1e-4."""
     kat = unet_sampler_kat
@@ -197,7 +232,8 @@ def test_unet_sampler_vs_oracle(cuda_dev):
 
 @pytest.mark.parametrize("name,precision,T", [("U1", "fp32", 6), ("U2", "fp32", 3),
                                               ("U3", "bf16", 3), ("U5", "fp32", 2),
-                                              ("U5", "bf16", 2)])
+                                              ("U5", "bf16", 2), ("U3", "bf16x3", 3),
+                                              ("U5", "bf16x3", 2)])
 def test_unet_plan_matches_direct_and_deterministic(name, precision, T, cuda_dev):
     """The captured step graph (skip convs on a forked branch, fused bf16 GN
     prologue) equals the eagerly launched sampler bit for bit."""
@@ -292,3 +328,23 @@ def test_unet_bf16_forward(name, B, L, ts, cuda_dev):
     # measured 4.6e-3..6.0e-3 vs the bf16 spec, 6.4e-3..8.5e-3 vs fp32 (U1/U3/U5)
     assert e16 < 1.2e-2, e16
     assert e32 < 1.6e-2, e32
+
+
+@pytest.mark.parametrize("name,B,L,ts", [("U1", 3, 129, [0, 17, 999]), ("U3", 2, 257, [999, 5]),
+                                         ("U5", 1, 129, [321])])
+def test_unet_bf16x3_forward(name, B, L, ts, cuda_dev):
+    """Split-bf16 conv operands (hi + lo planes, three bf16 MFMAs per product,
+    fp32 accumulate), random GN affine: against the FP32 spec <= 1e-4 rel-L2
+    (the north star's output tolerance; plain bf16 sits at ~7e-3)."""
+    cfg = U.CONFIGS[name]
+    W = U.init_weights(cfg, 13, affine="random")
+    m = _model_from_spec(name, W, cuda_dev, precision="bf16x3")
+    x = torch.from_numpy(synth_normal((B, cfg.param_dim), 113))
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 114))
+    t = torch.tensor(ts)
+    with torch.no_grad():
+        out = m(x.to(cuda_dev), t.to(cuda_dev), cond.to(cuda_dev)).cpu().double().numpy()
+        ref32 = U.forward(x, t, cond, W, cfg).double().numpy()
+    e32 = RN.rel_l2(out, ref32)
+    record_error(f"unet_forward_{name}_bf16x3_vs_fp32spec", e32)
+    assert e32 < 1e-4, e32

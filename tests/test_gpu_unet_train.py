@@ -123,6 +123,41 @@ def test_unet_train_step_deterministic_and_learns(cuda_dev):
     assert _rel(a, ref) < 1e-5
 
 
+@pytest.mark.parametrize("name,B,L", [("U1", 4, 257), ("U3", 2, 129)])
+def test_unet_train_plan_matches_eager_steps(name, B, L, cuda_dev):
+    """UNetTrainPlan (the train step captured once as a graph, Adam eager) ==
+    unet_train_step bit for bit over 4 optimizer steps with fresh batches:
+    losses, parameters, Adam moments."""
+    from ertdiff.unet_train import UNetTrainPlan
+    T = 1000
+    cfg = U.CONFIGS[name]
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    g = torch.Generator(device=cuda_dev).manual_seed(21)
+    data = [(torch.randn(B, cfg.param_dim, device=cuda_dev, generator=g),
+             torch.rand(B, 14, L, device=cuda_dev, generator=g),
+             torch.randint(0, T, (B,), device=cuda_dev, generator=g),
+             torch.randn(B, cfg.param_dim, device=cuda_dev, generator=g)) for _ in range(4)]
+    runs = []
+    for graph in (False, True):
+        m = ertdiff.ConditionalUNet.from_config(name, seed=8).to(cuda_dev)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        plan = UNetTrainPlan(m, opt, B, L, T, ab) if graph else None
+        losses = []
+        for x0, cond, t, n in data:
+            if graph:
+                losses.append(plan.step(x0, cond, t=t, noise=n))
+            else:
+                losses.append(unet_train_step(m, opt, x0, cond, T, ab, t=t, noise=n))
+        st = opt.state_dict()["state"]
+        runs.append((losses, [p.detach().clone() for p in m.parameters()],
+                     [st[i]["exp_avg_sq"].clone() for i in range(len(st))]))
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(runs[0][1], runs[1][1]))
+    assert all(torch.equal(a, b) for a, b in zip(runs[0][2], runs[1][2]))
+    with pytest.raises(RuntimeError):
+        plan.step(data[0][0][:1], data[0][1][:1])
+
+
 def test_unet_train_rejects_bf16(cuda_dev):
     m = ertdiff.ConditionalUNet.from_config("U1", seed=0, precision="bf16").to(cuda_dev)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
