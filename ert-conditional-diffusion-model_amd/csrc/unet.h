@@ -137,6 +137,8 @@ hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, 
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s,
                             bool flipT = false);
+// every packing of a prepared ertd_pack_desc table (device copy) in one launch (unet_pack.hip)
+hipError_t launch_pack_batch(const ertd_pack_desc* d, int n, int blocks, hipStream_t s);
 // fp32 Upsample conv weights: 4 parity classes of combined 2x2 taps
 size_t conv_packed_floats_up(int cin, int cout);
 hipError_t launch_pack_conv_up(const float* w, int cin, int cout, float* dst, hipStream_t s);

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "unet.h"
+#include "unet_pack.h"
 
 using namespace ertd;
 using namespace ertd::unet;
@@ -824,11 +825,24 @@ size_t ertd_conv_input_grad_ws_bytes(int Cin, int Cout, int B, int H, int ks, in
   return n * sizeof(float);
 }
 
-int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout, int Cin, int ks,
-                         int mode, float* dx, int accumulate, void* ws, size_t ws_bytes,
-                         void* stream) {
+}  // extern "C"
+
+namespace {
+// the gradient conv's packing: Winograd F(4x4) / F(2x2) where eligible, else direct,
+// at the head of ws (flipped, transposed)
+int input_grad_kind(int Cin, int Cout, int B, int H, int ks, int mode) {
+  const int Hg = mode == MODE_UP ? 2 * H : H;
+  if (ks == 3 && Cin > 1 && conv_packed_floats_wino4(Cout, Cin) > 0 && wino4_ok(Cout, Cout, Cin, Hg, B))
+    return ERTD_PACK_WINO4;
+  if (ks == 3 && Cin > 1 && conv_packed_floats_wino(Cout, Cin) > 0 && conv_wino_ok(Cout, Cout, Cin, Hg))
+    return ERTD_PACK_WINO;
+  return ERTD_PACK_DIRECT;
+}
+
+int input_grad_impl(const float* dy, int B, int H, const float* w, int Cout, int Cin, int ks, int mode,
+                    float* dx, int accumulate, void* ws, size_t ws_bytes, void* stream, bool pack) {
   const size_t need = ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, ks, mode);
-  if (!dy || !w || !dx || !ws || need == 0) return ERTD_EINVAL;
+  if (!dy || (pack && !w) || !dx || !ws || need == 0) return ERTD_EINVAL;
   if (need > ws_bytes) return ERTD_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
   float* pk = (float*)ws;
@@ -847,13 +861,13 @@ int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout
   a.srcA = src; a.Ca = Cout; a.Cb = 0;
   a.Cin = Cout; a.Cout = Cin;
   a.Hs = a.Ws = a.Ho = a.Wo = Hg;
-  const bool wino4 = ks == 3 && Cin > 1 && conv_packed_floats_wino4(Cout, Cin) > 0 &&
-                     wino4_ok(Cout, Cout, Cin, Hg, B);
-  const bool wino = wino4 || (ks == 3 && Cin > 1 && conv_packed_floats_wino(Cout, Cin) > 0 &&
-                              conv_wino_ok(Cout, Cout, Cin, Hg));
-  hipError_t e = wino4 ? launch_pack_conv_wino4(w, Cout, Cin, pk, s, true)
-                 : wino ? launch_pack_conv_wino(w, Cout, Cin, pk, s, true)
-                        : launch_pack_conv(w, Cout, Cin, ks, pk, s, true);
+  const int kind = input_grad_kind(Cin, Cout, B, H, ks, mode);
+  const bool wino4 = kind == ERTD_PACK_WINO4, wino = wino4 || kind == ERTD_PACK_WINO;
+  hipError_t e = hipSuccess;
+  if (pack)
+    e = wino4 ? launch_pack_conv_wino4(w, Cout, Cin, pk, s, true)
+        : wino ? launch_pack_conv_wino(w, Cout, Cin, pk, s, true)
+               : launch_pack_conv(w, Cout, Cin, ks, pk, s, true);
   if (e != hipSuccess) return (int)e;
   if (wino4) a.wpk_wino4 = pk; else if (wino) a.wpk_wino = pk; else a.wpk = pk;
   if (wino && wino_ksplit_wanted(Cout, Cin, Hg, B)) {
@@ -868,6 +882,93 @@ int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout
   if ((e = launch_conv(ks, MODE_S1, ACT_NONE, a, B, s)) != hipSuccess) return rcode(e);
   if (mode == MODE_UP) return rcode(launch_sum_pool2(scratch, B, Cin, H, dx, accumulate, s));
   return ERTD_OK;
+}
+
+void fill_desc(ertd_pack_desc* d, const float* w, float* dst, int cin, int cout, int ks, int kind, int flip) {
+  *d = ertd_pack_desc{};
+  d->w = w; d->dst = dst; d->cin = cin; d->cout = cout; d->ks = ks; d->kind = kind; d->flip = flip;
+  switch (kind) {
+    case ERTD_PACK_DIRECT:
+      d->total = (long long)conv_packed_floats(cin, cout, ks);
+      d->nchunk = (cin + conv_ck(ks) - 1) / conv_ck(ks);
+      break;
+    case ERTD_PACK_UP:
+      d->total = (long long)conv_packed_floats_up(cin, cout);
+      d->nchunk = (cin + conv_ck(2) - 1) / conv_ck(2);
+      break;
+    case ERTD_PACK_WINO:
+      d->total = (long long)conv_packed_floats_wino(cin, cout);
+      d->nchunk = cin / WINO_KC;
+      break;
+    default:
+      d->total = (long long)conv_packed_floats_wino4(cin, cout);
+      d->nchunk = cin / WINO4_KC;
+      break;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout, int Cin, int ks,
+                         int mode, float* dx, int accumulate, void* ws, size_t ws_bytes,
+                         void* stream) {
+  return input_grad_impl(dy, B, H, w, Cout, Cin, ks, mode, dx, accumulate, ws, ws_bytes, stream, true);
+}
+
+int ertd_conv_input_grad_run(const float* dy, int B, int H, int Cout, int Cin, int ks, int mode,
+                             float* dx, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return input_grad_impl(dy, B, H, nullptr, Cout, Cin, ks, mode, dx, accumulate, ws, ws_bytes, stream,
+                         false);
+}
+
+int ertd_conv_input_grad_pack_desc(int Cin, int Cout, int B, int H, int ks, int mode, const float* w,
+                                   void* ws, ertd_pack_desc* out) {
+  if (!w || !ws || !out || ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, ks, mode) == 0)
+    return ERTD_EINVAL;
+  fill_desc(out, w, (float*)ws, Cout, Cin, ks, input_grad_kind(Cin, Cout, B, H, ks, mode), 1);
+  return ERTD_OK;
+}
+
+// the packing ertd_conv2d_run on this ws reads (fp32; the dispatch of conv2d_impl)
+int ertd_conv2d_pack_desc(int Cin, int Ca, int Cout, int ks, int mode, int precision, int B, int H,
+                          const float* w, void* ws, ertd_pack_desc* out) {
+  if (!w || !ws || !out || precision != ERTD_PREC_FP32 || Ca < 1 || Ca > Cin ||
+      !conv2d_geom_ok(Cin, Cout, ks, precision, B, H, mode))
+    return ERTD_EINVAL;
+  const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  float* pk = (float*)ws;
+  const bool wino4 = ks == 3 && mode == MODE_S1 && Cout > 1 && conv_packed_floats_wino4(Cin, Cout) > 0 &&
+                     wino4_ok(Cin, Ca, Cout, Ho, B);
+  const bool wino = wino4 || (ks == 3 && mode == MODE_S1 && Cout > 1 && conv_packed_floats_wino(Cin, Cout) > 0 &&
+                              conv_wino_ok(Cin, Ca, Cout, Ho));
+  if (wino) {
+    float* pw = pk + a64(std::max(conv_packed_floats(Cin, Cout, ks), conv_packed_floats_up(Cin, Cout)));
+    fill_desc(out, w, pw, Cin, Cout, ks, wino4 ? ERTD_PACK_WINO4 : ERTD_PACK_WINO, 0);
+  } else if (ks == 3 && mode == MODE_UP) {
+    fill_desc(out, w, pk, Cin, Cout, ks, ERTD_PACK_UP, 0);
+  } else {
+    fill_desc(out, w, pk, Cin, Cout, ks, ERTD_PACK_DIRECT, 0);
+  }
+  return ERTD_OK;
+}
+
+int ertd_conv_pack_batch_prepare(ertd_pack_desc* d, int n) {
+  if (!d || n < 1) return ERTD_EINVAL;
+  long long blocks = 0;
+  for (int k = 0; k < n; ++k) {
+    if (!d[k].w || !d[k].dst || d[k].total < 1 || d[k].kind < ERTD_PACK_DIRECT || d[k].kind > ERTD_PACK_WINO4)
+      return ERTD_EINVAL;
+    d[k].block0 = (int)blocks;
+    blocks += (pack_work_items(d[k].kind, d[k].total) + 255) / 256;
+    if (blocks > (1LL << 30)) return ERTD_EINVAL;
+  }
+  return (int)blocks;
+}
+
+int ertd_conv_pack_batch(const ertd_pack_desc* descs, int n, int blocks, void* stream) {
+  if (!descs || n < 1 || blocks < 1) return ERTD_EINVAL;
+  return rcode(launch_pack_batch(descs, n, blocks, (hipStream_t)stream));
 }
 
 int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B, int HW,

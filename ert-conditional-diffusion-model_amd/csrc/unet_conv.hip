@@ -44,6 +44,7 @@
 #include <type_traits>
 
 #include "unet.h"
+#include "unet_pack.h"
 
 namespace ertd {
 namespace unet {
@@ -63,8 +64,7 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-// channels per K-chunk: 4 for 3x3 (36-deep K per chunk), 32 for 1x1 (32-deep)
-__host__ __device__ constexpr int conv_ck(int ks) { return ks == 3 ? 4 : (ks == 2 ? 8 : 32); }
+// channels per K-chunk: conv_ck (unet_pack.h) -- 4 for 3x3 (36-deep K per chunk), 32 for 1x1
 
 template <int KS, int MODE, int WCO, int WO, int TPX>
 struct ConvGeom {
@@ -553,28 +553,7 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, int cin, int cout,
                                  int nchunk, size_t total, float* __restrict__ dst, bool flipT) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int ck = conv_ck(ks), ch = ck / 2;
-  const int spc = ks == 3 ? 9 * ch : ch;
-  const int e = (int)(i & 1);
-  const int lane = (int)((i >> 1) & 63);
-  size_t rest = i >> 7;
-  const int sp = (int)(rest % (spc / 2));
-  rest /= (spc / 2);
-  const int k = (int)(rest % nchunk);
-  const int tile = (int)(rest / nchunk);
-  const int s = 2 * sp + e;
-  const int hh = lane >> 5;
-  const int co = tile * 32 + (lane & 31);
-  int ci, ky, kx;
-  if (ks == 3) { ci = k * ck + hh * ch + s / 9; ky = (s % 9) / 3; kx = s % 3; }
-  else { ci = k * ck + hh * ch + s; ky = 0; kx = 0; }
-  float v = 0.f;
-  // flipT: w is the forward conv's (cin, cout, ks, ks) weight and this packs the
-  // input-gradient conv's W'[co][ci] = W[ci][co] spatially flipped
-  if (co < cout && ci < cin)
-    v = flipT ? w[(((size_t)ci * cout + co) * ks + (ks - 1 - ky)) * ks + (ks - 1 - kx)]
-              : w[(((size_t)co * cin + ci) * ks + ky) * ks + kx];
-  dst[i] = v;
+  dst[i] = pack_conv_elem(w, cin, cout, ks, nchunk, i, flipT);
 }
 
 // Upsample conv: W (Cout, Cin, 3, 3) -> 4 classes (pa, pb) of 2x2 taps in the
@@ -587,32 +566,7 @@ __global__ void pack_conv_up_kernel(const float* __restrict__ w, int cin, int co
                                     size_t per_class, float* __restrict__ dst) {
   const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= 4 * per_class) return;
-  const int cls = (int)(gi / per_class);
-  const size_t i = gi - (size_t)cls * per_class;
-  const int pa = cls >> 1, pb = cls & 1;
-  constexpr int ck = conv_ck(2), ch = ck / 2, spc = 4 * ch;
-  const int e = (int)(i & 1);
-  const int lane = (int)((i >> 1) & 63);
-  size_t rest = i >> 7;
-  const int sp = (int)(rest % (spc / 2));
-  rest /= (spc / 2);
-  const int k = (int)(rest % nchunk);
-  const int tile = (int)(rest / nchunk);
-  const int st = 2 * sp + e;
-  const int co = tile * 32 + (lane & 31);
-  const int ci = k * ck + (lane >> 5) * ch + st / 4;
-  const int ty = (st % 4) / 2, tx = st % 2;
-  float v = 0.f;
-  if (co < cout && ci < cin) {
-    const float* wk = w + ((size_t)co * cin + ci) * 9;
-    const int y0 = (pa == 0) ? (ty == 0 ? 0 : 1) : (ty == 0 ? 0 : 2);
-    const int y1 = (pa == 0) ? (ty == 0 ? 0 : 2) : (ty == 0 ? 1 : 2);
-    const int x0 = (pb == 0) ? (tx == 0 ? 0 : 1) : (tx == 0 ? 0 : 2);
-    const int x1 = (pb == 0) ? (tx == 0 ? 0 : 2) : (tx == 0 ? 1 : 2);
-    for (int ky = y0; ky <= y1; ++ky)
-      for (int kx = x0; kx <= x1; ++kx) v += wk[ky * 3 + kx];
-  }
-  dst[gi] = v;
+  dst[gi] = pack_conv_up_elem(w, cin, cout, nchunk, per_class, gi);
 }
 
 hipError_t launch_pack_conv_up(const float* w, int cin, int cout, float* dst, hipStream_t s) {

@@ -47,6 +47,7 @@
 #include <cstdlib>
 
 #include "unet.h"
+#include "unet_pack.h"
 
 namespace ertd {
 namespace unet {
@@ -611,35 +612,12 @@ hipError_t launch_act(const ConvArgs& a, int B, hipStream_t s) {
 // (computed in float64, rounded once): the A-operand fragments of
 // v_mfma_f32_16x16x4_f32 for co block cb (16 co), both k-steps st in one
 // float2, lane l = 16 kk + c16 -> co = 16 cb + c16, channel 2 kk + st of the chunk
+// one thread per (co, ci): all 16 xi (pack_wino_tile)
 __global__ void pack_wino_kernel(const float* __restrict__ w, int cin, int cout, int nchunk,
-                                 size_t total, float* __restrict__ dst, bool flipT) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int st = (int)(i & 1);
-  const int c16 = (int)((i >> 1) & 15);
-  const int kk = (int)((i >> 5) & 3);
-  const int cb = (int)((i >> 7) & 3);
-  size_t rest = i >> 9;
-  const int xi = (int)(rest % 16);
-  rest /= 16;
-  const int k = (int)(rest % nchunk);
-  const int cog = (int)(rest / nchunk);
-  const int co = cog * 64 + cb * 16 + c16;
-  const int ci = k * WKC + 2 * kk + st;
-  const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
-  const int ri = xi >> 2, rj = xi & 3;
-  // flipT: w is the forward conv's (cin, cout, 3, 3) weight; pack the input-
-  // gradient conv's W'[co][ci] = W[ci][co] spatially flipped
-  const float* g = flipT ? w + ((size_t)ci * cout + co) * 9 : w + ((size_t)co * cin + ci) * 9;
-  double u = 0.0;
-#pragma unroll
-  for (int y = 0; y < 3; ++y) {
-    double row = 0.0;
-#pragma unroll
-    for (int x = 0; x < 3; ++x) row += (double)(flipT ? g[8 - (y * 3 + x)] : g[y * 3 + x]) * G[rj][x];
-    u += G[ri][y] * row;
-  }
-  dst[i] = (float)u;
+                                 size_t items, float* __restrict__ dst, bool flipT) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= items) return;
+  pack_wino_tile(w, cin, cout, nchunk, j, flipT, dst);
 }
 
 }  // namespace
@@ -699,7 +677,8 @@ hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, 
                                  bool flipT) {
   const size_t total = conv_packed_floats_wino(cin, cout);
   if (!total) return hipErrorInvalidValue;
-  pack_wino_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(w, cin, cout, cin / WKC, total, dst,
+  const size_t items = total / 16;
+  pack_wino_kernel<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(w, cin, cout, cin / WKC, items, dst,
                                                                     flipT);
   return hipGetLastError();
 }

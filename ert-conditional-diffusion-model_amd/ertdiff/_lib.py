@@ -48,6 +48,14 @@ _VP, _I, _U32, _U64, _SZ, _F = (ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32,
                                 ctypes.c_uint64, ctypes.c_size_t, ctypes.c_float)
 _LL = ctypes.c_longlong
 _W = ctypes.POINTER(ErtdWeights)
+class PackDesc(ctypes.Structure):
+    """ertd_pack_desc (include/ertdiff.h): one weight packing of a batched pack."""
+    _fields_ = [("w", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("total", ctypes.c_longlong),
+                ("cin", ctypes.c_int), ("cout", ctypes.c_int), ("ks", ctypes.c_int), ("kind", ctypes.c_int),
+                ("flip", ctypes.c_int), ("nchunk", ctypes.c_int), ("block0", ctypes.c_int),
+                ("reserved", ctypes.c_int)]
+
+
 SIGNATURES = {
     "ertd_version": (_I, []),
     "ertd_error_string": (ctypes.c_char_p, [_I]),
@@ -126,6 +134,11 @@ SIGNATURES = {
     "ertd_conv_wgrad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
     "ertd_conv_input_grad_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
     "ertd_conv_input_grad": (_I, [_VP, _I, _I, _VP, _I, _I, _I, _I, _VP, _I, _VP, ctypes.c_size_t, _VP]),
+    "ertd_conv_input_grad_run": (_I, [_VP, _I, _I, _I, _I, _I, _I, _VP, _I, _VP, ctypes.c_size_t, _VP]),
+    "ertd_conv2d_pack_desc": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _VP, _VP, _VP]),
+    "ertd_conv_input_grad_pack_desc": (_I, [_I, _I, _I, _I, _I, _I, _VP, _VP, _VP]),
+    "ertd_conv_pack_batch_prepare": (_I, [_VP, _I]),
+    "ertd_conv_pack_batch": (_I, [_VP, _I, _I, _VP]),
     "ertd_conv_wgrad": (_I, [_VP, _VP, _I, _VP, _I, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _VP,
                              ctypes.c_size_t, _VP]),
     "ertd_encoder_train_ws_bytes": (_SZ, [_I, _I]),

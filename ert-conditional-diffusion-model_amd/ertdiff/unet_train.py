@@ -56,15 +56,84 @@ def _arr(ts, ctype=ctypes.c_void_p):
     return (ctype * len(ts))(*ts)
 
 
+class _PackRegistry:
+    """Every conv's weight packings, rebuilt ONCE per optimizer step in one launch.
+
+    Each conv call site (forward conv, input-gradient conv) of the train walk
+    owns a persistent workspace whose head holds its packing.  The first walk
+    packs per call (ertd_conv2d / ertd_conv_input_grad) and records each
+    packing's descriptor (ertd_conv2d_pack_desc / ertd_conv_input_grad_pack_desc:
+    the library's own dispatch decides the layout); at the end of that backward
+    the descriptor table is uploaded once.  From then on a forward walk starts
+    with one ertd_conv_pack_batch launch that re-packs all of them (~100 for
+    U2) from the current weights, and the convs run on their packings
+    (ertd_conv2d_run / ertd_conv_input_grad_run).  Held per (model, batch)."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.lib = _lib.lib()
+        self.entries = {}          # key -> (ws, PackDesc, parameter)
+        self.table: Optional[torch.Tensor] = None
+        self.in_table = set()
+        self.blocks = 0
+        self.armed = False         # the batch ran at the start of this walk
+
+    def start(self, k: "_K"):
+        self.armed = False
+        if self.table is None:
+            return
+        if any(p.data_ptr() != d.w for _, d, p in self.entries.values()):
+            self.__init__(self.dev)            # parameters replaced: start over
+            return
+        _lib.check(self.lib.ertd_conv_pack_batch(self.table.data_ptr(), len(self.in_table), self.blocks, k.s),
+                   "conv_pack_batch")
+        self.armed = True
+
+    def finish(self):
+        if self.table is not None or not self.entries:
+            return
+        keys = list(self.entries)
+        arr = (_lib.PackDesc * len(keys))(*[self.entries[q][1] for q in keys])
+        blocks = self.lib.ertd_conv_pack_batch_prepare(arr, len(keys))
+        if blocks <= 0:
+            raise RuntimeError(f"ertdiff: ertd_conv_pack_batch_prepare failed ({blocks})")
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self.table = host.to(self.dev)
+        self.in_table = set(keys)
+        self.blocks = blocks
+
+    def get(self, key, nbytes, describe, param):
+        """(workspace, packed-already) for one call site; describe(ws, desc) fills a new descriptor."""
+        e = self.entries.get(key)
+        if e is None:
+            ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.dev)
+            d = _lib.PackDesc()
+            describe(ws, d)
+            self.entries[key] = (ws, d, param)
+            self.table = None            # rebuilt (with this call site) after the walk
+            return ws, False
+        return e[0], self.armed and key in self.in_table
+
+
+def _packs_of(model, B) -> _PackRegistry:
+    reg = model.__dict__.setdefault("_train_packs", {})
+    dev = model.conv_in.weight.device
+    r = reg.get(B)
+    if r is None or r.dev != dev:
+        r = reg[B] = _PackRegistry(dev)
+    return r
+
+
 class _K:
     """Thin wrappers: each is one or two HIP kernel launches (raise on error)."""
 
-    def __init__(self, dev):
+    def __init__(self, dev, packs: Optional[_PackRegistry] = None):
         self.dev = dev
         self.lib = _lib.lib()
         self.s = _lib.stream_of(dev)
         self._ws: Optional[torch.Tensor] = None
         self._zero: Dict[int, torch.Tensor] = {}
+        self.packs = packs
 
     def empty(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)
@@ -85,21 +154,35 @@ class _K:
         return self._ws
 
     # ---- convolution forward / input gradient (ertd_conv2d)
-    def conv(self, x, w, b, xb=None, mode=MODE_S1, ebias=None, res=None, gn=None, act=0):
+    def conv(self, x, w, b, xb=None, mode=MODE_S1, ebias=None, res=None, gn=None, act=0, name=None):
         """conv(act(cat(x, xb))) + b (+ ebias[:, :, None, None]) (+ res); act(v) =
         v * gn.scale + gn.shift (+ SiLU) applied while staging; ebias may be a
-        column block of a wider (B, n) matrix (its row stride is passed)."""
+        column block of a wider (B, n) matrix (its row stride is passed).
+        name: the call site (its packing lives in the pack registry)."""
         B, Ca, H, _ = x.shape
         Cb = 0 if xb is None else xb.shape[1]
         Cout, Cin, ks, _ = w.shape
         Ho = H // 2 if mode == MODE_S2 else (2 * H if mode == MODE_UP else H)
         out = self.empty(B, Cout, Ho, Ho)
         n = self.lib.ertd_conv2d_workspace_bytes(Cin, Cout, ks, PREC_FP32, B, H, mode)
-        ws = self.ws(n)
-        _lib.check(self.lib.ertd_conv2d(
-            x.data_ptr(), Ca, _p(xb), Cb, B, H, w.data_ptr(), b.data_ptr(), Cout, ks, mode, _p(gn), act,
-            _p(ebias), 0 if ebias is None else ebias.stride(0), _p(res), out.data_ptr(), PREC_FP32,
-            ws.data_ptr(), ws.numel(), self.s), "conv2d")
+        packed = False
+        if self.packs is not None and name is not None:
+            def describe(ws, d):
+                _lib.check(self.lib.ertd_conv2d_pack_desc(Cin, Ca, Cout, ks, mode, PREC_FP32, B, H, w.data_ptr(),
+                                                          ws.data_ptr(), ctypes.byref(d)), "conv2d_pack_desc")
+            ws, packed = self.packs.get(("fwd", name, Ca, B, H), n, describe, w)
+        else:
+            ws = self.ws(n)
+        eb_ld = 0 if ebias is None else ebias.stride(0)
+        if packed:
+            _lib.check(self.lib.ertd_conv2d_run(
+                x.data_ptr(), Ca, _p(xb), Cb, B, H, b.data_ptr(), Cout, ks, mode, _p(gn), act, _p(ebias), eb_ld,
+                _p(res), out.data_ptr(), PREC_FP32, ws.data_ptr(), ws.numel(), self.s), "conv2d_run")
+        else:
+            _lib.check(self.lib.ertd_conv2d(
+                x.data_ptr(), Ca, _p(xb), Cb, B, H, w.data_ptr(), b.data_ptr(), Cout, ks, mode, _p(gn), act,
+                _p(ebias), eb_ld, _p(res), out.data_ptr(), PREC_FP32, ws.data_ptr(), ws.numel(), self.s),
+                "conv2d")
         return out
 
     # ---- GroupNorm
@@ -179,17 +262,30 @@ class _K:
         _lib.check(self.lib.ertd_wgrad_gemm(dy.data_ptr(), col.data_ptr(), M, N, P, B, M * P, N * P,
                                             out.data_ptr(), 0, ws.data_ptr(), n, self.s), "wgrad_gemm")
 
-    def conv_input_grad(self, dy, w, mode, H):
+    def conv_input_grad(self, dy, w, mode, H, name=None):
         """dL/dx (B, Cin, H, H) of y = conv(x) with weight w given dy: a conv of dy with
-        w transposed and flipped, packed straight from w (ertd_conv_input_grad)."""
+        w transposed and flipped (ertd_conv_input_grad; with a registry, the packing
+        of the step's batched pack)."""
         Cout, Cin, ks, _ = w.shape
         B = dy.shape[0]
         n = self.lib.ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, ks, mode)
-        ws = self.ws(n)
+        packed = False
+        if self.packs is not None and name is not None:
+            def describe(ws, d):
+                _lib.check(self.lib.ertd_conv_input_grad_pack_desc(Cin, Cout, B, H, ks, mode, w.data_ptr(),
+                                                                   ws.data_ptr(), ctypes.byref(d)),
+                           "conv_input_grad_pack_desc")
+            ws, packed = self.packs.get(("dgrad", name, B, H), n, describe, w)
+        else:
+            ws = self.ws(n)
         dx = self.empty(B, Cin, H, H)
-        _lib.check(self.lib.ertd_conv_input_grad(dy.data_ptr(), B, H, w.data_ptr(), Cout, Cin, ks, mode,
-                                                 dx.data_ptr(), 0, ws.data_ptr(), ws.numel(), self.s),
-                   "conv_input_grad")
+        if packed:
+            _lib.check(self.lib.ertd_conv_input_grad_run(dy.data_ptr(), B, H, Cout, Cin, ks, mode, dx.data_ptr(), 0,
+                                                         ws.data_ptr(), ws.numel(), self.s), "conv_input_grad_run")
+        else:
+            _lib.check(self.lib.ertd_conv_input_grad(dy.data_ptr(), B, H, w.data_ptr(), Cout, Cin, ks, mode,
+                                                     dx.data_ptr(), 0, ws.data_ptr(), ws.numel(), self.s),
+                       "conv_input_grad")
         return dx
 
     def flip(self, w):
@@ -342,7 +438,7 @@ def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, g
     if not x_needs_grad:
         return None
     # input gradient: a conv of dY with the flipped, transposed weights
-    return k.conv_input_grad(dy, w, mode, xa.shape[2])
+    return k.conv_input_grad(dy, w, mode, xa.shape[2], name=name)
 
 
 def _encoder_pack(model: ConditionalUNet, k: _K, W):
@@ -363,19 +459,20 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
     if model.precision != "fp32":
         raise RuntimeError("ertdiff: the U-Net train step runs fp32 (set_precision('fp32'))")
     dev = _lib.require_device(x, t, cond, model.conv_in.weight)
-    k = _K(dev)
+    B = x.shape[0]
+    k = _K(dev, _packs_of(model, B))
     W = dict(model.named_parameters())
     for n, p in W.items():
         if not p.is_contiguous():
             raise RuntimeError(f"ertdiff: parameter {n} must be contiguous")
     sp = model.spec
     g = sp["groups"]
-    B = x.shape[0]
     img = model.image
     L = cond.shape[2]
     tape = {"k": k, "B": B, "L": L, "cond": cond, "nodes": []}
     nodes = tape["nodes"]
     with torch.cuda.device(dev):
+        k.packs.start(k)           # every conv packing of this step: one launch
         # ---- embedding path
         from .model import get_timestep_embedding
         sin = get_timestep_embedding(t, sp["ch"])
@@ -416,19 +513,20 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             ss1, mr1 = k.gn_stats(xa, xb, g, W[n + ".norm1.weight"], W[n + ".norm1.bias"])
             eb = eb_all[:, eoff[n]:eoff[n] + cout]
             h = k.conv(xa, W[n + ".conv1.weight"], W[n + ".conv1.bias"], xb=xb, ebias=eb, gn=ss1,
-                       act=ACT_GN_SILU)
+                       act=ACT_GN_SILU, name=n + ".conv1")
             ss2, mr2 = k.gn_stats(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"])
             if Cin != cout:
-                sk = k.conv(xa, W[n + ".skip.weight"], W[n + ".skip.bias"], xb=xb)
+                sk = k.conv(xa, W[n + ".skip.weight"], W[n + ".skip.bias"], xb=xb, name=n + ".skip")
             else:
                 sk = xa
-            y = k.conv(h, W[n + ".conv2.weight"], W[n + ".conv2.bias"], res=sk, gn=ss2, act=ACT_GN_SILU)
+            y = k.conv(h, W[n + ".conv2.weight"], W[n + ".conv2.bias"], res=sk, gn=ss2, act=ACT_GN_SILU,
+                       name=n + ".conv2")
             nodes.append(("res", n, dict(xa=xa, xb=xb, ss1=ss1, mr1=mr1, h=h, ss2=ss2, mr2=mr2,
                                          skip=Cin != cout, y=y)))
             return y
 
         x4 = x.reshape(B, 1, img, img)
-        h = k.conv(x4, W["conv_in.weight"], W["conv_in.bias"])
+        h = k.conv(x4, W["conv_in.weight"], W["conv_in.bias"], name="conv_in")
         nodes.append(("conv_in", "conv_in", dict(x=x4, y=h)))
         hs = [h]
         nl = len(sp["ch_mult"])
@@ -438,7 +536,7 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
                 hs.append(h)
             if i != nl - 1:
                 y = k.conv(h, W[f"down.{i}.downsample.weight"], W[f"down.{i}.downsample.bias"],
-                           mode=MODE_S2)
+                           mode=MODE_S2, name=f"down.{i}.downsample")
                 nodes.append(("down", f"down.{i}.downsample", dict(x=h, y=y)))
                 h = y
                 hs.append(h)
@@ -448,7 +546,8 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             C = h.shape[1]
             N = h.shape[2] * h.shape[3]
             ssn, mrn = k.gn_stats(h, None, g, W[n + ".norm.weight"], W[n + ".norm.bias"])
-            qkv = k.conv(h, W[n + ".qkv.weight"], W[n + ".qkv.bias"], gn=ssn, act=ACT_GN).view(B, 3, C, N)
+            qkv = k.conv(h, W[n + ".qkv.weight"], W[n + ".qkv.bias"], gn=ssn, act=ACT_GN,
+                         name=n + ".qkv").view(B, 3, C, N)
             q, kk, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
             S = k.empty(B, N, N)    # S[i][j] = sum_c q[c][i] k[c][j]
             k.gemm(q, (1, N, 3 * C * N), kk, (N, 1, 3 * C * N), S, (N, 1, N * N), N, N, C, batch=B)
@@ -456,7 +555,7 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             O = k.empty(B, C, N)    # O[c][i] = sum_j v[c][j] P[i][j]
             k.gemm(v, (N, 1, 3 * C * N), P, (1, N, N * N), O, (N, 1, C * N), C, N, N, batch=B)
             O4 = O.view(B, C, h.shape[2], h.shape[3])
-            y = k.conv(O4, W[n + ".proj.weight"], W[n + ".proj.bias"], res=h)
+            y = k.conv(O4, W[n + ".proj.weight"], W[n + ".proj.bias"], res=h, name=n + ".proj")
             nodes.append(("attn", n, dict(x=h, ss=ssn, mr=mrn, qkv=qkv, P=P, O=O4, y=y)))
             h = y
         h = resblock("mid.res2", h, None)
@@ -465,11 +564,12 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
                 sk = hs.pop()
                 h = resblock(f"up.{i}.res.{r}", h, sk)
             if i != 0:
-                y = k.conv(h, W[f"up.{i}.upsample.weight"], W[f"up.{i}.upsample.bias"], mode=MODE_UP)
+                y = k.conv(h, W[f"up.{i}.upsample.weight"], W[f"up.{i}.upsample.bias"], mode=MODE_UP,
+                           name=f"up.{i}.upsample")
                 nodes.append(("up", f"up.{i}.upsample", dict(x=h, y=y)))
                 h = y
         sso, mro = k.gn_stats(h, None, g, W["norm_out.weight"], W["norm_out.bias"])
-        eps = k.conv(h, W["conv_out.weight"], W["conv_out.bias"], gn=sso, act=ACT_GN_SILU)
+        eps = k.conv(h, W["conv_out.weight"], W["conv_out.bias"], gn=sso, act=ACT_GN_SILU, name="conv_out")
         nodes.append(("out", "conv_out", dict(x=h, ss=sso, mr=mro, y=eps)))
     return eps.reshape(B, -1), tape
 
@@ -613,6 +713,8 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
     missing = [nm for nm, _ in model.layout if nm not in grads]
     if missing:
         raise RuntimeError(f"ertdiff: no gradient for {missing[:4]}")
+    if k.packs is not None:
+        k.packs.finish()           # every call site seen: batch the packings from the next step on
     return grads
 
 

@@ -438,9 +438,44 @@ size_t ertd_conv_input_grad_ws_bytes(int Cin, int Cout, int B, int H, int ks, in
 int ertd_conv_input_grad(const float* dy, int B, int H, const float* w, int Cout, int Cin, int ks,
                          int mode, float* dx, int accumulate, void* ws, size_t ws_bytes,
                          void* stream);
+/* ertd_conv_input_grad_run: the same, reusing the flipped packing an earlier
+ *   ertd_conv_input_grad (or ertd_conv_pack_batch with the descriptor of
+ *   ertd_conv_input_grad_pack_desc) left at the head of ws.                    */
+int ertd_conv_input_grad_run(const float* dy, int B, int H, int Cout, int Cin, int ks, int mode,
+                             float* dx, int accumulate, void* ws, size_t ws_bytes, void* stream);
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
                     int Cout, int ks, int mode, const float* gn, int act, float* dw, int accumulate,
                     void* ws, size_t ws_bytes, void* stream);
+
+/* Batched fp32 weight packing (the train step packs every conv once per
+ * optimizer step, in one launch).  A descriptor names one packing: the source
+ * weight, its destination, and the layout a later ertd_conv2d_run /
+ * ertd_conv_input_grad_run on that workspace reads -- filled by the two
+ * *_pack_desc queries from the same dispatch decisions as ertd_conv2d /
+ * ertd_conv_input_grad, so the batch writes exactly their packings, bit for bit. */
+#define ERTD_PACK_DIRECT 0 /* implicit-GEMM fragment order (1x1 / 3x3)   */
+#define ERTD_PACK_UP 1     /* sub-pixel Upsample classes                 */
+#define ERTD_PACK_WINO 2   /* Winograd F(2x2,3x3) U = G g G^T            */
+#define ERTD_PACK_WINO4 3  /* Winograd F(4x4,3x3)                        */
+typedef struct {
+  const float* w;      /* source weight (Cout, Cin, ks, ks) of the FORWARD conv    */
+  float* dst;          /* destination (inside the conv's workspace)               */
+  long long total;     /* packed floats                                           */
+  int cin, cout, ks;   /* of the packed conv (flip: the input-gradient conv's)    */
+  int kind;            /* ERTD_PACK_*                                             */
+  int flip;            /* 1: the input-gradient conv's transposed, flipped weight */
+  int nchunk;          /* K chunks of the layout                                  */
+  int block0;          /* first 256-thread block (ertd_conv_pack_batch_prepare)   */
+  int reserved;
+} ertd_pack_desc;
+int ertd_conv2d_pack_desc(int Cin, int Ca, int Cout, int ks, int mode, int precision, int B, int H,
+                          const float* w, void* ws, ertd_pack_desc* out);
+int ertd_conv_input_grad_pack_desc(int Cin, int Cout, int B, int H, int ks, int mode, const float* w,
+                                   void* ws, ertd_pack_desc* out);
+/* host: fills block0 of descs[0..n) in order; returns the batch's block count (< 0: error) */
+int ertd_conv_pack_batch_prepare(ertd_pack_desc* descs, int n);
+/* one launch packing all n descriptors (descs: DEVICE copy of the prepared table) */
+int ertd_conv_pack_batch(const ertd_pack_desc* descs, int n, int blocks, void* stream);
 int ertd_concat(const float* const* srcs, const long long* sizes, int n, float* dst, void* stream);
 /* ertd_split: dsts[k] = alpha * src[sum(sizes[<k]) ...] (the inverse of ertd_concat, scaled):
  *   the data-parallel train step's gradient bucket back into the per-tensor gradients. */
