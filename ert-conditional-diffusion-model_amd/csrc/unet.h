@@ -128,6 +128,16 @@ hipError_t launch_pack_conv_wino4(const float* w, int cin, int cout, float* dst,
 hipError_t launch_conv_wino4(int act, const ConvArgs& a, int B, hipStream_t s, int cus);
 int wino4_tile_items(int cout, int wo, int B);
 bool wino4_ksplit(int cin, int cout, int wo, int B);
+// F(4x4) with register-resident weights (unet_conv_wino4s.hip): items of 64 co x
+// 16 tiles (the 16x16 level fills the CUs at B = 64 without a K split); same
+// wpk_wino4 packing; Cin a multiple of 8, Ca even, W in {16, 32, 64}.  wino4_ok
+// is true where wino4s_ok is, and launch_conv_wino then dispatches it.
+bool wino4s_ok(int cin, int ca, int cout, int wo, int B);
+int wino4s_items(int cout, int wo, int B);
+// the same kernel for the fp32 Upsample conv (MODE_UP, no activation; wo = the
+// OUTPUT width): conv3x3 of the nearest-x2 source through the F(4x4) packing
+bool wino4s_up_ok(int cin, int ca, int cout, int wo, int B);
+hipError_t launch_conv_wino4s(int act, const ConvArgs& a, int B, hipStream_t s, int cus);
 hipError_t launch_add_inplace(float* out, const float* part, size_t n, hipStream_t s);
 // flipT: w is a forward conv's (cin, cout, 3, 3) weight; pack the input-gradient
 // conv's weight W'[co][ci] = W[ci][co] spatially flipped (training)

@@ -185,6 +185,12 @@ Layout layout(const ertd_unet_config* c) {
     // fp32 ResBlock 3x3 convs also get the Winograd F(2x2,3x3) packing
     // (dispatch picks it when conv_wino_ok; ERTD_UNET_WINO=0 keeps the direct one)
     if (c->precision == ERTD_PREC_FP32 && p.shape.size() == 4 && p.shape[2] == 3 &&
+        ends_with(p.name, ".upsample.weight") && conv_packed_floats_wino4(p.shape[1], p.shape[0]) > 0) {
+      // ... and the Upsample convs the F(4x4) packing (wino4s_up_ok dispatch)
+      L.offw4[p.name] = o;
+      o += a64(conv_packed_floats_wino4(p.shape[1], p.shape[0]));
+    }
+    if (c->precision == ERTD_PREC_FP32 && p.shape.size() == 4 && p.shape[2] == 3 &&
         (ends_with(p.name, ".conv1.weight") || ends_with(p.name, ".conv2.weight")) &&
         conv_packed_floats_wino(p.shape[1], p.shape[0]) > 0) {
       L.offw[p.name] = o;
@@ -759,8 +765,9 @@ int conv2d_impl(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   // the Winograd path reads only its own packing: skip the direct one then
   const int Ho_ = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   const bool bf = bf_prec(precision), split = precision == ERTD_PREC_BF16X3;
-  const bool wino4 = !bf && ks == 3 && mode == MODE_S1 && Cout > 1 &&
-                     conv_packed_floats_wino4(Cin, Cout) > 0 && wino4_ok(Cin, Ca, Cout, Ho_, B);
+  const bool wino4 = !bf && ks == 3 && Cout > 1 && conv_packed_floats_wino4(Cin, Cout) > 0 &&
+                     ((mode == MODE_S1 && wino4_ok(Cin, Ca, Cout, Ho_, B)) ||
+                      (mode == MODE_UP && act == ACT_NONE && wino4s_up_ok(Cin, Ca, Cout, Ho_, B)));
   const bool wino = wino4 || (!bf && ks == 3 && mode == MODE_S1 && Cout > 1 &&
                               conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho_));
   hipError_t e = hipSuccess;
@@ -938,8 +945,10 @@ int ertd_conv2d_pack_desc(int Cin, int Ca, int Cout, int ks, int mode, int preci
     return ERTD_EINVAL;
   const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   float* pk = (float*)ws;
-  const bool wino4 = ks == 3 && mode == MODE_S1 && Cout > 1 && conv_packed_floats_wino4(Cin, Cout) > 0 &&
-                     wino4_ok(Cin, Ca, Cout, Ho, B);
+  // (the fp32 Upsample conv has no activation: ertd_conv2d_run dispatches it with ACT_NONE)
+  const bool wino4 = ks == 3 && Cout > 1 && conv_packed_floats_wino4(Cin, Cout) > 0 &&
+                     ((mode == MODE_S1 && wino4_ok(Cin, Ca, Cout, Ho, B)) ||
+                      (mode == MODE_UP && wino4s_up_ok(Cin, Ca, Cout, Ho, B)));
   const bool wino = wino4 || (ks == 3 && mode == MODE_S1 && Cout > 1 && conv_packed_floats_wino(Cin, Cout) > 0 &&
                               conv_wino_ok(Cin, Ca, Cout, Ho));
   if (wino) {

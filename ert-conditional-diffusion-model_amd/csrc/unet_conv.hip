@@ -503,10 +503,17 @@ static hipError_t launch_t(const ConvArgs& a, int B, hipStream_t s) {
   return launch_w<KS, MODE, ACT, 1>(a, B, s);
 }
 
+// the fp32 Upsample conv through the F(4x4) register-weight kernel
+static bool wino4s_up_dispatchable(int ks, int mode, int act, const ConvArgs& a, int B) {
+  return ks == 3 && mode == MODE_UP && act == ACT_NONE && a.wpk_wino4 && a.Hs * 2 == a.Ho &&
+         wino4s_up_ok(a.Cin, a.Ca, a.Cout, a.Wo, B);
+}
+
 int conv_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B) {
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN) return 0;   // conv_out
   if (conv_in_ok(a, ks, mode, act)) return 0;
   if (ks == 3 && mode == MODE_S1 && wino_dispatchable(a, B)) return wino_gn_parts(a, B);
+  if (wino4s_up_dispatchable(ks, mode, act, a, B)) return (a.Wo / 4) * (a.Wo / 4) / 16;
   return 0;
 }
 
@@ -523,6 +530,7 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
   if (ks == 3 && mode == MODE_S1 && act == ACT_NONE) return launch_t<3, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) return launch_t<3, MODE_S1, ACT_GN_SILU>(a, B, s);
   if (ks == 3 && mode == MODE_S2 && act == ACT_NONE) return launch_t<3, MODE_S2, ACT_NONE>(a, B, s);
+  if (wino4s_up_dispatchable(ks, mode, act, a, B)) return launch_conv_wino4s(act, a, B, s, device_cu_count());
   if (ks == 3 && mode == MODE_UP && act == ACT_NONE) {
     // sub-pixel: 2x2 taps per class at the source resolution (weights packed
     // by launch_pack_conv_up); the template width is the SOURCE width

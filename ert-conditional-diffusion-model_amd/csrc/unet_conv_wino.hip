@@ -638,14 +638,38 @@ static int wino4_w16_env() {
   return v;
 }
 
+// ERTD_WINO4S (A/B): 0 off, 1 the 16x16 level (where its items fill the CUs),
+// 2 every eligible level, 3 the 32x32 / 64x64 levels only, 4 (default) the
+// 32x32 / 64x64 levels and 16x16 where its items fill the CUs.  U2 B=64
+// (same box): 204.3 steps/s off, 222.1 (1), 224.2 (2), 205.9 (3).
+static int wino4s_env() {
+  static int v = [] {
+    const char* e = getenv("ERTD_WINO4S");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
+bool wino4s_ok(int cin, int ca, int cout, int wo, int B) {
+  const int e = wino4s_env();
+  if (e == 0 || wino_env() != 1 || cin % 8 || ca % 2 || cout % 64) return false;
+  if (wo != 16 && wo != 32 && wo != 64) return false;
+  if (e == 2) return true;
+  if (e == 3) return wo != 16;
+  if (e == 4 && wo != 16) return true;
+  return wo == 16 && wino4s_items(cout, wo, B) >= cu_count();
+}
+
 bool wino4_ok(int cin, int ca, int cout, int wo, int B) {
   if (wino_env() != 1 || cin % 4 || ca % 4 || cout % 64) return false;
+  if (wino4s_ok(cin, ca, cout, wo, B)) return true;
   if (wo == 16)
     return B % 2 == 0 && (wino4_w16_env() == 1 || wino4_tile_items(cout, wo, B) >= cu_count());
   return wo == 32 || wo == 64 || wo == 128;
 }
 
 bool wino4_ksplit(int cin, int cout, int wo, int B) {
+  if (wino4s_ok(cin, cin, cout, wo, B)) return false;
   const int nchunk = cin / 4;
   return nchunk % 2 == 0 && nchunk >= 4 && wino4_tile_items(cout, wo, B) < ksplit_items() * cu_count();
 }
@@ -699,6 +723,9 @@ int wino_gn_parts(const ConvArgs& a, int B) {
 }
 
 hipError_t launch_conv_wino(int act, const ConvArgs& a, int B, hipStream_t s) {
+  if (a.wpk_wino4 && wino4s_ok(a.Cin, a.Ca, a.Cout, a.Wo, B) && a.Ho == a.Wo && a.Hs == a.Ho &&
+      a.Ws == a.Wo)
+    return launch_conv_wino4s(act, a, B, s, cu_count());
   if (a.wpk_wino4 && wino4_ok(a.Cin, a.Ca, a.Cout, a.Wo, B) && a.Ho == a.Wo && a.Hs == a.Ho &&
       a.Ws == a.Wo)
     return launch_conv_wino4(act, a, B, s, cu_count());

@@ -1,0 +1,515 @@
+// Winograd F(4x4,3x3) with register-resident weights: the variant of
+// conv_wino4_kernel (unet_conv_wino4.hip, same points, same U packing, same
+// fp32 arithmetic) for work items of 64 output channels x 16 tiles.
+//
+// Why a second schedule: conv_wino4_kernel stages the transformed weights U
+// through a 108 KB LDS ring and feeds BOTH MFMA operands from LDS; its items
+// are 64 co x 32 tiles, so at 16x16 (16 tiles per sample) a B = 64 batch has
+// 128 items for 256 CUs and the level ran F(2x2) instead.  Here
+//   * each of the 4 MFMA waves (one per SIMD) owns 16 co x 16 tiles x all 36 xi
+//     (144 accumulator VGPRs) and streams ITS OWN U fragments from L2 straight
+//     into VGPRs (18 buffer_load_dwordx2 per k-step, one k-step ahead, double
+//     buffered: the A operand never touches LDS, no LDS-DMA issue on the MFMA
+//     waves) -- no other wave reads them, so nothing is lost by not sharing;
+//   * LDS holds only V (the transformed input, 18 KB per 8-channel chunk,
+//     double-buffered): one ds_read_b64 per xi pair feeds two MFMAs;
+//   * 4 producer waves, each two channels of the chunk (lane = channel bit 5,
+//     column half bit 4, tile bits 0-3), do GroupNorm + SiLU + B^T d B exactly
+//     as conv_wino4_kernel's producers (the half exchange is v_permlane16_swap:
+//     the halves are 16 lanes apart here);
+//   * 512 threads, 256 VGPRs per wave (2 waves per SIMD), 36 KB of LDS.
+// Item = (co group of 64, block of 16 consecutive tiles of one sample); the
+// output transform, bias / emb / residual epilogue and the GroupNorm partials
+// (one part per 16 tiles, as conv_wino4_kernel) are per MFMA wave.  No K split.
+#include <cstdlib>
+#include <type_traits>
+
+#include "unet.h"
+
+namespace ertd {
+namespace unet {
+
+namespace {
+
+constexpr int NMW = 4;                        // MFMA waves (one per SIMD)
+constexpr int NPW = 4;                        // producer waves
+constexpr int WT = 64 * (NMW + NPW);          // 512 threads
+constexpr int CCH = 8;                        // input channels per chunk (2 MFMA k-steps)
+constexpr int NX = 36;
+constexpr int VKS = 18 * 128;                 // V floats per k-step: [xi/2 18][k 4][tile 16][xi&1]
+constexpr int V_FL = 2 * VKS;                 // per chunk (4608 floats = 18 KB)
+constexpr size_t WLDS = (size_t)2 * V_FL * sizeof(float);   // 36 KB
+constexpr int NRS = 3;                        // producer register sets
+#ifndef WINO4S_PPRIO
+#define WINO4S_PPRIO 2
+#endif
+#ifndef WINO4S_PD
+#define WINO4S_PD 2                           // V operand read-ahead (xi pairs)
+#endif
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned;
+
+__device__ __forceinline__ f32x2 fmac(f32x2 x, float c, f32x2 s) {
+  return __builtin_elementwise_fma(x, f32x2{c, c}, s);
+}
+// B^T d and A^T m of the points {0, 1, -1, 1/2, -2, inf} (unet_conv_wino4.hip)
+__device__ __forceinline__ void bt6(const float (&d)[6], float (&o)[6]) {
+  const float c = d[4] - d[2], e = d[3] - d[1];
+  const float u = d[4] - d[1], v = d[4] + d[1];
+  o[0] = __builtin_fmaf(1.5f, e, __builtin_fmaf(-2.f, d[2], d[0] + d[4]));
+  o[1] = __builtin_fmaf(2.5f, d[3], __builtin_fmaf(0.5f, d[2], u));
+  o[2] = __builtin_fmaf(0.5f, d[3], __builtin_fmaf(-2.5f, d[2], v));
+  o[3] = __builtin_fmaf(2.f, e, c);
+  o[4] = __builtin_fmaf(-0.5f, e, c);
+  o[5] = __builtin_fmaf(1.5f, c, __builtin_fmaf(-2.f, d[3], d[1] + d[5]));
+}
+__device__ __forceinline__ void at6(const f32x2 (&m)[6], f32x2 (&y)[4]) {
+  const f32x2 s = m[1] + m[2], d = m[1] - m[2];
+  y[0] = (m[0] + s) + (m[3] + m[4]);
+  y[1] = fmac(m[3], 0.5f, fmac(m[4], -2.f, d));
+  y[2] = fmac(m[3], 0.25f, fmac(m[4], 4.f, s));
+  y[3] = fmac(m[3], 0.125f, fmac(m[4], -8.f, d + m[5]));
+}
+
+// item it -> (co group, 16-tile block): co group fastest
+struct Item {
+  int cog, blk;
+};
+__device__ __forceinline__ Item item_of(int it, int ncog) {
+  Item r;
+  r.cog = it % ncog;
+  r.blk = it / ncog;
+  return r;
+}
+
+// UP: the Upsample conv, conv3x3 of the nearest-x2 upsampled source (WO / 2)^2:
+// the window rows 4ty-1 .. 4ty+4 of the upsampled image are source rows 2ty-1,
+// 2ty, 2ty, 2ty+1, 2ty+1, 2ty+2 and a lane's two columns one source column, so
+// a producer lane loads 4 source values instead of 12 (36 of the 144
+// multiplies per 4x4 output tile, against 64 for the sub-pixel direct kernel)
+template <int WO, int ACT, bool UP>
+__global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* vbuf = smem;                  // [2][V_FL]
+
+  constexpr int TPR = WO / 4;
+  constexpr int HW = WO * WO;
+  constexpr int TS = TPR * TPR;        // tiles per sample (a multiple of 16)
+  constexpr int WS = UP ? WO / 2 : WO; // source width
+  constexpr int HWS = WS * WS;
+  static_assert(TS % 16 == 0 && TPR <= 16, "a 16-tile block is whole tile rows of one sample");
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Cin = a.Cin, Ca = a.Ca;
+  const int nchunk = Cin / CCH;
+  const int ncog = a.Cout / 64;
+  const int bid = blockIdx.x, G = gridDim.x;
+  const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;
+  const int gtot = nloc * nchunk;
+
+  if (wave >= NMW) {
+    // =================== producer waves ===================
+    __builtin_amdgcn_s_setprio(WINO4S_PPRIO);
+    const int q = wave - NMW;                 // channels 2q, 2q+1 of every chunk
+    const int chb = lane >> 5, h = (lane >> 4) & 1, t = lane & 15;
+    const int cl = 2 * q + chb;               // channel of the chunk: k-step cl >> 2, k = cl & 3
+    const int vwoff = ((((cl >> 2) * 18 + 9 * h) * 4 + (cl & 3)) * 16 + t) * 2;
+    // the outer window column from the neighbouring tile's other half (16 lanes apart)
+    const int nbaddr = (lane + 15 - 30 * h) * 4;
+    const unsigned choff = (unsigned)(chb * HWS * 4);
+    float2 raw[NRS][6];
+    float2 gnv[NRS];
+    f32x4 pad[NRS];
+    int cur_g = 0, cur_k = 0, cur_b = 0, cur_il = 0;
+    unsigned roff[6];   // per window row (UP: per distinct source row, 4)
+    f32x4 cur_pad;
+    auto set_item = [&](int il) {
+      const Item itm = item_of(bid + il * G, ncog);
+      const int flat0 = itm.blk * 16;
+      cur_b = flat0 / TS;
+      const int tg = flat0 % TS + t;
+      const int ty = tg / TPR, tx = tg - ty * TPR;
+      if constexpr (UP) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int sy = 2 * ty - 1 + r;
+          roff[r] = (unsigned)(((sy >= 0 && sy < WS ? sy : 2 * ty) * WS + 2 * tx + h) * 4) + choff;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          const int iy = 4 * ty - 1 + r;
+          roff[r] = (unsigned)(((iy >= 0 && iy < WO ? iy : 4 * ty) * WO + 4 * tx + 2 * h) * 4) + choff;
+        }
+      }
+      cur_pad = f32x4{ty > 0 ? 1.f : 0.f, ty < TPR - 1 ? 1.f : 0.f,
+                      (h ? tx < TPR - 1 : tx > 0) ? 1.f : 0.f, 0.f};
+    };
+    const int glast = gtot - 1;
+    auto load_next = [&](const int set) {
+      const int cg = cur_k * CCH + 2 * q;     // wave-uniform first channel of the pair
+      pad[set] = cur_pad;
+      if constexpr (ACT != ACT_NONE) gnv[set] = a.gn[(size_t)cur_b * Cin + cg + chb];
+      const bool inA = cg < Ca;               // Ca even: both channels on one side
+      const float* p = inA ? a.srcA + ((size_t)cur_b * Ca + cg) * HWS
+                           : a.srcB + ((size_t)cur_b * a.Cb + (cg - Ca)) * HWS;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 2 * HWS * 4, 0x00020000);
+      if constexpr (UP) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)roff[r], 0, 0));
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          const float u = v[(r + 1) >> 1];
+          raw[set][r] = make_float2(u, u);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)roff[r], 0, 0);
+          raw[set][r] = make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+        }
+      }
+      if (cur_g < glast) {
+        ++cur_g;
+        if (++cur_k == nchunk) {
+          cur_k = 0;
+          set_item(++cur_il);
+        }
+      }
+    };
+    // act[ab][c][i]: row i of B^T d for local column c (window columns 1+2h,
+    // 2+2h and the outer one): the lane transforms its own two columns and takes
+    // the outer column's transform from the neighbouring tile's lane (B^T is
+    // linear, so transforming before the exchange skips the third column's bt6)
+    float act[2][3][6];
+    auto act_stage = [&](const int set, const int ab) {
+      float cx[6], cy[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        float2 m = raw[set][r];
+        if constexpr (ACT != ACT_NONE) {
+          m.x = __builtin_fmaf(m.x, gnv[set].x, gnv[set].y);
+          m.y = __builtin_fmaf(m.y, gnv[set].x, gnv[set].y);
+          if constexpr (ACT == ACT_GN_SILU) {
+            m.x = m.x * __builtin_amdgcn_rcpf(1.0f + __expf(-m.x));
+            m.y = m.y * __builtin_amdgcn_rcpf(1.0f + __expf(-m.y));
+          }
+        }
+        if (r == 0 || r == 5) {
+          const float fy = r == 0 ? pad[set].x : pad[set].y;
+          m.x *= fy;
+          m.y *= fy;
+        }
+        cx[r] = m.x;
+        cy[r] = m.y;
+      }
+      bt6(cx, act[ab][0]);
+      bt6(cy, act[ab][1]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const float give = h ? act[ab][1][i] : act[ab][0][i];
+        const float nb = __int_as_float(__builtin_amdgcn_ds_bpermute(nbaddr, __float_as_int(give)));
+        act[ab][2][i] = nb * pad[set].z;
+      }
+    };
+    auto tr_stage = [&](const int ab, float* vb) {
+      float w[6][3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) w[i][c] = act[ab][c][i];
+      // rows 0-2 to the lower half (h = 0), 3-5 to the upper: the rows of 16
+      // lanes pair (0,1), (2,3) -- afterwards row[a][j] is row 3h+a of window column j
+      float row[3][6];
+#pragma unroll
+      for (int aa = 0; aa < 3; ++aa)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[aa][c]),
+                                                           __float_as_uint(w[3 + aa][c]), false, false);
+          const int jl = c == 0 ? 1 : (c == 1 ? 2 : 0);
+          row[aa][jl] = __uint_as_float(sw[0]);
+          row[aa][3 + c] = __uint_as_float(sw[1]);
+        }
+      float* o = vb + vwoff;
+#pragma unroll
+      for (int aa = 0; aa < 3; ++aa) {
+        float vv[6];
+        bt6(row[aa], vv);
+#pragma unroll
+        for (int jp = 0; jp < 6; jp += 2)
+          *reinterpret_cast<f32x2*>(o + (aa * 3 + jp / 2) * 128) = f32x2{vv[jp], vv[jp + 1]};
+      }
+    };
+    auto slot = [&](auto sa, auto ab, int g) {
+      constexpr int SA = decltype(sa)::value, AB = decltype(ab)::value;
+      tr_stage(AB ^ 1, vbuf + ((g + 1) & 1) * V_FL);
+      act_stage(SA, AB);
+      load_next(SA);
+      __syncthreads();   // (B) end of slot g
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    if (gtot > 0) {
+      set_item(0);
+      load_next(0);
+      load_next(1);
+      load_next(2);
+      act_stage(0, 0);
+      tr_stage(0, vbuf);
+      load_next(0);      // chunk 3
+      act_stage(1, 1);
+      load_next(1);      // chunk 4
+    }
+    __syncthreads();   // (A) chunk 0 staged
+    int g = 0;
+    for (; g + 5 < gtot; g += 6) {
+      slot(I2{}, I0{}, g);
+      slot(I0{}, I1{}, g + 1);
+      slot(I1{}, I0{}, g + 2);
+      slot(I2{}, I1{}, g + 3);
+      slot(I0{}, I0{}, g + 4);
+      slot(I1{}, I1{}, g + 5);
+    }
+    if (g < gtot) slot(I2{}, I0{}, g);
+    if (g + 1 < gtot) slot(I0{}, I1{}, g + 1);
+    if (g + 2 < gtot) slot(I1{}, I0{}, g + 2);
+    if (g + 3 < gtot) slot(I2{}, I1{}, g + 3);
+    if (g + 4 < gtot) slot(I0{}, I0{}, g + 4);
+    return;
+  }
+
+  // =================== MFMA waves ===================
+  const int cb = wave;                         // co block of 16
+  f32x4 acc[NX];
+  // U fragments of (co group, 4-channel k-step ks, xi pair p, co block cb):
+  // 128 floats at byte ((cog * nks + ks) * 18 + p) * 2048 + cb * 512 of wpk_wino4
+  // (launch_pack_conv_wino4's layout); lane l reads the float2 at l * 8
+  const int nks = Cin / 4;
+  const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.wpk_wino4), (short)0, (int)((size_t)NX * a.Cout * Cin * 4), 0x00020000);
+  // U cursor: the k-step whose fragments load next (clamped at the last one)
+  int u_il = 0, u_ks = 0;
+  int u_base = 0;                              // byte offset of (cog, ks = 0) of item u_il
+  auto u_item = [&](int il) {
+    const Item itm = item_of(bid + il * G, ncog);
+    u_base = itm.cog * nks * 36864;
+  };
+  auto u_advance = [&]() {
+    if (++u_ks == nks) {
+      if (u_il + 1 < nloc) {
+        u_ks = 0;
+        u_item(++u_il);
+      } else {
+        u_ks = nks - 1;                        // past the end: re-load the last k-step
+      }
+    }
+  };
+  if (nloc > 0) u_item(0);
+  f32x2 ub[2][18];
+  const int uvoff = lane * 8 + cb * 512;
+  auto u_load = [&](f32x2 (&u)[18], const int p) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(ru, uvoff, u_base + u_ks * 36864 + p * 2048, 0);
+    u[p] = f32x2{__uint_as_float(v[0]), __uint_as_float(v[1])};
+  };
+  if (nloc > 0) {
+#pragma unroll
+    for (int p = 0; p < 18; ++p) u_load(ub[0], p);
+    u_advance();
+  }
+  __syncthreads();   // (A)
+  // one k-step: 36 MFMAs on V (LDS) and U (registers u), the next k-step's U
+  // fragments loaded into nx, one per xi pair
+  auto kstep = [&](const f32x2 (&u)[18], f32x2 (&nx)[18], const float* vs) {
+    constexpr int PD = WINO4S_PD;
+    f32x2 rb[PD + 1];
+#pragma unroll
+    for (int p = 0; p < PD; ++p) rb[p] = *reinterpret_cast<const f32x2*>(vs + p * 128);
+#pragma unroll
+    for (int p = 0; p < 18; ++p) {
+      if (p + PD < 18) rb[(p + PD) % (PD + 1)] = *reinterpret_cast<const f32x2*>(vs + (p + PD) * 128);
+      const int r = p % (PD + 1);
+      acc[2 * p] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[p].x, rb[r].x, acc[2 * p], 0, 0, 0);
+      acc[2 * p + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[p].y, rb[r].y, acc[2 * p + 1], 0, 0, 0);
+      u_load(nx, p);
+      if (p + PD < 18) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                      // MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                      // VMEM read
+    }
+    u_advance();
+  };
+  for (int il = 0; il < nloc; ++il) {
+#pragma unroll
+    for (int x = 0; x < NX; ++x) acc[x] = f32x4{};
+    for (int k = 0; k < nchunk; ++k) {
+      const int g = il * nchunk + k;
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      const float* vb = vbuf + (g & 1) * V_FL + ln * 2;
+      kstep(ub[0], ub[1], vb);
+      kstep(ub[1], ub[0], vb + VKS);
+#pragma unroll
+      for (int x = 0; x < NX; ++x) asm volatile("" : "+v"(acc[x]));
+      __syncthreads();   // (B)
+    }
+
+    // ---- output transform: lane l holds M[xi] of co = 16 cb + 4 (l >> 4) + i, tile l & 15
+    const Item itm = item_of(bid + il * G, ncog);
+    const int flatw = itm.blk * 16;
+    const int smpl = flatw / TS;
+    const bool has_eb = a.ebias != nullptr, has_res = a.res != nullptr, has_bias = a.bias != nullptr;
+    const unsigned smp = (unsigned)(a.Cout * HW * 4);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (size_t)smpl * a.Cout * HW, (short)0, smp, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        has_res ? const_cast<float*>(a.res) + (size_t)smpl * a.Cout * HW : nullptr, (short)0, smp,
+        0x00020000);
+    f32x4 y[4][4];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      f32x2 P[6][4];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        f32x2 m[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) m[j] = f32x2{acc[6 * i + j][2 * pp], acc[6 * i + j][2 * pp + 1]};
+        at6(m, P[i]);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        f32x2 col[6], yc[4];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) col[i] = P[i][x];
+        at6(col, yc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          y[2 * pp][r][x] = yc[r].x;
+          y[2 * pp + 1][r][x] = yc[r].y;
+        }
+      }
+    }
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const int co0 = itm.cog * 64 + cb * 16 + 4 * (ln >> 4);
+    const int tg = flatw % TS + (ln & 15);
+    const int ty = tg / TPR, tx = tg - ty * TPR;
+    const int vo = (co0 * HW + 4 * ty * WO + 4 * tx) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float bi = has_bias ? a.bias[co0 + i] : 0.f;
+      const float ei = has_eb ? a.ebias[(size_t)smpl * a.eb_stride + co0 + i] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        y[i][r] = y[i][r] + bi;
+        if (has_eb) y[i][r] = y[i][r] + ei;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_res) {
+      f32x4 rv[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          rv[i][r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, vo, i * HW * 4 + r * WO * 4, 0));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[i][r] = y[i][r] + rv[i][r];
+    }
+    if (a.gnp) {
+      float2 pr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sm = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm += (y[i][r][0] + y[i][r][1]) + (y[i][r][2] + y[i][r][3]);
+        sm = row16_sum(sm);
+        const float mu = sm * (1.0f / 256.0f);
+        float qq = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const float d = y[i][r][x] - mu;
+            qq = __builtin_fmaf(d, d, qq);
+          }
+        pr[i] = make_float2(sm, row16_sum(qq));
+      }
+      if ((ln & 15) == 0) {
+        const int np = TS / 16, part = (flatw % TS) / 16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.gnp[((size_t)smpl * a.Cout + co0 + i) * np + part] = pr[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
+                                               i * HW * 4 + r * WO * 4, 0);
+  }
+}
+
+template <int WO, int ACT, bool UP>
+hipError_t launch_wo4s(const ConvArgs& a, int B, hipStream_t s, int cus) {
+  static std::atomic<unsigned long long> attr{0};
+  set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP>, (int)WLDS, attr);
+  const int nitems = wino4s_items(a.Cout, WO, B);
+  const int grid = nitems < cus ? nitems : cus;
+  conv_wino4s_kernel<WO, ACT, UP><<<grid, WT, WLDS, s>>>(a, nitems);
+  return hipGetLastError();
+}
+
+template <int ACT>
+hipError_t launch_act4s(const ConvArgs& a, int B, hipStream_t s, int cus) {
+  switch (a.Wo) {
+    case 16: return launch_wo4s<16, ACT, false>(a, B, s, cus);
+    case 32: return launch_wo4s<32, ACT, false>(a, B, s, cus);
+    case 64: return launch_wo4s<64, ACT, false>(a, B, s, cus);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+int wino4s_items(int cout, int wo, int B) { return (wo / 4) * (wo / 4) / 16 * B * (cout / 64); }
+
+// ERTD_WINO4S_UP=0 keeps the sub-pixel direct kernel for the Upsample convs (A/B)
+bool wino4s_up_ok(int cin, int ca, int cout, int wo, int B) {
+  static const int env = [] {
+    const char* e = getenv("ERTD_WINO4S_UP");
+    return e ? atoi(e) : 1;
+  }();
+  return env != 0 && wino4s_ok(cin, ca, cout, wo, B) && (wo == 16 || wo == 32 || wo == 64);
+}
+
+hipError_t launch_conv_wino4s(int act, const ConvArgs& a, int B, hipStream_t s, int cus) {
+  if (a.Cin % CCH || a.Ca % 2 || a.Cout % 64 || !a.wpk_wino4 || a.Ho != a.Wo || a.Hs != a.Ws)
+    return hipErrorInvalidValue;
+  if (a.Hs * 2 == a.Wo) {   // Upsample conv (no activation)
+    if (act != ACT_NONE) return hipErrorInvalidValue;
+    switch (a.Wo) {
+      case 16: return launch_wo4s<16, ACT_NONE, true>(a, B, s, cus);
+      case 32: return launch_wo4s<32, ACT_NONE, true>(a, B, s, cus);
+      case 64: return launch_wo4s<64, ACT_NONE, true>(a, B, s, cus);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (a.Hs != a.Wo) return hipErrorInvalidValue;
+  switch (act) {
+    case ACT_NONE: return launch_act4s<ACT_NONE>(a, B, s, cus);
+    case ACT_GN_SILU: return launch_act4s<ACT_GN_SILU>(a, B, s, cus);
+    case ACT_GN: return launch_act4s<ACT_GN>(a, B, s, cus);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace unet
+}  // namespace ertd

@@ -241,11 +241,12 @@ def test_conv2d_workspace_covers_launch_scratch():
     pre-transformed input image (caller-owned, include/ertdiff.h)."""
     lib = _lib.load()
     fp32, bf16 = _lib.PREC_FP32, _lib.PREC_BF16
-    # 128 -> 128 at 32x32, B = 32: 128 tile items < 256 CUs -> K split
-    small = lib.ertd_conv2d_workspace_bytes(128, 128, 3, fp32, 64, 32, 0)
-    split = lib.ertd_conv2d_workspace_bytes(128, 128, 3, fp32, 32, 32, 0)
-    assert split >= 32 * 128 * 32 * 32 * 4
-    assert split > small - 64 * 128 * 32 * 32 * 4     # the B = 64 layer needs no split buffer
+    # 256 -> 256 at 16x16, B = 32: 128 F(2x2) tile items < 256 CUs -> K split (at
+    # B = 64 the F(4x4) register-weight kernel has 256 items and no split)
+    small = lib.ertd_conv2d_workspace_bytes(256, 256, 3, fp32, 64, 16, 0)
+    split = lib.ertd_conv2d_workspace_bytes(256, 256, 3, fp32, 32, 16, 0)
+    assert split >= 32 * 256 * 16 * 16 * 4
+    assert split > small - 64 * 256 * 16 * 16 * 4     # the B = 64 layer needs no split buffer
     # bf16 3x3 stride-1 conv: the [B][C/16][H][W][16] bf16 image (C*H*W*2 bytes per sample)
     img = lib.ertd_conv2d_workspace_bytes(64, 64, 3, bf16, 8, 64, 0)
     assert img >= 8 * 64 * 64 * 64 * 2

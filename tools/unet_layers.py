@@ -57,7 +57,8 @@ def walk():
 
 
 layers = walk()
-KEYS = ("conv_kernel<", "conv_out_kernel<", "conv_in_kernel<", "conv_wino_kernel<", "conv_wino4_kernel<", "conv_bf16_kernel<")
+KEYS = ("conv_kernel<", "conv_out_kernel<", "conv_in_kernel<", "conv_wino_kernel<", "conv_wino4_kernel<", "conv_wino4s_kernel<",
+        "conv_bf16_kernel<")
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if any(k in r["Kernel_Name"] for k in KEYS)]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 last = rows[-len(layers):]
@@ -75,6 +76,9 @@ for (n, cin, cout, ks, wo), r in zip(layers, last):
     if "conv_wino4_kernel<" in r["Kernel_Name"]:  # Winograd F(4x4,3x3): 36 of 144 multiplies
         fl = fl // 4
         n = n + "W"
+    if "conv_wino4s_kernel<" in r["Kernel_Name"]:  # F(4x4,3x3), register-weight schedule
+        fl = fl // 4
+        n = n + "S"
     tot_t += us
     tot_f += fl
     peak = 2500.0 if "conv_bf16_kernel<" in r["Kernel_Name"] else 157.3   # dense bf16 / fp32 MFMA peak
@@ -83,5 +87,5 @@ for (n, cin, cout, ks, wo), r in zip(layers, last):
     print(f"{n:14s} {cin:4d}->{cout:4d} k{ks} {wo:3d}  {tmpl:22s} wg {wgs:5d}  {us:8.1f} us  "
           f"{fl / us / 1e6:7.1f} TF  {fl / us / 1e6 / peak * 100:5.1f}%  (alg {alg / us / 1e6:6.1f} TF)")
 print(f"total {tot_t:.0f} us, {tot_f / tot_t / 1e6:.1f} TF (executed FLOP; * = sub-pixel Upsample, "
-      f"4 of 9 taps; w = Winograd F(2x2,3x3), 16 of 36 multiplies; W = F(4x4,3x3), 36 of 144; "
+      f"4 of 9 taps; w = Winograd F(2x2,3x3), 16 of 36 multiplies; W = F(4x4,3x3), 36 of 144; S = the same, register-weight schedule; "
       f"% of the fp32 peak, of the bf16 peak for bf16 kernels)")
