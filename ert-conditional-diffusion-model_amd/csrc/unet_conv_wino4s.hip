@@ -46,6 +46,13 @@ constexpr int NRS = 3;                        // producer register sets
 #ifndef WINO4S_PD
 #define WINO4S_PD 2                           // V operand read-ahead (xi pairs)
 #endif
+// Ablations for a diagnostic build only (tools/build_variant.sh ... -DWINO4S_ABL=n;
+// results WRONG, never in the shipped library): bit 0 the producers skip the
+// activation and transform, bit 1 every U load reads the first k-step (L2-hot),
+// bit 2 the MFMAs become one VALU fma, bit 3 the output transform / stores are skipped
+#ifndef WINO4S_ABL
+#define WINO4S_ABL 0
+#endif
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x2 = __attribute__((ext_vector_type(2))) float;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
@@ -248,8 +255,10 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
     };
     auto slot = [&](auto sa, auto ab, int g) {
       constexpr int SA = decltype(sa)::value, AB = decltype(ab)::value;
-      tr_stage(AB ^ 1, vbuf + ((g + 1) & 1) * V_FL);
-      act_stage(SA, AB);
+      if constexpr (!(WINO4S_ABL & 1)) {
+        tr_stage(AB ^ 1, vbuf + ((g + 1) & 1) * V_FL);
+        act_stage(SA, AB);
+      }
       load_next(SA);
       __syncthreads();   // (B) end of slot g
     };
@@ -315,7 +324,8 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
   f32x2 ub[2][18];
   const int uvoff = lane * 8 + cb * 512;
   auto u_load = [&](f32x2 (&u)[18], const int p) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(ru, uvoff, u_base + u_ks * 36864 + p * 2048, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+        ru, uvoff, (WINO4S_ABL & 2) ? p * 2048 : u_base + u_ks * 36864 + p * 2048, 0);
     u[p] = f32x2{__uint_as_float(v[0]), __uint_as_float(v[1])};
   };
   if (nloc > 0) {
@@ -335,8 +345,13 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
     for (int p = 0; p < 18; ++p) {
       if (p + PD < 18) rb[(p + PD) % (PD + 1)] = *reinterpret_cast<const f32x2*>(vs + (p + PD) * 128);
       const int r = p % (PD + 1);
-      acc[2 * p] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[p].x, rb[r].x, acc[2 * p], 0, 0, 0);
-      acc[2 * p + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[p].y, rb[r].y, acc[2 * p + 1], 0, 0, 0);
+      if constexpr (WINO4S_ABL & 4) {
+        acc[2 * p][0] = __builtin_fmaf(u[p].x, rb[r].x, acc[2 * p][0]);
+        acc[2 * p + 1][0] = __builtin_fmaf(u[p].y, rb[r].y, acc[2 * p + 1][0]);
+      } else {
+        acc[2 * p] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[p].x, rb[r].x, acc[2 * p], 0, 0, 0);
+        acc[2 * p + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[p].y, rb[r].y, acc[2 * p + 1], 0, 0, 0);
+      }
       u_load(nx, p);
       if (p + PD < 18) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                      // MFMAs
@@ -359,6 +374,14 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
       __syncthreads();   // (B)
     }
 
+    if constexpr ((WINO4S_ABL & 8) != 0) {
+      if (il == nloc - 1) {
+        float sacc = 0.f;
+        for (int x = 0; x < NX; ++x) sacc += acc[x][0] + acc[x][3];
+        a.out[(size_t)bid * 64 + lane] = sacc;
+      }
+      continue;
+    }
     // ---- output transform: lane l holds M[xi] of co = 16 cb + 4 (l >> 4) + i, tile l & 15
     const Item itm = item_of(bid + il * G, ncog);
     const int flatw = itm.blk * 16;
