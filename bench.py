@@ -359,17 +359,17 @@ def bench_hbm_kernels(dev, reps=50):
 # The U-Net's conv kernels at the headline's shapes (U2, B = 64): (kernel, layer,
 # Ca, Cb, Cout, H (source), ks, mode, act, emb, residual, executed / direct FLOP)
 CONV_KERNEL_CASES = [
-    ("conv_wino4_kernel", "d0r0.conv1 64->64 @64x64, GN+SiLU, +emb", 64, 0, 64, 64, 3, 0, 1, True, False, 1 / 4),
-    ("conv_wino4_kernel", "d0r0.conv2 64->64 @64x64, GN+SiLU, +residual", 64, 0, 64, 64, 3, 0, 1, False, True,
+    ("conv_wino4s_kernel", "d0r0.conv1 64->64 @64x64, GN+SiLU, +emb", 64, 0, 64, 64, 3, 0, 1, True, False, 1 / 4),
+    ("conv_wino4s_kernel", "d0r0.conv2 64->64 @64x64, GN+SiLU, +residual", 64, 0, 64, 64, 3, 0, 1, False, True,
      1 / 4),
-    ("conv_wino4_kernel", "u1r0.conv1 256+128->128 @32x32 (skip concat), GN+SiLU, +emb", 256, 128, 128, 32, 3,
+    ("conv_wino4s_kernel", "u1r0.conv1 256+128->128 @32x32 (skip concat), GN+SiLU, +emb", 256, 128, 128, 32, 3,
      0, 1, True, False, 1 / 4),
-    ("conv_wino_kernel", "mid1.conv1 256->256 @16x16 F(2x2), GN+SiLU, +emb", 256, 0, 256, 16, 3, 0, 1, True,
-     False, 4 / 9),
+    ("conv_wino4s_kernel", "mid1.conv1 256->256 @16x16, GN+SiLU, +emb", 256, 0, 256, 16, 3, 0, 1, True,
+     False, 1 / 4),
     ("conv_kernel<3,MODE_S2>", "d0.down 64->64 64x64 -> 32x32 (stride 2)", 64, 0, 64, 64, 3, 1, 0, False, False,
      1.0),
-    ("conv_kernel<2,MODE_UPP>", "u1.up 128->128 32x32 -> 64x64 (sub-pixel Upsample)", 128, 0, 128, 32, 3, 2, 0,
-     False, False, 4 / 9),
+    ("conv_wino4s_kernel<UP>", "u1.up 128->128 32x32 -> 64x64 (Upsample: F(4x4) on the nearest-x2 source)", 128, 0,
+     128, 32, 3, 2, 0, False, False, 1 / 4),
     ("conv_kernel<1>", "u0r0.skip 128+64->64 @64x64 (1x1, concat)", 128, 64, 64, 64, 1, 0, 0, False, False, 1.0),
     ("conv_in_kernel", "conv_in 1->64 @64x64", 1, 0, 64, 64, 3, 0, 0, False, False, 1.0),
     ("conv_out_kernel", "conv_out 64->1 @64x64, GN+SiLU", 64, 0, 1, 64, 3, 0, 1, False, False, 1.0),
@@ -877,7 +877,7 @@ def main():
     B, T = a.batch, a.T
     from ertdiff.unet import CONFIGS, unet_flops
     spec = CONFIGS[a.unet]
-    flops = unet_flops(**spec)
+    flops = unet_flops(**spec, batch=B)
     model = ertdiff.ConditionalUNet.from_config(a.unet, seed=0).to(dev).eval()
     g = torch.Generator(device=dev).manual_seed(1042)
     cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
@@ -892,14 +892,14 @@ def main():
     traffic = _traffic(f"unet_{a.unet}_B{B}_fp32_step")
     ex_flop_step = flops["conv_executed_fp32"] * B
     ex_tf = ex_flop_step / (ev_s / a.steps) / 1e12
-    roof = {"kernel": "conv_wino4_kernel (ResBlock 3x3 at 64x64 / 32x32, Winograd F(4x4,3x3)) + "
-                      "conv_wino_kernel (16x16, F(2x2,3x3)) + conv_kernel (the other convs): all "
+    roof = {"kernel": "conv_wino4s_kernel (every ResBlock 3x3 and both Upsample convs, Winograd "
+                      "F(4x4,3x3)) + conv_kernel (1x1 skips, stride-2) + conv_in / conv_out: all "
                       "convs of one U-Net step",
             "bound": "mfma", "achieved": round(ex_tf, 3), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-            "flop_basis": "EXECUTED MFMA FLOP of one step (F(4x4) Winograd layers at 36/144, "
-                          "F(2x2) at 16/36, sub-pixel Upsample at 4/9 of the direct count) / the "
-                          "step's duration",
+            "flop_basis": "EXECUTED MFMA FLOP of one step (F(4x4) Winograd layers at 36/144 of the "
+                          "direct count, F(2x2) at 16/36, sub-pixel Upsample at 4/9: "
+                          "ertdiff.unet.unet_flops(batch=B)) / the step's duration",
             "executed_flop_per_step": ex_flop_step,
             "avg_us_per_step": round(ev_s / a.steps * 1e6, 1),
             "timing": f"HIP events on the launching stream around {a.steps} replayed step graphs "
@@ -928,8 +928,10 @@ def main():
         ck = bench_conv_kernels(dev)
         extra["conv_kernels"] = ck
         dom = ck["d0r0.conv1 64->64 @64x64, GN+SiLU, +emb"]
-        roof["dominant"] = {"kernel": "conv_wino4_kernel (Winograd F(4x4,3x3), 18 of the 52 convs, 1.9 of "
-                                      "4.8 ms of conv time per step)",
+        roof["dominant"] = {"kernel": "conv_wino4s_kernel (Winograd F(4x4,3x3), register-resident weights: "
+                                      "36 of the 51 convs -- every ResBlock 3x3 and both Upsample convs -- "
+                                      "3.4 of 4.2 ms of serialized conv time per step, "
+                                      "profiles/r03_unet_layers.txt)",
                             "layer": "d0r0.conv1 64->64 @64x64, B=64, GN+SiLU prologue, +emb epilogue",
                             "achieved": dom["executed_tflops"], "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                             "frac": dom["mfma_frac"], "avg_us": dom["avg_us"],

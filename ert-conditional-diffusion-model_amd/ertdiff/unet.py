@@ -74,13 +74,15 @@ def param_layout(cfg: ErtdUnetConfig) -> List[Tuple[str, Tuple[int, ...]]]:
 
 
 def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, attn=False,
-               groups=32) -> Dict[str, int]:
+               groups=32, batch: Optional[int] = None, cus: int = 256) -> Dict[str, int]:
     """Algorithmic FLOP per sample-step (multiply-add = 2) of the U-Net forward:
     convs, attention core (QK^T and PV) and the dense layers; elementwise work
-    (GroupNorm, SiLU, adds) is not counted."""
+    (GroupNorm, SiLU, adds) is not counted.  `conv_executed_fp32` is the MFMA
+    work the fp32 kernels execute at batch `batch` on `cus` CUs (the 16x16
+    level's kernel depends on the batch; None = the F(2x2) count there)."""
     cfg = make_config(image, ch, ch_mult, num_res, attn, groups)
     layout = param_layout(cfg)
-    conv = dense = ups = wino = wino4 = 0
+    conv = dense = ups = ups4 = wino = wino4 = 0
     # spatial size per conv: walk the layout names
     res_of = {}
     r = image
@@ -92,6 +94,10 @@ def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, a
     res_of["mid"] = r
     for i in reversed(range(nl)):
         res_of[f"up.{i}"] = image >> i
+
+    def f4_items_fill(hw, cout):   # csrc/unet_conv_wino.hip wino4s_ok at W = 16
+        return batch is not None and (hw // 4) ** 2 // 16 * batch * (cout // 64) >= cus
+
     for name, shape in layout:
         if not name.endswith(".weight") or name.startswith("condition_encoder"):
             continue
@@ -110,13 +116,19 @@ def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, a
             f = 2 * shape[0] * shape[1] * shape[2] * shape[3] * hw * hw
             conv += f
             if len(parts) > 2 and parts[2] == "upsample":
-                ups += f
+                # F(4x4) on the nearest-x2 source (unet_conv_wino4s.hip, UP) where
+                # wino4s_up_ok, else 4 sub-pixel 2x2 convs (4 of the 9 taps)
+                if shape[1] % 8 == 0 and shape[0] % 64 == 0 and hw in (32, 64) or \
+                        (hw == 16 and shape[1] % 8 == 0 and shape[0] % 64 == 0 and f4_items_fill(hw, shape[0])):
+                    ups4 += f
+                else:
+                    ups += f
             # ResBlock 3x3 convs the fp32 Winograd kernels take: F(4x4,3x3) at
-            # W >= 32 (csrc/unet_conv_wino4.hip: Cin % 4 == 0, Cout % 64 == 0),
-            # F(2x2,3x3) at W = 16 (unet_conv_wino.hip: Cin % 8 == 0; F(4x4) there
-            # only for batches whose tile items fill the CUs, not counted here)
+            # W >= 32 (unet_conv_wino4s.hip / unet_conv_wino4.hip) and at W = 16
+            # where its tile items fill the CUs, else F(2x2,3x3) (unet_conv_wino.hip)
             if parts[-2] in ("conv1", "conv2") and shape[2] == 3 and shape[0] % 64 == 0:
-                if hw >= 32 and shape[1] % 4 == 0:
+                if (hw >= 32 and shape[1] % 4 == 0) or (hw == 16 and shape[1] % 8 == 0 and
+                                                        f4_items_fill(hw, shape[0])):
                     wino4 += f
                 elif shape[1] % 8 == 0:
                     wino += f
@@ -128,15 +140,13 @@ def unet_flops(image=64, ch=64, ch_mult: Sequence[int] = (1, 2, 4), num_res=2, a
         N = res_of["mid"] ** 2
         attn_f = 2 * 2 * N * N * C
     enc = 6_308_736 + 14_426_112 + 2 * 64 * 128   # the reference's condition encoder
-    # the fp32 kernels run each Upsample conv as 4 sub-pixel 2x2 convs (4 of
-    # the 9 counted taps per output pixel) and the ResBlock 3x3 convs by
-    # Winograd F(4x4,3x3) (36 multiplies per 4x4 outputs instead of 144) or
-    # F(2x2,3x3) (16 per 2x2 instead of 36): the MFMA work actually executed
+    # executed MFMA work: F(4x4,3x3) 36 multiplies per 4x4 outputs instead of
+    # 144, F(2x2,3x3) 16 per 2x2 instead of 36, sub-pixel Upsample 4 of 9 taps
     return {"conv": conv, "attention": attn_f, "dense": dense, "condition_encoder": enc,
             "total": conv + attn_f + dense + enc,
-            "conv_winograd": wino + wino4,
-            "conv_winograd_f4": wino4,
-            "conv_executed_fp32": conv - ups * 5 // 9 - wino * 5 // 9 - wino4 * 3 // 4}
+            "conv_winograd": wino + wino4 + ups4,
+            "conv_winograd_f4": wino4 + ups4,
+            "conv_executed_fp32": conv - ups * 5 // 9 - wino * 5 // 9 - (wino4 + ups4) * 3 // 4}
 
 
 class ConditionalUNet(nn.Module):
