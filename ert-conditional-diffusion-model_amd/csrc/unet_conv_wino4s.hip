@@ -49,7 +49,8 @@ constexpr int NRS = 3;                        // producer register sets
 // Ablations for a diagnostic build only (tools/build_variant.sh ... -DWINO4S_ABL=n;
 // results WRONG, never in the shipped library): bit 0 the producers skip the
 // activation and transform, bit 1 every U load reads the first k-step (L2-hot),
-// bit 2 the MFMAs become one VALU fma, bit 3 the output transform / stores are skipped
+// bit 2 the MFMAs become one VALU fma, bit 3 the output transform / stores are skipped,
+// bit 4 no per-chunk barrier (either role), bit 5 the MFMA waves issue no U loads
 #ifndef WINO4S_ABL
 #define WINO4S_ABL 0
 #endif
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
         act_stage(SA, AB);
       }
       load_next(SA);
-      __syncthreads();   // (B) end of slot g
+      if constexpr (!(WINO4S_ABL & 16)) __syncthreads();   // (B) end of slot g
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -324,6 +325,10 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
   f32x2 ub[2][18];
   const int uvoff = lane * 8 + cb * 512;
   auto u_load = [&](f32x2 (&u)[18], const int p) {
+    if constexpr ((WINO4S_ABL & 32) != 0) {
+      u[p] = u[p] + f32x2{1.f, 1.f};
+      return;
+    }
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(
         ru, uvoff, (WINO4S_ABL & 2) ? p * 2048 : u_base + u_ks * 36864 + p * 2048, 0);
     u[p] = f32x2{__uint_as_float(v[0]), __uint_as_float(v[1])};
@@ -334,6 +339,9 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
     u_advance();
   }
   __syncthreads();   // (A)
+#ifndef WINO4S_XK
+#define WINO4S_XK 1                           // V read-ahead continues across the chunk's two k-steps
+#endif
   // one k-step: 36 MFMAs on V (LDS) and U (registers u), the next k-step's U
   // fragments loaded into nx, one per xi pair
   auto kstep = [&](const f32x2 (&u)[18], f32x2 (&nx)[18], const float* vs) {
@@ -359,6 +367,30 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
     }
     u_advance();
   };
+  // a whole chunk (both k-steps) as one stream: the V operand reads run PD xi
+  // pairs ahead across the k-step boundary too
+  auto chunk2 = [&](const float* vs) {
+    constexpr int PD = WINO4S_PD;
+    f32x2 rb[PD + 1];
+#pragma unroll
+    for (int q = 0; q < PD; ++q) rb[q] = *reinterpret_cast<const f32x2*>(vs + q * 128);
+#pragma unroll
+    for (int q = 0; q < 36; ++q) {
+      const int st = q / 18, p = q % 18;
+      const int qn = q + PD;
+      if (qn < 36) rb[qn % (PD + 1)] = *reinterpret_cast<const f32x2*>(vs + (qn / 18) * VKS + (qn % 18) * 128);
+      const int r = q % (PD + 1);
+      const f32x2 u = st == 0 ? ub[0][p] : ub[1][p];
+      acc[2 * p] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.x, rb[r].x, acc[2 * p], 0, 0, 0);
+      acc[2 * p + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.y, rb[r].y, acc[2 * p + 1], 0, 0, 0);
+      if (st == 0) u_load(ub[1], p);
+      else u_load(ub[0], p);
+      if (qn < 36) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                  // MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                  // VMEM read
+      if (p == 17) u_advance();
+    }
+  };
   for (int il = 0; il < nloc; ++il) {
 #pragma unroll
     for (int x = 0; x < NX; ++x) acc[x] = f32x4{};
@@ -367,11 +399,15 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
       int ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
       const float* vb = vbuf + (g & 1) * V_FL + ln * 2;
-      kstep(ub[0], ub[1], vb);
-      kstep(ub[1], ub[0], vb + VKS);
+      if constexpr (WINO4S_XK && !(WINO4S_ABL & 4)) {
+        chunk2(vb);
+      } else {
+        kstep(ub[0], ub[1], vb);
+        kstep(ub[1], ub[0], vb + VKS);
+      }
 #pragma unroll
       for (int x = 0; x < NX; ++x) asm volatile("" : "+v"(acc[x]));
-      __syncthreads();   // (B)
+      if constexpr (!(WINO4S_ABL & 16)) __syncthreads();   // (B)
     }
 
     if constexpr ((WINO4S_ABL & 8) != 0) {

@@ -1,13 +1,13 @@
 #!/bin/bash
 # conv_wino4s_kernel chunk-cost breakdown (diagnostic): the ablation builds
-# variants/abl<n>.so (tools/build_variant.sh unet_conv_wino4s -DWINO4S_ABL=<n>)
+# variants/*.so (e.g. tools/build_variant.sh unet_conv_wino4s -DWINO4S_ABL=<n> variants/abl<n>.so)
 # of one layer under rocprofv3 --kernel-trace, per layer shape; prints the conv
 # kernel's average per variant ("base" = the shipped library).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 for shape in ${SHAPES:-"64 64 64" "256 256 16" "512 256 16" "128 128 32"}; do
   set -- $shape
-  for lib in base $(ls variants/abl*.so 2>/dev/null); do
+  for lib in base $(ls variants/*.so 2>/dev/null); do
     tag=$(basename $lib .so); d=gpurun_out/abl_${tag}_$1_$2_$3; rm -rf "$d"
     if [ "$lib" = base ]; then unset ERTD_LIB_PATH; else export ERTD_LIB_PATH=$PWD/$lib; fi
     timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$d" -o run \
