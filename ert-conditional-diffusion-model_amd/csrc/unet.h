@@ -143,6 +143,10 @@ hipError_t launch_add_inplace(float* out, const float* part, size_t n, hipStream
 // conv's weight W'[co][ci] = W[ci][co] spatially flipped (training)
 hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, hipStream_t s,
                                  bool flipT = false);
+// fp32 1x1 conv without activation / emb / residual (the ResBlock skips;
+// unet_conv1x1.hip): per-sample GEMM, weights and input by LDS-DMA
+bool conv1x1_ok(const ConvArgs& a, int act, int B);
+hipError_t launch_conv1x1(const ConvArgs& a, int B, hipStream_t s);
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s,

@@ -170,6 +170,11 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnPartArgs a, int B) {
     if (!inB) return pa[k];                       // channel-major items are contiguous
     return pb[k - itemsA];
   };
+  // gamma / beta of the lane's channel loaded first (cpg <= 64 in every U-Net
+  // config; wider groups re-read them below): no memory round trip after the
+  // two reductions
+  const float gam = lane < cpg ? a.gamma[c0 + lane] : 0.f;
+  const float bet = lane < cpg ? a.beta[c0 + lane] : 0.f;
   // at most 4 items per lane held in registers (groups up to 256 items)
   float2 it[4];
   bool ib[4];
@@ -210,8 +215,8 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnPartArgs a, int B) {
   if (a.mr && lane == 0) a.mr[(size_t)b * a.groups + g] = make_float2((float)mean, rstd);
   for (int cl = lane; cl < cpg; cl += 64) {
     const int c = c0 + cl;
-    const float scale = rstd * a.gamma[c];
-    const float shift = -scale * (float)mean + a.beta[c];
+    const float scale = rstd * (cl < 64 ? gam : a.gamma[c]);
+    const float shift = -scale * (float)mean + (cl < 64 ? bet : a.beta[c]);
     a.out[(size_t)b * C + c] = make_float2(scale, shift);
   }
 }

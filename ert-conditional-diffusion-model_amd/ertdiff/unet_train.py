@@ -424,17 +424,20 @@ class _Grads:
             self.k.chan_copy(dx, c0, cd, buf, 0, accumulate=acc)
 
 
-def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, gn=None, act=0):
+def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, gn=None, act=0,
+                   bias_grad=True):
     """Gradients of y = conv(act(cat(xa, xb))) + bias: weight and bias grads into
-    grads[name.weight / .bias]; returns dL/d act(cat(xa, xb)) (or None)."""
+    grads[name.weight / .bias] (bias_grad=False: the caller supplies the bias
+    gradient); returns dL/d act(cat(xa, xb)) (or None)."""
     Cout, Cin, ks, _ = w.shape
     dW = k.empty(Cout, Cin, ks, ks)
     if not k.conv_wgrad(dy, xa, xb, ks, mode, dW, gn, act):
         k.wgrad_im2col(dy, xa, xb, ks, mode, dW, gn, act)
     grads[name + ".weight"] = dW
-    db = k.empty(Cout)
-    k.chan_sums(dy, out_c=db)
-    grads[name + ".bias"] = db
+    if bias_grad:
+        db = k.empty(Cout)
+        k.chan_sums(dy, out_c=db)
+        grads[name + ".bias"] = db
     if not x_needs_grad:
         return None
     # input gradient: a conv of dY with the flipped, transposed weights
@@ -661,8 +664,11 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                 # h = conv1(a1) + b1 + emb(ea): the emb grad is dh summed over pixels
                 cout = h.shape[1]
                 k.chan_sums(dh, out_bc=deb_all[:, eoff[n]:eoff[n] + cout])
+                # conv1's bias gradient sum_{b,p} dh equals the emb bias gradient
+                # sum_b deb[b] (the same per-sample sums, reduced by the same
+                # fixed-order kernel): taken from the emb backward below
                 da1 = _conv_backward(k, grads, n + ".conv1", W[n + ".conv1.weight"], xa, xb,
-                                     dh, MODE_S1, gn=d["ss1"], act=ACT_GN_SILU)
+                                     dh, MODE_S1, gn=d["ss1"], act=ACT_GN_SILU, bias_grad=False)
                 dxa, acc_a = G.target(xa)
                 dxb, acc_b = (None, acc_a) if xb is None else G.target(xb)
                 if acc_a != acc_b:     # one accumulate flag per launch: pre-zero the new one
@@ -679,6 +685,7 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
         for n in tape["blocks"]:
             o, c = eoff[n], W[n + ".emb.weight"].shape[0]
             grads[n + ".emb.weight"], grads[n + ".emb.bias"] = dw_all[o:o + c], db_all[o:o + c]
+            grads[n + ".conv1.bias"] = db_all[o:o + c]
         # ---- embedding path: ea = silu(emb), emb = time MLP + cond_proj(cond_emb)
         d_emb = k.elt(ELT_SILU_BWD, tape["emb"], d_ea)
         w = W["time_embed.2.weight"]

@@ -118,6 +118,21 @@ def test_conv2d_headline_variants(Cin, Cout, H, B, cuda_dev):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("B", [2, 64])
+def test_conv2d_1x1_skip_kernel(B, cuda_dev):
+    """The 1x1 skip conv kernel (unet_conv1x1.hip: LDS-DMA'd input and gathered
+    weight slices, 256-px items at B=2, 512-px items at the headline's B=64) on
+    U2's u0r0.skip shape: 128 + 64 (concatenated) -> 64 at 64x64, with bias."""
+    Ca, Cb, Cout, H = 128, 64, 64, 64
+    x, x2 = _rand((B, Ca, H, H), 60), _rand((B, Cb, H, H), 61)
+    w, b = _rand((Cout, Ca + Cb, 1, 1), 62, 1.0 / np.sqrt(Ca + Cb)), _rand((Cout,), 63, 0.1)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev), x2=x2.to(cuda_dev)).cpu()
+    ref = F.conv2d(torch.cat([x, x2], 1), w, b)
+    err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
+    record_error(f"conv2d_1x1_skip_B{B}", err)
+    assert err < 1e-5, err
+
+
 def test_conv2d_wino4_16x16_two_sample_blocks(cuda_dev):
     """Winograd F(4x4,3x3) at 16x16 (taken only when its tile items fill the
     CUs without a K split: B=128, Cout=256 -> 256 items): a 32-tile block holds
