@@ -18,6 +18,7 @@
 // operand fetch is one ds_read_b128 (+ one b32 for a tap's left / right
 // neighbour), and the 3 taps of a kernel row share one fetch.  Wave tile:
 // 32 co x 16 ci x taps (2 x taps v_mfma_f32_16x16x4_f32 accumulators).
+#include <algorithm>
 #include <cstdlib>
 
 #include "unet.h"
@@ -381,7 +382,8 @@ extern "C" {
 size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mode) {
   Plan p;
   if (!plan_of(Cin, Cout, B, H, ks, mode, &p)) return 0;
-  return p.part_floats * sizeof(float);
+  // the Winograd path (3x3 stride 1, unet_wgrad_wino.hip) where eligible
+  return std::max(p.part_floats, wgrad_wino_ws_floats(Cin, Cout, B, H, ks, mode)) * sizeof(float);
 }
 
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
@@ -392,6 +394,13 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
     return ERTD_EINVAL;
   Plan p;
   if (!plan_of(Ca + Cb, Cout, B, H, ks, mode, &p)) return ERTD_EINVAL;
+  const size_t wf = wgrad_wino_ws_floats(Ca + Cb, Cout, B, H, ks, mode);
+  if (wf > 0) {
+    if (wf * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+    const hipError_t e = launch_wgrad_wino(dy, x, Ca, x2, Cb, B, H, Cout, gn, act, dw, accumulate,
+                                           (float*)ws, (hipStream_t)stream);
+    return e == hipSuccess ? ERTD_OK : (int)e;
+  }
   if (p.part_floats * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
   WgArgs a{dy, x, x2, Ca, Cb, Cout, H, p.Ho, p.R, (const float2*)gn, p.ntiles, p.nco, p.nsplit,
            p.cps, p.nchunks, (float*)ws};

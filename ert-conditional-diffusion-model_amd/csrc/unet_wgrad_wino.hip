@@ -1,0 +1,334 @@
+// Weight gradient of the fp32 3x3 stride-1 ResBlock convs by Winograd
+// F(4x4,3x3) -- the transpose of the forward kernels' algorithm (same points
+// {0, 1, -1, 1/2, -2, inf}, unet_conv_wino4.hip):
+//
+//   forward   y_tile = A^T [ (G g G^T) (.) (B^T d B) ] A
+//   gradient  dg     = G^T [ sum_tiles (A dy_tile A^T) (.) (B^T d B) ] G
+//
+// (d = the 6x6 window of the ACTIVATED input, zero padding after the
+// activation as in the spec; dy_tile the 4x4 output-gradient tile.)  The sum
+// over tiles is 36 GEMMs dU[xi] = D[xi] V[xi]^T with M = Cout, N = Cin,
+// K = B * tiles -- a quarter of the direct implicit GEMM's FLOP (36 per 16
+// outputs instead of 144).  Four launches:
+//   wgw_v_kernel   V[xi][ci][t] = B^T d B   (GroupNorm + SiLU on load)
+//   wgw_d_kernel   D[xi][co][t] = A dy A^T
+//   wgw_gemm_kernel  one wave per (xi, 64 co, 64 ci, K range): the operand
+//                  fragments come straight from L2 as float4s (lane l = (row
+//                  l & 15, k-quad l >> 4): four k-steps of v_mfma_f32_16x16x4_f32
+//                  per load; K order permuted identically for both operands),
+//                  4 x 4 accumulator blocks, loads two 16-k blocks ahead
+//   wgw_sum_kernel / wgw_final_kernel  fixed-order sum of the K-range partials
+//                  (one thread per (xi, co, ci)), then G^T dU G in float64 -> dW (= or +=)
+// Bitwise reproducible (no atomics).  U2 B = 32 train step 13.95 -> 13.22 ms
+// (same box); ERTD_WGRAD_WINO=0 keeps the implicit GEMM (A/B).
+#include <cstdlib>
+
+#include "unet.h"
+
+namespace ertd {
+namespace unet {
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int NX = 36;
+
+// o = B^T d (unet_conv_wino4.hip)
+__device__ __forceinline__ void bt6(const float (&d)[6], float (&o)[6]) {
+  const float c = d[4] - d[2], e = d[3] - d[1];
+  const float u = d[4] - d[1], v = d[4] + d[1];
+  o[0] = __builtin_fmaf(1.5f, e, __builtin_fmaf(-2.f, d[2], d[0] + d[4]));
+  o[1] = __builtin_fmaf(2.5f, d[3], __builtin_fmaf(0.5f, d[2], u));
+  o[2] = __builtin_fmaf(0.5f, d[3], __builtin_fmaf(-2.5f, d[2], v));
+  o[3] = __builtin_fmaf(2.f, e, c);
+  o[4] = __builtin_fmaf(-0.5f, e, c);
+  o[5] = __builtin_fmaf(1.5f, c, __builtin_fmaf(-2.f, d[3], d[1] + d[5]));
+}
+// o = A v for a 4-vector v (A = the forward's A^T transposed, 6 x 4)
+__device__ __forceinline__ void a4(const float (&v)[4], float (&o)[6]) {
+  const float s = v[0] + v[2], d = v[1] + v[3];
+  o[0] = v[0];
+  o[1] = s + d;
+  o[2] = s - d;
+  o[3] = __builtin_fmaf(0.125f, v[3], __builtin_fmaf(0.25f, v[2], __builtin_fmaf(0.5f, v[1], v[0])));
+  o[4] = __builtin_fmaf(-8.f, v[3], __builtin_fmaf(4.f, v[2], __builtin_fmaf(-2.f, v[1], v[0])));
+  o[5] = v[3];
+}
+
+struct WgwArgs {
+  const float* dy;      // (B, Cout, H, H)
+  const float* xa;      // (B, Ca, H, H)
+  const float* xb;      // (B, Cb, H, H) or null
+  int Ca, Cb, Cout, H, B;
+  const float2* gn;     // (B, Cin) {scale, shift} (ACT != NONE)
+  float* V;             // [36][Cin][T]
+  float* D;             // [36][Cout][T]
+  float* P;             // [nks][36][Cout][Cin]
+  int T, nks, kr;       // tiles (K), K ranges, K per range (multiple of 16)
+};
+
+// one thread per (channel c, tile t), t fastest (coalesced stores per xi)
+template <int ACT>
+__global__ __launch_bounds__(256) void wgw_v_kernel(WgwArgs a) {
+  const int Cin = a.Ca + a.Cb;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)a.T * Cin) return;
+  const int t = (int)(i % a.T);
+  const int c = (int)(i / a.T);
+  const int tpr = a.H / 4, ts = tpr * tpr;
+  const int b = t / ts, tt = t - b * ts, ty = tt / tpr, tx = tt - ty * tpr;
+  const float* src = c < a.Ca ? a.xa + ((size_t)b * a.Ca + c) * a.H * a.H
+                              : a.xb + ((size_t)b * a.Cb + (c - a.Ca)) * a.H * a.H;
+  float2 g = make_float2(1.f, 0.f);
+  if constexpr (ACT != ACT_NONE) g = a.gn[(size_t)b * Cin + c];
+  float d[6][6];
+#pragma unroll
+  for (int y = 0; y < 6; ++y) {
+    const int iy = 4 * ty - 1 + y;
+#pragma unroll
+    for (int x = 0; x < 6; ++x) {
+      const int ix = 4 * tx - 1 + x;
+      const bool ok = iy >= 0 && iy < a.H && ix >= 0 && ix < a.H;
+      float v = src[(ok ? iy : 0) * a.H + (ok ? ix : 0)];
+      if constexpr (ACT != ACT_NONE) {
+        v = __builtin_fmaf(v, g.x, g.y);
+        if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+      }
+      d[y][x] = ok ? v : 0.f;   // the padding pads the activated tensor
+    }
+  }
+  // columns: B^T over the rows of each column, then rows
+  float w[6][6];
+#pragma unroll
+  for (int x = 0; x < 6; ++x) {
+    float col[6], o[6];
+#pragma unroll
+    for (int y = 0; y < 6; ++y) col[y] = d[y][x];
+    bt6(col, o);
+#pragma unroll
+    for (int y = 0; y < 6; ++y) w[y][x] = o[y];
+  }
+  const size_t xs = (size_t)a.T * Cin;   // xi stride
+  float* out = a.V + (size_t)c * a.T + t;
+#pragma unroll
+  for (int y = 0; y < 6; ++y) {
+    float o[6];
+    bt6(w[y], o);
+#pragma unroll
+    for (int x = 0; x < 6; ++x) out[(size_t)(6 * y + x) * xs] = o[x];
+  }
+}
+
+__global__ __launch_bounds__(256) void wgw_d_kernel(WgwArgs a) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)a.T * a.Cout) return;
+  const int t = (int)(i % a.T);
+  const int co = (int)(i / a.T);
+  const int tpr = a.H / 4, ts = tpr * tpr;
+  const int b = t / ts, tt = t - b * ts, ty = tt / tpr, tx = tt - ty * tpr;
+  const float* src = a.dy + ((size_t)b * a.Cout + co) * a.H * a.H + (4 * ty) * a.H + 4 * tx;
+  float m[4][6];   // A applied along each row of the 4x4 tile
+#pragma unroll
+  for (int y = 0; y < 4; ++y) {
+    const float4 q = *reinterpret_cast<const float4*>(src + y * a.H);
+    const float v[4] = {q.x, q.y, q.z, q.w};
+    a4(v, m[y]);
+  }
+  const size_t xs = (size_t)a.T * a.Cout;
+  float* out = a.D + (size_t)co * a.T + t;
+#pragma unroll
+  for (int x = 0; x < 6; ++x) {
+    const float v[4] = {m[0][x], m[1][x], m[2][x], m[3][x]};
+    float o[6];
+    a4(v, o);
+#pragma unroll
+    for (int y = 0; y < 6; ++y) out[(size_t)(6 * y + x) * xs] = o[y];
+  }
+}
+
+// one wave per task (xi, co block 64, ci block 64, K range); 4 waves per workgroup
+__global__ __launch_bounds__(256) void wgw_gemm_kernel(WgwArgs a, int ntask) {
+  const int lane = threadIdx.x & 63;
+  const int task = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (task >= ntask) return;
+  const int Cin = a.Ca + a.Cb;
+  const int ncb = Cin / 64, nmb = a.Cout / 64;
+  int r = task;
+  const int nb = r % ncb; r /= ncb;
+  const int mb = r % nmb; r /= nmb;
+  const int xi = r % NX;
+  const int ks = r / NX;
+  const int c16 = lane & 15, g = lane >> 4;
+  // lane's float4 of 16-k block Q, row block i: [xi][row0 + 16 i + c16][16 Q + 4 g .. + 3]
+  const f32x4* Db = reinterpret_cast<const f32x4*>(a.D + ((size_t)xi * a.Cout + mb * 64 + c16) * a.T) + g;
+  const f32x4* Vb = reinterpret_cast<const f32x4*>(a.V + ((size_t)xi * Cin + nb * 64 + c16) * a.T) + g;
+  const size_t rs = (size_t)16 * a.T / 4;        // 16 rows, in float4s
+  const int q0 = ks * (a.kr / 16), q1 = min(q0 + a.kr / 16, a.T / 16);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+  // three register sets: the loads run two 16-k blocks ahead of the MFMAs
+  f32x4 av[3][4], bv[3][4];
+  auto load = [&](int Q, int s) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) av[s][i] = Db[(size_t)4 * Q + i * rs];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[s][j] = Vb[(size_t)4 * Q + j * rs];
+  };
+  auto step = [&](int s) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][i][k], bv[s][j][k], acc[i][j], 0, 0, 0);
+  };
+  // blocks past q1 re-load the last block (unconditional loads keep the
+  // compiler's vmcnt counting exact across the loop)
+  auto qc = [&](int Q) { return Q < q1 ? Q : q1 - 1; };
+  if (q0 < q1) {
+    load(q0, 0);
+    load(qc(q0 + 1), 1);
+  }
+  int Q = q0;
+  for (; Q + 2 < q1; Q += 3) {
+    load(qc(Q + 2), 2);
+    step(0);
+    load(qc(Q + 3), 0);
+    step(1);
+    load(qc(Q + 4), 1);
+    step(2);
+  }
+  if (Q < q1) step(0);
+  if (Q + 1 < q1) step(1);
+  // lane holds rows co = 64 mb + 16 i + 4 g + e, column ci = 64 nb + 16 j + c16
+  float* P = a.P + (((size_t)ks * NX + xi) * a.Cout) * Cin;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        P[(size_t)(64 * mb + 16 * i + 4 * g + e) * Cin + 64 * nb + 16 * j + c16] = acc[i][j][e];
+}
+
+// G (6 x 3) of the points {0, 1, -1, 1/2, -2, inf}
+__constant__ double kG[6][3] = {{1.0, 0.0, 0.0},
+                                {1.0 / 3, 1.0 / 3, 1.0 / 3},
+                                {-1.0 / 3, 1.0 / 3, -1.0 / 3},
+                                {-16.0 / 15, -8.0 / 15, -4.0 / 15},
+                                {1.0 / 15, -2.0 / 15, 4.0 / 15},
+                                {0.0, 0.0, 1.0}};
+
+// fixed-order sum of the K-range partials: one thread per (xi, co, ci), into
+// partial slot 0
+__global__ __launch_bounds__(256) void wgw_sum_kernel(WgwArgs a) {
+  const size_t n = (size_t)NX * a.Cout * (a.Ca + a.Cb);
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = a.P[i];
+  for (int k = 1; k < a.nks; ++k) s += a.P[(size_t)k * n + i];
+  a.P[i] = s;
+}
+
+// dW[co][ci] = G^T dU G in float64 (one thread per (co, ci))
+__global__ __launch_bounds__(256) void wgw_final_kernel(WgwArgs a, float* dw, int accumulate) {
+  const int Cin = a.Ca + a.Cb;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t cc = (size_t)a.Cout * Cin;
+  if (i >= cc) return;
+  double u[NX];
+#pragma unroll
+  for (int x = 0; x < NX; ++x) u[x] = (double)a.P[(size_t)x * cc + i];
+  float* o = dw + i * 9;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      double v = 0.0;
+#pragma unroll
+      for (int p = 0; p < 6; ++p) {
+        double rw = 0.0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) rw += u[6 * p + q] * kG[q][kx];
+        v += kG[p][ky] * rw;
+      }
+      const float f = (float)v;
+      o[3 * ky + kx] = accumulate ? o[3 * ky + kx] + f : f;
+    }
+}
+
+int wgw_env() {
+  static const int v = [] {
+    const char* e = getenv("ERTD_WGRAD_WINO");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+struct WgwPlan {
+  int T, nks, kr;
+  size_t v, d, p;   // floats
+};
+
+bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
+  if (Cin % 64 || Cout % 64 || (H != 16 && H != 32 && H != 64) || B < 1) return false;
+  const int T = B * (H / 4) * (H / 4);
+  if (T % 16) return false;
+  const int base = NX * (Cout / 64) * (Cin / 64);
+  const int nq = T / 16;                         // 16-k blocks
+  int nks = (2048 + base - 1) / base;            // ~2048 wave tasks (8 waves per CU)
+  if (nks > nq) nks = nq;
+  if (nks < 1) nks = 1;
+  const int qpr = (nq + nks - 1) / nks;
+  nks = (nq + qpr - 1) / qpr;
+  pl->T = T;
+  pl->nks = nks;
+  pl->kr = qpr * 16;
+  pl->v = (size_t)NX * T * Cin;
+  pl->d = (size_t)NX * T * Cout;
+  pl->p = (size_t)nks * NX * Cout * Cin;
+  return true;
+}
+
+}  // namespace
+
+size_t wgrad_wino_ws_floats(int Cin, int Cout, int B, int H, int ks, int mode) {
+  WgwPlan pl;
+  if (!wgw_env() || ks != 3 || mode != MODE_S1 || !wgw_plan(Cin, Cout, B, H, &pl)) return 0;
+  return pl.v + pl.d + pl.p;
+}
+
+hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B,
+                             int H, int Cout, const float* gn, int act, float* dw, int accumulate,
+                             float* ws, hipStream_t s) {
+  WgwPlan pl;
+  if (!wgw_plan(Ca + Cb, Cout, B, H, &pl)) return hipErrorInvalidValue;
+  const int Cin = Ca + Cb;
+  WgwArgs a{dy, x, x2, Ca, Cb, Cout, H, B, (const float2*)gn, ws, ws + pl.v, ws + pl.v + pl.d,
+            pl.T, pl.nks, pl.kr};
+  const size_t nv = (size_t)pl.T * Cin, nd = (size_t)pl.T * Cout;
+  if (act == ACT_GN_SILU) wgw_v_kernel<ACT_GN_SILU><<<(unsigned)((nv + 255) / 256), 256, 0, s>>>(a);
+  else if (act == ACT_GN) wgw_v_kernel<ACT_GN><<<(unsigned)((nv + 255) / 256), 256, 0, s>>>(a);
+  else wgw_v_kernel<ACT_NONE><<<(unsigned)((nv + 255) / 256), 256, 0, s>>>(a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  wgw_d_kernel<<<(unsigned)((nd + 255) / 256), 256, 0, s>>>(a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int ntask = pl.nks * NX * (Cout / 64) * (Cin / 64);
+  wgw_gemm_kernel<<<(unsigned)((ntask + 3) / 4), 256, 0, s>>>(a, ntask);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const size_t nw = (size_t)Cout * Cin;
+  if (pl.nks > 1) {
+    wgw_sum_kernel<<<(unsigned)((nw * NX + 255) / 256), 256, 0, s>>>(a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  wgw_final_kernel<<<(unsigned)((nw + 255) / 256), 256, 0, s>>>(a, dw, accumulate);
+  return hipGetLastError();
+}
+
+}  // namespace unet
+}  // namespace ertd

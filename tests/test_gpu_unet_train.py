@@ -170,6 +170,8 @@ def test_unet_train_rejects_bf16(cuda_dev):
 
 @pytest.mark.parametrize("Ca,Cb,Cout,H,ks,mode,B", [
     (64, 0, 64, 64, 3, 0, 3),      # ResBlock conv, 64x64
+    (64, 0, 64, 64, 3, 0, 32),     # ... at the train step's B = 32 (Winograd F(4x4) wgrad)
+    (384, 128, 256, 16, 3, 0, 32), # the widest decoder conv1 at B = 32
     (128, 64, 64, 32, 3, 0, 2),    # concat input, Cout < Cin
     (256, 0, 256, 16, 3, 0, 2),
     (1, 0, 32, 32, 3, 0, 2),       # conv_in: Cin = 1 (masked ci tile)
