@@ -370,7 +370,7 @@ CONV_KERNEL_CASES = [
      1.0),
     ("conv_wino4s_kernel<UP>", "u1.up 128->128 32x32 -> 64x64 (Upsample: F(4x4) on the nearest-x2 source)", 128, 0,
      128, 32, 3, 2, 0, False, False, 1 / 4),
-    ("conv_kernel<1>", "u0r0.skip 128+64->64 @64x64 (1x1, concat)", 128, 64, 64, 64, 1, 0, 0, False, False, 1.0),
+    ("conv1x1_kernel", "u0r0.skip 128+64->64 @64x64 (1x1, concat)", 128, 64, 64, 64, 1, 0, 0, False, False, 1.0),
     ("conv_in_kernel", "conv_in 1->64 @64x64", 1, 0, 64, 64, 3, 0, 0, False, False, 1.0),
     ("conv_out_kernel", "conv_out 64->1 @64x64, GN+SiLU", 64, 0, 1, 64, 3, 0, 1, False, False, 1.0),
 ]

@@ -82,19 +82,24 @@ __global__ __launch_bounds__(256) void wgw_v_kernel(WgwArgs a) {
   float2 g = make_float2(1.f, 0.f);
   if constexpr (ACT != ACT_NONE) g = a.gn[(size_t)b * Cin + c];
   float d[6][6];
+  const bool okl = tx > 0, okr = 4 * tx + 4 < a.H;
 #pragma unroll
   for (int y = 0; y < 6; ++y) {
     const int iy = 4 * ty - 1 + y;
+    const bool oky = iy >= 0 && iy < a.H;
+    // the row's four interior columns as one float4, the two halo columns alone
+    const float* row = src + (oky ? iy : 0) * a.H + 4 * tx;
+    const float4 m = *reinterpret_cast<const float4*>(row);
+    float v[6] = {okl ? row[-1] : 0.f, m.x, m.y, m.z, m.w, okr ? row[4] : 0.f};
 #pragma unroll
     for (int x = 0; x < 6; ++x) {
-      const int ix = 4 * tx - 1 + x;
-      const bool ok = iy >= 0 && iy < a.H && ix >= 0 && ix < a.H;
-      float v = src[(ok ? iy : 0) * a.H + (ok ? ix : 0)];
+      const bool ok = oky && (x == 0 ? okl : (x == 5 ? okr : true));
+      float u = v[x];
       if constexpr (ACT != ACT_NONE) {
-        v = __builtin_fmaf(v, g.x, g.y);
-        if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+        u = __builtin_fmaf(u, g.x, g.y);
+        if constexpr (ACT == ACT_GN_SILU) u = u * __builtin_amdgcn_rcpf(1.0f + __expf(-u));
       }
-      d[y][x] = ok ? v : 0.f;   // the padding pads the activated tensor
+      d[y][x] = ok ? u : 0.f;   // the padding pads the activated tensor
     }
   }
   // columns: B^T over the rows of each column, then rows
