@@ -152,8 +152,8 @@ hipError_t launch_conv1x1(const ConvArgs& a, int B, hipStream_t s);
 // multiples of 64, H in {16, 32, 64}; ERTD_WGRAD_WINO=0 disables)
 size_t wgrad_wino_ws_floats(int Cin, int Cout, int B, int H, int ks, int mode);
 hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B,
-                             int H, int Cout, const float* gn, int act, float* dw, int accumulate,
-                             float* ws, hipStream_t s);
+                             int H, int Cout, int mode, const float* gn, int act, float* dw,
+                             int accumulate, float* ws, hipStream_t s);
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s,

@@ -33,7 +33,6 @@ namespace {
 
 constexpr int NMW = 4;                        // MFMA waves (one per SIMD)
 constexpr int NPW = 4;                        // producer waves
-constexpr int WT = 64 * (NMW + NPW);          // 512 threads
 constexpr int CCH = 8;                        // input channels per chunk (2 MFMA k-steps)
 constexpr int NX = 36;
 constexpr int VKS = 18 * 128;                 // V floats per k-step: [xi/2 18][k 4][tile 16][xi&1]
@@ -97,8 +96,13 @@ __device__ __forceinline__ Item item_of(int it, int ncog) {
 // 2ty, 2ty, 2ty+1, 2ty+1, 2ty+2 and a lane's two columns one source column, so
 // a producer lane loads 4 source values instead of 12 (36 of the 144
 // multiplies per 4x4 output tile, against 64 for the sub-pixel direct kernel)
-template <int WO, int ACT, bool UP>
-__global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems) {
+// XS = 2: each co block's 36 xi are split over two MFMA waves (xi 0-17 / 18-35:
+// Winograd rows 0-2 / 3-5) -- two MFMA waves per SIMD hide each other's
+// operand-read and issue stalls; each computes the partial output transform
+// of its rows, the halves are exchanged through LDS across the item's last
+// barrier, and each wave finishes two of the lane's four channels
+template <int WO, int ACT, bool UP, int XS>
+__global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvArgs a, int nitems) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* vbuf = smem;                  // [2][V_FL]
 
@@ -118,10 +122,10 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
   const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;
   const int gtot = nloc * nchunk;
 
-  if (wave >= NMW) {
+  if (wave >= 4 * XS) {
     // =================== producer waves ===================
     __builtin_amdgcn_s_setprio(WINO4S_PPRIO);
-    const int q = wave - NMW;                 // channels 2q, 2q+1 of every chunk
+    const int q = wave - 4 * XS;              // channels 2q, 2q+1 of every chunk
     const int chb = lane >> 5, h = (lane >> 4) & 1, t = lane & 15;
     const int cl = 2 * q + chb;               // channel of the chunk: k-step cl >> 2, k = cl & 3
     const int vwoff = ((((cl >> 2) * 18 + 9 * h) * 4 + (cl & 3)) * 16 + t) * 2;
@@ -295,6 +299,7 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
     return;
   }
 
+  if constexpr (XS == 1) {
   // =================== MFMA waves ===================
   const int cb = wave;                         // co block of 16
   f32x4 acc[NX];
@@ -514,16 +519,243 @@ __global__ __launch_bounds__(WT) void conv_wino4s_kernel(ConvArgs a, int nitems)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
                                                i * HW * 4 + r * WO * 4, 0);
   }
+  } else {
+  // =================== MFMA waves, xi split over two waves ===================
+  constexpr int NP = 9;                        // xi pairs per wave
+  const int cb = wave & 3, xh = wave >> 2;
+  float* xbuf = smem + 2 * V_FL;               // [4 cb][2 receiver][8][64 lanes][4]
+  f32x4 acc[2 * NP];
+  const int nks = Cin / 4;
+  const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.wpk_wino4), (short)0, (int)((size_t)NX * a.Cout * Cin * 4), 0x00020000);
+  int u_il = 0, u_ks = 0, u_base = 0;
+  auto u_item = [&](int il) {
+    const Item itm = item_of(bid + il * G, ncog);
+    u_base = itm.cog * nks * 36864;
+  };
+  auto u_advance = [&]() {
+    if (++u_ks == nks) {
+      if (u_il + 1 < nloc) {
+        u_ks = 0;
+        u_item(++u_il);
+      } else {
+        u_ks = nks - 1;
+      }
+    }
+  };
+  if (nloc > 0) u_item(0);
+  f32x2 ub[2][NP];
+  const int uvoff = lane * 8 + cb * 512;
+  const int psoff = xh * NP * 2048;
+  auto u_load = [&](f32x2 (&u)[NP], const int p) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(ru, uvoff, u_base + u_ks * 36864 + psoff + p * 2048, 0);
+    u[p] = f32x2{__uint_as_float(v[0]), __uint_as_float(v[1])};
+  };
+  if (nloc > 0) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) u_load(ub[0], p);
+    u_advance();
+  }
+  __syncthreads();   // (A)
+  auto chunk2 = [&](const float* vs) {
+    constexpr int PD = WINO4S_PD;
+    f32x2 rb[PD + 1];
+#pragma unroll
+    for (int q = 0; q < PD; ++q) rb[q] = *reinterpret_cast<const f32x2*>(vs + (xh * NP + q) * 128);
+#pragma unroll
+    for (int q = 0; q < 2 * NP; ++q) {
+      const int st = q / NP, p = q % NP;
+      const int qn = q + PD;
+      if (qn < 2 * NP)
+        rb[qn % (PD + 1)] = *reinterpret_cast<const f32x2*>(vs + (qn / NP) * VKS + (xh * NP + qn % NP) * 128);
+      const int r = q % (PD + 1);
+      const f32x2 u = st == 0 ? ub[0][p] : ub[1][p];
+      acc[2 * p] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.x, rb[r].x, acc[2 * p], 0, 0, 0);
+      acc[2 * p + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.y, rb[r].y, acc[2 * p + 1], 0, 0, 0);
+      if (st == 0) u_load(ub[1], p);
+      else u_load(ub[0], p);
+      if (qn < 2 * NP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if (p == NP - 1) u_advance();
+    }
+  };
+  for (int il = 0; il < nloc; ++il) {
+#pragma unroll
+    for (int x = 0; x < 2 * NP; ++x) acc[x] = f32x4{};
+    f32x2 own[4][4];     // this wave's partial Y of its channel pair (pp = xh): [row][col]
+    for (int k = 0; k < nchunk; ++k) {
+      const int g = il * nchunk + k;
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      chunk2(vbuf + (g & 1) * V_FL + ln * 2);
+#pragma unroll
+      for (int x = 0; x < 2 * NP; ++x) asm volatile("" : "+v"(acc[x]));
+      if (k == nchunk - 1) {
+        // partial output transform of rows 3 xh .. 3 xh + 2:  P = M A per row,
+        // then Y[r] = sum_i A^T[r][3 xh + i] P[i]; the partner's channel pair to LDS
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          f32x2 P[3][4];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            f32x2 m[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) m[j] = f32x2{acc[6 * i + j][2 * pp], acc[6 * i + j][2 * pp + 1]};
+            at6(m, P[i]);
+          }
+          f32x2 Y[4][4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            if (xh == 0) {
+              const f32x2 s12 = P[1][x] + P[2][x], d12 = P[1][x] - P[2][x];
+              Y[0][x] = P[0][x] + s12;
+              Y[1][x] = d12;
+              Y[2][x] = s12;
+              Y[3][x] = d12;
+            } else {
+              Y[0][x] = P[0][x] + P[1][x];
+              Y[1][x] = fmac(P[0][x], 0.5f, P[1][x] * f32x2{-2.f, -2.f});
+              Y[2][x] = fmac(P[0][x], 0.25f, P[1][x] * f32x2{4.f, 4.f});
+              Y[3][x] = fmac(P[0][x], 0.125f, fmac(P[1][x], -8.f, P[2][x]));
+            }
+          }
+          if (pp == xh) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int x = 0; x < 4; ++x) own[r][x] = Y[r][x];
+          } else {
+            float* xw = xbuf + ((cb * 2 + (xh ^ 1)) * 8) * 256 + lane * 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int x = 0; x < 4; x += 2)
+                *reinterpret_cast<f32x4*>(xw + (r * 2 + x / 2) * 256) =
+                    f32x4{Y[r][x].x, Y[r][x].y, Y[r][x + 1].x, Y[r][x + 1].y};
+          }
+        }
+      }
+      __syncthreads();   // (B)
+    }
+    // ---- finish this wave's channel pair: own partial + the partner's
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    f32x4 y[2][4];   // [channel of the pair][output row]: 4 pixels
+    {
+      const float* xr = xbuf + ((cb * 2 + xh) * 8) * 256 + ln * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int x = 0; x < 4; x += 2) {
+          const f32x4 o = *reinterpret_cast<const f32x4*>(xr + (r * 2 + x / 2) * 256);
+          const f32x2 q0 = own[r][x] + f32x2{o[0], o[1]}, q1 = own[r][x + 1] + f32x2{o[2], o[3]};
+          y[0][r][x] = q0.x;
+          y[1][r][x] = q0.y;
+          y[0][r][x + 1] = q1.x;
+          y[1][r][x + 1] = q1.y;
+        }
+    }
+    const Item itm = item_of(bid + il * G, ncog);
+    const int flatw = itm.blk * 16;
+    const int smpl = flatw / TS;
+    const bool has_eb = a.ebias != nullptr, has_res = a.res != nullptr, has_bias = a.bias != nullptr;
+    const unsigned smp = (unsigned)(a.Cout * HW * 4);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (size_t)smpl * a.Cout * HW, (short)0, smp, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        has_res ? const_cast<float*>(a.res) + (size_t)smpl * a.Cout * HW : nullptr, (short)0, smp,
+        0x00020000);
+    const int co0 = itm.cog * 64 + cb * 16 + 4 * (ln >> 4) + 2 * xh;
+    const int tg = flatw % TS + (ln & 15);
+    const int ty = tg / TPR, tx = tg - ty * TPR;
+    const int vo = (co0 * HW + 4 * ty * WO + 4 * tx) * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float bi = has_bias ? a.bias[co0 + i] : 0.f;
+      const float ei = has_eb ? a.ebias[(size_t)smpl * a.eb_stride + co0 + i] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        y[i][r] = y[i][r] + bi;
+        if (has_eb) y[i][r] = y[i][r] + ei;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_res) {
+      f32x4 rv[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          rv[i][r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, vo, i * HW * 4 + r * WO * 4, 0));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[i][r] = y[i][r] + rv[i][r];
+    }
+    if (a.gnp) {
+      float2 pr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float sm = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm += (y[i][r][0] + y[i][r][1]) + (y[i][r][2] + y[i][r][3]);
+        sm = row16_sum(sm);
+        const float mu = sm * (1.0f / 256.0f);
+        float qq = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const float d = y[i][r][x] - mu;
+            qq = __builtin_fmaf(d, d, qq);
+          }
+        pr[i] = make_float2(sm, row16_sum(qq));
+      }
+      if ((ln & 15) == 0) {
+        const int np = TS / 16, part = (flatw % TS) / 16;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a.gnp[((size_t)smpl * a.Cout + co0 + i) * np + part] = pr[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
+                                               i * HW * 4 + r * WO * 4, 0);
+  }
+  }
+
+}
+
+// xi split over two MFMA waves per co block (default; ERTD_WINO4S_XS=1 keeps
+// one wave with all 36 xi, A/B): U2 B=64 240.5 -> 243.0 steps/s (same box,
+// two alternations).  Needs Cin >= 16: the exchange buffer is reused across an
+// item boundary only after a barrier that every wave passes between the two uses
+static int wino4s_xs() {
+  static const int v = [] {
+    const char* e = getenv("ERTD_WINO4S_XS");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
+template <int WO, int ACT, bool UP, int XS>
+hipError_t launch_wo4x(const ConvArgs& a, int B, hipStream_t s, int cus) {
+  constexpr size_t lds = WLDS + (XS == 2 ? (size_t)4 * 2 * 8 * 256 * sizeof(float) : 0);
+  static std::atomic<unsigned long long> attr{0};
+  set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS>, (int)lds, attr);
+  const int nitems = wino4s_items(a.Cout, WO, B);
+  const int grid = nitems < cus ? nitems : cus;
+  conv_wino4s_kernel<WO, ACT, UP, XS><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems);
+  return hipGetLastError();
 }
 
 template <int WO, int ACT, bool UP>
 hipError_t launch_wo4s(const ConvArgs& a, int B, hipStream_t s, int cus) {
-  static std::atomic<unsigned long long> attr{0};
-  set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP>, (int)WLDS, attr);
-  const int nitems = wino4s_items(a.Cout, WO, B);
-  const int grid = nitems < cus ? nitems : cus;
-  conv_wino4s_kernel<WO, ACT, UP><<<grid, WT, WLDS, s>>>(a, nitems);
-  return hipGetLastError();
+  if (wino4s_xs() == 2 && a.Cin >= 16) return launch_wo4x<WO, ACT, UP, 2>(a, B, s, cus);
+  return launch_wo4x<WO, ACT, UP, 1>(a, B, s, cus);
 }
 
 template <int ACT>

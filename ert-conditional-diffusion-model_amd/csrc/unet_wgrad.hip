@@ -397,7 +397,7 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
   const size_t wf = wgrad_wino_ws_floats(Ca + Cb, Cout, B, H, ks, mode);
   if (wf > 0) {
     if (wf * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
-    const hipError_t e = launch_wgrad_wino(dy, x, Ca, x2, Cb, B, H, Cout, gn, act, dw, accumulate,
+    const hipError_t e = launch_wgrad_wino(dy, x, Ca, x2, Cb, B, H, Cout, mode, gn, act, dw, accumulate,
                                            (float*)ws, (hipStream_t)stream);
     return e == hipSuccess ? ERTD_OK : (int)e;
   }

@@ -20,7 +20,9 @@
 //   wgw_sum_kernel / wgw_final_kernel  fixed-order sum of the K-range partials
 //                  (one thread per (xi, co, ci)), then G^T dU G in float64 -> dW (= or +=)
 // Bitwise reproducible (no atomics).  U2 B = 32 train step 13.95 -> 13.22 ms
-// (same box); ERTD_WGRAD_WINO=0 keeps the implicit GEMM (A/B).
+// (same box); ERTD_WGRAD_WINO=0 keeps the implicit GEMM (A/B).  The Upsample
+// convs (3x3 over the nearest-upsampled x) take the same path: only the V
+// transform's loads change (ERTD_WGRAD_WINO=2 keeps them on the implicit GEMM).
 #include <cstdlib>
 
 #include "unet.h"
@@ -66,9 +68,13 @@ struct WgwArgs {
   float* P;             // [nks][36][Cout][Cin]
   int T, nks, kr;       // tiles (K), K ranges, K per range (multiple of 16)
 };
+// (H = the conv's output size; the Upsample convs read x at H / 2, nearest)
 
-// one thread per (channel c, tile t), t fastest (coalesced stores per xi)
-template <int ACT>
+// one thread per (channel c, tile t), t fastest (coalesced stores per xi).
+// UP: the conv reads the nearest-upsampled x -- window row iy, column ix is
+// x[iy / 2][ix / 2] of the H / 2 plane (the 4 interior columns = 2 source
+// pixels, each twice)
+template <int ACT, bool UP>
 __global__ __launch_bounds__(256) void wgw_v_kernel(WgwArgs a) {
   const int Cin = a.Ca + a.Cb;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -77,8 +83,9 @@ __global__ __launch_bounds__(256) void wgw_v_kernel(WgwArgs a) {
   const int c = (int)(i / a.T);
   const int tpr = a.H / 4, ts = tpr * tpr;
   const int b = t / ts, tt = t - b * ts, ty = tt / tpr, tx = tt - ty * tpr;
-  const float* src = c < a.Ca ? a.xa + ((size_t)b * a.Ca + c) * a.H * a.H
-                              : a.xb + ((size_t)b * a.Cb + (c - a.Ca)) * a.H * a.H;
+  const int Hs = UP ? a.H / 2 : a.H;
+  const float* src = c < a.Ca ? a.xa + ((size_t)b * a.Ca + c) * Hs * Hs
+                              : a.xb + ((size_t)b * a.Cb + (c - a.Ca)) * Hs * Hs;
   float2 g = make_float2(1.f, 0.f);
   if constexpr (ACT != ACT_NONE) g = a.gn[(size_t)b * Cin + c];
   float d[6][6];
@@ -87,10 +94,26 @@ __global__ __launch_bounds__(256) void wgw_v_kernel(WgwArgs a) {
   for (int y = 0; y < 6; ++y) {
     const int iy = 4 * ty - 1 + y;
     const bool oky = iy >= 0 && iy < a.H;
-    // the row's four interior columns as one float4, the two halo columns alone
-    const float* row = src + (oky ? iy : 0) * a.H + 4 * tx;
-    const float4 m = *reinterpret_cast<const float4*>(row);
-    float v[6] = {okl ? row[-1] : 0.f, m.x, m.y, m.z, m.w, okr ? row[4] : 0.f};
+    // the row's four interior columns as one float4 (UP: one float2), the two
+    // halo columns alone
+    float v[6];
+    if constexpr (UP) {
+      const float* row = src + (oky ? iy >> 1 : 0) * Hs + 2 * tx;
+      const float2 m = *reinterpret_cast<const float2*>(row);
+      v[0] = okl ? row[-1] : 0.f;
+      v[1] = v[2] = m.x;
+      v[3] = v[4] = m.y;
+      v[5] = okr ? row[2] : 0.f;
+    } else {
+      const float* row = src + (oky ? iy : 0) * a.H + 4 * tx;
+      const float4 m = *reinterpret_cast<const float4*>(row);
+      v[0] = okl ? row[-1] : 0.f;
+      v[1] = m.x;
+      v[2] = m.y;
+      v[3] = m.z;
+      v[4] = m.w;
+      v[5] = okr ? row[4] : 0.f;
+    }
 #pragma unroll
     for (int x = 0; x < 6; ++x) {
       const bool ok = oky && (x == 0 ? okl : (x == 5 ? okr : true));
@@ -301,24 +324,32 @@ bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
 
 }  // namespace
 
+// H = the input size (the Upsample convs: Ho = 2 H)
 size_t wgrad_wino_ws_floats(int Cin, int Cout, int B, int H, int ks, int mode) {
   WgwPlan pl;
-  if (!wgw_env() || ks != 3 || mode != MODE_S1 || !wgw_plan(Cin, Cout, B, H, &pl)) return 0;
+  if (!wgw_env() || ks != 3 || (mode != MODE_S1 && mode != MODE_UP)) return 0;
+  if (mode == MODE_UP && wgw_env() == 2) return 0;   // ERTD_WGRAD_WINO=2: stride-1 only (A/B)
+  if (!wgw_plan(Cin, Cout, B, mode == MODE_UP ? 2 * H : H, &pl)) return 0;
   return pl.v + pl.d + pl.p;
 }
 
 hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B,
-                             int H, int Cout, const float* gn, int act, float* dw, int accumulate,
-                             float* ws, hipStream_t s) {
+                             int H, int Cout, int mode, const float* gn, int act, float* dw,
+                             int accumulate, float* ws, hipStream_t s) {
+  const bool up = mode == MODE_UP;
+  if ((mode != MODE_S1 && !up) || (up && act != ACT_NONE)) return hipErrorInvalidValue;
+  const int Ho = up ? 2 * H : H;
   WgwPlan pl;
-  if (!wgw_plan(Ca + Cb, Cout, B, H, &pl)) return hipErrorInvalidValue;
+  if (!wgw_plan(Ca + Cb, Cout, B, Ho, &pl)) return hipErrorInvalidValue;
   const int Cin = Ca + Cb;
-  WgwArgs a{dy, x, x2, Ca, Cb, Cout, H, B, (const float2*)gn, ws, ws + pl.v, ws + pl.v + pl.d,
+  WgwArgs a{dy, x, x2, Ca, Cb, Cout, Ho, B, (const float2*)gn, ws, ws + pl.v, ws + pl.v + pl.d,
             pl.T, pl.nks, pl.kr};
   const size_t nv = (size_t)pl.T * Cin, nd = (size_t)pl.T * Cout;
-  if (act == ACT_GN_SILU) wgw_v_kernel<ACT_GN_SILU><<<(unsigned)((nv + 255) / 256), 256, 0, s>>>(a);
-  else if (act == ACT_GN) wgw_v_kernel<ACT_GN><<<(unsigned)((nv + 255) / 256), 256, 0, s>>>(a);
-  else wgw_v_kernel<ACT_NONE><<<(unsigned)((nv + 255) / 256), 256, 0, s>>>(a);
+  const unsigned gv = (unsigned)((nv + 255) / 256);
+  if (up) wgw_v_kernel<ACT_NONE, true><<<gv, 256, 0, s>>>(a);
+  else if (act == ACT_GN_SILU) wgw_v_kernel<ACT_GN_SILU, false><<<gv, 256, 0, s>>>(a);
+  else if (act == ACT_GN) wgw_v_kernel<ACT_GN, false><<<gv, 256, 0, s>>>(a);
+  else wgw_v_kernel<ACT_NONE, false><<<gv, 256, 0, s>>>(a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   wgw_d_kernel<<<(unsigned)((nd + 255) / 256), 256, 0, s>>>(a);

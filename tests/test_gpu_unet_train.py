@@ -181,6 +181,8 @@ def test_unet_train_rejects_bf16(cuda_dev):
     (128, 0, 128, 32, 3, 1, 2),    # 32 -> 16
     (128, 0, 128, 16, 3, 2, 2),    # Upsample 16 -> 32
     (64, 0, 64, 64, 3, 2, 1),      # Upsample 64 -> 128
+    (128, 0, 128, 32, 3, 2, 8),    # u1.up 32 -> 64 (Winograd wgrad over the upsampled input)
+    (256, 0, 256, 16, 3, 2, 8),    # u2.up 16 -> 32
     (96, 32, 64, 32, 1, 0, 2),     # 1x1 skip on a concat
     (256, 0, 768, 16, 1, 0, 2),    # attention qkv
 ])
