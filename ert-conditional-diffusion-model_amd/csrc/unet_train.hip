@@ -83,7 +83,12 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 // Pass 1 reduces each channel's two sums within each wave (shuffles, no
 // barrier) into LDS; one barrier per 64 channels; the wave partials are then
-// added in a fixed order.  float4 loads throughout (HW % 4 == 0).
+// added in a fixed order.  float4 loads throughout (HW % 4 == 0).  A channel
+// gets min(4, HW / 256) waves (wpc): at 16x16 (64 float4s per
+// channel) the four waves take four channels at once instead of one wave
+// working while three idle.  The partial sums are the same values either way
+// (a wave that held no pixels contributed exact zeros), so results are
+// bitwise unchanged.
 constexpr int GNB_CB = 64;
 __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
     const float* __restrict__ xa, int Ca, const float* __restrict__ xb, int Cb, int HW, int groups,
@@ -93,6 +98,10 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
   __shared__ double part[2][GNB_CB][4];
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int C = Ca + Cb, cpg = C / groups, HW4 = HW / 4;
+  const int wpc = HW4 >= 256 ? 4 : (HW4 >= 128 ? 2 : 1);   // waves per channel
+  const int cpi = 4 / wpc;                                  // channels in flight
+  const int sub = w / wpc, wl = w - sub * wpc;
+  const int p0 = wl * 64 + lane, pst = wpc * 64;
   const float2 m = mr[(size_t)b * groups + g];
   const float mean = m.x, rstd = m.y;
   auto xptr = [&](int c) {
@@ -105,13 +114,13 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
   double A = 0.0, Bs = 0.0;
   for (int c0 = 0; c0 < cpg; c0 += GNB_CB) {
     const int nc = cpg - c0 < GNB_CB ? cpg - c0 : GNB_CB;
-    for (int cl = 0; cl < nc; ++cl) {
+    for (int cl = sub; cl < nc; cl += cpi) {
       const int c = g * cpg + c0 + cl;
       const float4* x = (const float4*)xptr(c);
       const float4* d = (const float4*)(dy + ((size_t)b * C + c) * HW);
       const float ga = gamma[c], be = beta[c];
       double sg = 0.0, sb = 0.0;
-      for (int p = tid; p < HW4; p += 256) {
+      for (int p = p0; p < HW4; p += pst) {
         const float4 xv = x[p], dv = d[p];
         float xh, dn;
         dn = dxn_of(xv.x, dv.x, ga, be, xh); sg += (double)dn * xh; sb += (double)dn;
@@ -122,15 +131,24 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
       sg = wave_sum_d(sg);
       sb = wave_sum_d(sb);
       if (lane == 0) {
-        part[0][cl][w] = sg;
-        part[1][cl][w] = sb;
+        part[0][cl][wl] = sg;
+        part[1][cl][wl] = sb;
       }
     }
     __syncthreads();
     for (int cl = 0; cl < nc; ++cl) {
       const int c = g * cpg + c0 + cl;
-      const double sg = (part[0][cl][0] + part[0][cl][1]) + (part[0][cl][2] + part[0][cl][3]);
-      const double sb = (part[1][cl][0] + part[1][cl][1]) + (part[1][cl][2] + part[1][cl][3]);
+      double sg, sb;
+      if (wpc == 4) {
+        sg = (part[0][cl][0] + part[0][cl][1]) + (part[0][cl][2] + part[0][cl][3]);
+        sb = (part[1][cl][0] + part[1][cl][1]) + (part[1][cl][2] + part[1][cl][3]);
+      } else if (wpc == 2) {
+        sg = part[0][cl][0] + part[0][cl][1];
+        sb = part[1][cl][0] + part[1][cl][1];
+      } else {
+        sg = part[0][cl][0];
+        sb = part[1][cl][0];
+      }
       if (tid == 0) {
         dgb[(size_t)(2 * b) * C + c] = (float)sg;        // [b][0][c]: dgamma partial
         dgb[(size_t)(2 * b + 1) * C + c] = (float)sb;    // [b][1][c]: dbeta partial
@@ -143,13 +161,13 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
   }
   const double n = (double)cpg * HW;
   const float mA = (float)(A / n), mB = (float)(Bs / n);
-  for (int cl = 0; cl < cpg; ++cl) {
+  for (int cl = sub; cl < cpg; cl += cpi) {
     const int c = g * cpg + cl;
     const float4* x = (const float4*)xptr(c);
     float4* dx = (float4*)(c < Ca ? dxa + ((size_t)b * Ca + c) * HW : dxb + ((size_t)b * Cb + c - Ca) * HW);
     const float4* d = (const float4*)(dy + ((size_t)b * C + c) * HW);
     const float ga = gamma[c], be = beta[c];
-    for (int p = tid; p < HW4; p += 256) {
+    for (int p = p0; p < HW4; p += pst) {
       const float4 xv = x[p], dv = d[p];
       float4 o = accumulate ? dx[p] : float4{0.f, 0.f, 0.f, 0.f};
       float xh, dn;
