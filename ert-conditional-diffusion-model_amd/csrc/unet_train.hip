@@ -17,6 +17,7 @@
 //   ertd_zero_insert / ertd_sum_pool2   stride-2 / upsample dX plumbing
 //   ertd_channel_sums         per (sample, channel) and per channel sums (bias / emb grads)
 //   ertd_reduce_rows          fixed-order sum over rows (per-sample partials -> grads)
+//   ertd_reduce_rows_multi    many of those in one launch (bitwise equal)
 //   ertd_gemm_small           strided batched fp32 GEMM (+ bias / accumulate): dense layers,
 //                             attention forward / backward
 //   ertd_softmax_rows / ertd_softmax_backward   attention softmax and its backward
@@ -270,6 +271,48 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   if (ty == 0 && j < cols) {
     const float s = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
     out[j] = accumulate ? out[j] + s : s;
+  }
+}
+
+// Several reduce_rows_kernel problems in one launch (the train step's per-layer
+// dgamma/dbeta and bias reductions, deferred to the end of the backward walk):
+// workgroup -> (problem k, 64-column block) through the block prefix; the sum
+// of every column in exactly reduce_rows_kernel's order (bitwise equal)
+constexpr int RM_T = 48;
+struct ReduceMulti {
+  const float* part[RM_T];
+  float* out[RM_T];
+  long long cols[RM_T];
+  int rows[RM_T];
+  int acc[RM_T];
+  int blk[RM_T + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void reduce_rows_multi_kernel(ReduceMulti a) {
+  __shared__ float red[4][64];
+  const int bid = blockIdx.x;
+  int k = 0;
+  while (k + 1 < a.n && bid >= a.blk[k + 1]) ++k;
+  const float* __restrict__ part = a.part[k];
+  const int rows = a.rows[k];
+  const size_t cols = (size_t)a.cols[k];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const size_t j = (size_t)(bid - a.blk[k]) * 64 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (j < cols) {
+    int r = ty;
+    for (; r + 4 < rows; r += 8) {
+      s0 += part[(size_t)r * cols + j];
+      s1 += part[(size_t)(r + 4) * cols + j];
+    }
+    if (r < rows) s0 += part[(size_t)r * cols + j];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && j < cols) {
+    const float sum = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    float* out = a.out[k];
+    out[j] = a.acc[k] ? out[j] + sum : sum;
   }
 }
 
@@ -634,6 +677,33 @@ int ertd_reduce_rows(const float* part, int rows, long long cols, float* out, in
   reduce_rows_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, (hipStream_t)stream>>>(part, rows, (size_t)cols,
                                                                                    out, accumulate);
   return rcode(hipGetLastError());
+}
+
+int ertd_reduce_rows_multi(const float* const* parts, const int* rows, const long long* cols,
+                           float* const* outs, const int* accumulate, int n, void* stream) {
+  if (!parts || !rows || !cols || !outs || !accumulate || n < 0) return ERTD_EINVAL;
+  for (int i = 0; i < n; ++i)
+    if (!parts[i] || !outs[i] || rows[i] < 1 || cols[i] < 1) return ERTD_EINVAL;
+  for (int t0 = 0; t0 < n; t0 += RM_T) {
+    ReduceMulti a{};
+    a.n = n - t0 < RM_T ? n - t0 : RM_T;
+    long long nb = 0;
+    for (int i = 0; i < a.n; ++i) {
+      a.part[i] = parts[t0 + i];
+      a.out[i] = outs[t0 + i];
+      a.rows[i] = rows[t0 + i];
+      a.cols[i] = cols[t0 + i];
+      a.acc[i] = accumulate[t0 + i];
+      a.blk[i] = (int)nb;
+      nb += (cols[t0 + i] + 63) / 64;
+    }
+    if (nb > 0x7fffffffLL) return ERTD_EINVAL;
+    a.blk[a.n] = (int)nb;
+    reduce_rows_multi_kernel<<<(unsigned)nb, 256, 0, (hipStream_t)stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return ERTD_OK;
 }
 
 int ertd_conv_weight_flip(const float* w, int Cout, int Cin, int ks, float* out, void* stream) {

@@ -113,6 +113,7 @@ SIGNATURES = {
     "ertd_wgrad_ws_bytes": (_SZ, [_I, _I, _I, _I]),
     "ertd_wgrad_gemm": (_I, [_VP, _VP, _I, _I, _I, _I, _LL, _LL, _VP, _I, _VP, _SZ, _VP]),
     "ertd_reduce_rows": (_I, [_VP, _I, _LL, _VP, _I, _VP]),
+    "ertd_reduce_rows_multi": (_I, [_VP, _VP, _VP, _VP, _VP, _I, _VP]),
     "ertd_conv_weight_flip": (_I, [_VP, _I, _I, _I, _VP, _VP]),
     "ertd_zero_insert": (_I, [_VP, _I, _I, _I, _VP, _VP]),
     "ertd_sum_pool2": (_I, [_VP, _I, _I, _I, _VP, _I, _VP]),

@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -134,6 +135,10 @@ class _K:
         self._ws: Optional[torch.Tensor] = None
         self._zero: Dict[int, torch.Tensor] = {}
         self.packs = packs
+        # GroupNorm dgamma/dbeta row reductions, launched together by
+        # flush_reductions() at the end of the backward walk (nothing reads them
+        # before the optimizer); ERTD_DEFER_REDUCE=0 launches each one in place
+        self.deferred = [] if os.environ.get("ERTD_DEFER_REDUCE", "1") != "0" else None
 
     def empty(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)
@@ -215,12 +220,28 @@ class _K:
             mr.data_ptr(), act, dy.data_ptr(), dxa.data_ptr(), _p(dxb), int(accumulate),
             part.data_ptr(), self.s), "gn_act_backward")
         dgb = self.empty(2, C)
-        self.reduce_rows(part, B, 2 * C, dgb)
+        if self.deferred is None:
+            self.reduce_rows(part, B, 2 * C, dgb)
+        else:
+            self.deferred.append((part, B, 2 * C, dgb))   # holds part until the flush
         return dgb[0], dgb[1]
 
     def reduce_rows(self, part, rows, cols, out, accumulate=False):
         _lib.check(self.lib.ertd_reduce_rows(part.data_ptr(), rows, cols, out.data_ptr(),
                                              int(accumulate), self.s), "reduce_rows")
+
+    def flush_reductions(self):
+        """The deferred row reductions in one ertd_reduce_rows_multi call (each
+        output bitwise equal to its own ertd_reduce_rows)."""
+        d = self.deferred
+        if not d:
+            return
+        n = len(d)
+        _lib.check(self.lib.ertd_reduce_rows_multi(
+            _arr([p.data_ptr() for p, _, _, _ in d]), _arr([r for _, r, _, _ in d], ctypes.c_int),
+            _arr([c for _, _, c, _ in d], ctypes.c_longlong), _arr([o.data_ptr() for _, _, _, o in d]),
+            _arr([0] * n, ctypes.c_int), n, self.s), "reduce_rows_multi")
+        self.deferred = []
 
     # ---- conv gradients
     def conv_wgrad(self, dy, xa, xb, ks, mode, out, gn=None, act=0):
@@ -717,6 +738,7 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
             tape["ews"].data_ptr(), tape["ews"].numel(), k.s), "encoder_train_bwd")
         grads["condition_encoder.0.weight"], grads["condition_encoder.0.bias"] = enc[0], enc[1]
         grads["condition_encoder.2.weight"], grads["condition_encoder.2.bias"] = enc[2], enc[3]
+    k.flush_reductions()
     missing = [nm for nm, _ in model.layout if nm not in grads]
     if missing:
         raise RuntimeError(f"ertdiff: no gradient for {missing[:4]}")

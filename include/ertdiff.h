@@ -405,6 +405,13 @@ int ertd_wgrad_gemm(const float* dY, const float* X, int M, int N, int P, int B,
                     void* stream);
 int ertd_reduce_rows(const float* part, int rows, long long cols, float* out, int accumulate,
                      void* stream);
+/* ertd_reduce_rows_multi: n independent ertd_reduce_rows problems (host arrays of
+ * their arguments) in ceil(n / 48) launches; every output bitwise equal to the
+ * single call's.  The U-Net train walk defers its per-layer dgamma/dbeta and
+ * linear-bias reductions (no other kernel reads them before the optimizer) to one
+ * such call at the end of the backward.                                         */
+int ertd_reduce_rows_multi(const float* const* parts, const int* rows, const long long* cols,
+                           float* const* outs, const int* accumulate, int n, void* stream);
 int ertd_conv_weight_flip(const float* w, int Cout, int Cin, int ks, float* out, void* stream);
 int ertd_zero_insert(const float* x, int B, int C, int Ho, float* out, void* stream);
 int ertd_sum_pool2(const float* x, int B, int C, int H, float* out, int accumulate, void* stream);

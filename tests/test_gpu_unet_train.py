@@ -346,6 +346,39 @@ def test_gn_act_backward_vs_autograd(Ca, Cb, HW, groups, act, acc, cuda_dev):
     assert max(e) < 1e-5, e
 
 
+@pytest.mark.gpu
+def test_reduce_rows_multi_bitwise(cuda_dev):
+    """ertd_reduce_rows_multi (the train walk's deferred dgamma/dbeta sums): 53
+    problems of ragged shapes (two launches of <= 48), accumulate on and off,
+    every output bitwise equal to its own ertd_reduce_rows call."""
+    import ctypes
+    from ertdiff import _lib
+    lib = _lib.lib()
+    s = _lib.stream_of(cuda_dev)
+    g = torch.Generator().manual_seed(11)
+    probs = []
+    for i in range(53):
+        rows = [1, 3, 4, 5, 8, 9, 32, 33][i % 8]
+        cols = [1, 63, 64, 65, 128, 1000, 2 * 384][i % 7]
+        part = torch.randn(rows, cols, generator=g).to(cuda_dev)
+        init = torch.randn(cols, generator=g).to(cuda_dev)
+        probs.append((part, rows, cols, init, i % 3 == 0))
+    want, outs = [], []
+    for part, rows, cols, init, acc in probs:
+        o = init.clone()
+        assert lib.ertd_reduce_rows(part.data_ptr(), rows, cols, o.data_ptr(), int(acc), s) == 0
+        want.append(o)
+        outs.append(init.clone())
+    arr = lambda v, t=ctypes.c_void_p: (t * len(v))(*v)
+    assert lib.ertd_reduce_rows_multi(arr([p[0].data_ptr() for p in probs]), arr([p[1] for p in probs], ctypes.c_int),
+                                      arr([p[2] for p in probs], ctypes.c_longlong), arr([o.data_ptr() for o in outs]),
+                                      arr([int(p[4]) for p in probs], ctypes.c_int), len(probs), s) == 0
+    torch.cuda.synchronize(cuda_dev)
+    for w, o in zip(want, outs):
+        assert torch.equal(w, o)
+    assert lib.ertd_reduce_rows_multi(None, None, None, None, None, 1, s) != 0
+
+
 @pytest.mark.parametrize("Cin,Cout,H,ks,mode,B,acc", [
     (64, 64, 64, 3, 0, 2, 0),      # Winograd-eligible gradient conv
     (192, 64, 32, 3, 0, 2, 1),     # Cin_grad = 64 -> Cout_grad = 192, accumulate
