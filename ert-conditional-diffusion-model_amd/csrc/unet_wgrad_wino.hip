@@ -308,7 +308,12 @@ bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
   if (T % 16) return false;
   const int base = NX * (Cout / 64) * (Cin / 64);
   const int nq = T / 16;                         // 16-k blocks
-  int nks = (2048 + base - 1) / base;            // ~2048 wave tasks (8 waves per CU)
+  static const int target = [] {                 // ERTD_WGW_TASKS: wave-task target (A/B)
+    const char* e = getenv("ERTD_WGW_TASKS");
+    const int v = e ? atoi(e) : 2048;
+    return v > 0 ? v : 2048;
+  }();
+  int nks = (target + base - 1) / base;          // ~2048 wave tasks (8 waves per CU)
   if (nks > nq) nks = nq;
   if (nks < 1) nks = 1;
   const int qpr = (nq + nks - 1) / nks;
