@@ -34,6 +34,9 @@ namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 constexpr int NX = 36;
+#ifndef WGW_SETS
+#define WGW_SETS 3
+#endif
 
 // o = B^T d (unet_conv_wino4.hip)
 __device__ __forceinline__ void bt6(const float (&d)[6], float (&o)[6]) {
@@ -197,8 +200,11 @@ __global__ __launch_bounds__(256) void wgw_gemm_kernel(WgwArgs a, int ntask) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
-  // three register sets: the loads run two 16-k blocks ahead of the MFMAs
-  f32x4 av[3][4], bv[3][4];
+  // WGW_SETS register sets: the loads run WGW_SETS - 1 16-k blocks ahead of
+  // the MFMAs.  3 (176 VGPRs); 4 and 5 (192+ VGPRs, still two waves per SIMD)
+  // measured 1.5 % / 2 % slower on the U2 B=32 train step (same box)
+  constexpr int NS = WGW_SETS;
+  f32x4 av[NS][4], bv[NS][4];
   auto load = [&](int Q, int s) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) av[s][i] = Db[(size_t)4 * Q + i * rs];
@@ -218,20 +224,21 @@ __global__ __launch_bounds__(256) void wgw_gemm_kernel(WgwArgs a, int ntask) {
   // compiler's vmcnt counting exact across the loop)
   auto qc = [&](int Q) { return Q < q1 ? Q : q1 - 1; };
   if (q0 < q1) {
-    load(q0, 0);
-    load(qc(q0 + 1), 1);
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) load(qc(q0 + s), s);
   }
+  // invariant at the loop head: set s holds block Q + s (s < NS - 1)
   int Q = q0;
-  for (; Q + 2 < q1; Q += 3) {
-    load(qc(Q + 2), 2);
-    step(0);
-    load(qc(Q + 3), 0);
-    step(1);
-    load(qc(Q + 4), 1);
-    step(2);
+  for (; Q + NS - 1 < q1; Q += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      load(qc(Q + s + NS - 1), (s + NS - 1) % NS);
+      step(s);
+    }
   }
-  if (Q < q1) step(0);
-  if (Q + 1 < q1) step(1);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (Q + s < q1) step(s);
   // lane holds rows co = 64 mb + 16 i + 4 g + e, column ci = 64 nb + 16 j + c16
   float* P = a.P + (((size_t)ks * NX + xi) * a.Cout) * Cin;
 #pragma unroll
