@@ -14,6 +14,8 @@
 // already holds (fp32 [co_tile32][chunk][step pair][lane][2] or bf16
 // [co_tile32][chunk][step][lane][8]); the bf16 variant also rounds the staged
 // activation to bf16 (RNE), so its products equal the bf16 MFMA's.
+#include <cstdlib>
+
 #include "unet.h"
 
 namespace ertd {
@@ -47,62 +49,69 @@ __device__ __forceinline__ float packed_w_bf16(const float* w, int ci, int tap, 
 // ROWS whole rows (the whole image at W <= 32).  Staged rows: W + 8 floats,
 // data at column 4 (16-B aligned float4 stores / loads), zero columns 3 and
 // W + 4; the 3 taps of a kernel row read one float4 + two neighbours.
-template <int WO, int RWS>
+// NS channel groups: the workgroup is NS x NT threads, group g sweeps input
+// channels [g Cq, (g + 1) Cq) (Cq = ceil(Cin / NS) rounded to OCC) through its
+// own staging buffer, and the NS partial sums of a pixel are added in a fixed
+// order at the end -- NS times the loads in flight per CU (one 4-wave
+// workgroup per CU left the layer latency-bound: 42 us at U2 B=64)
+template <int WO, int RWS, int NS>
 struct OutGeom {
   static constexpr int TPR = WO / 4;                          // threads per output row
   static constexpr int ROWS = RWS;
-  static constexpr int NT = TPR * ROWS;                       // threads per workgroup
+  static constexpr int NT = TPR * ROWS;                       // threads per channel group
   static constexpr int IR = ROWS + 2;
   static constexpr int IP = WO + 8;
   static constexpr int CSZ = IR * IP;
-  static constexpr int OCC = 8;                               // channels per staged chunk
+  static constexpr int OCC = NS >= 4 ? 4 : 8;                 // channels per staged chunk
   static_assert(WO % ROWS == 0 && NT <= 256 && NT % 64 == 0, "whole output rows per workgroup");
 };
 
-template <int ACT, int WO, int RWS, int PK>
-__global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
+template <int ACT, int WO, int RWS, int PK, int NS>
+__global__ __launch_bounds__(1024) void conv_out_kernel(ConvArgs a) {
   constexpr bool BF = PK == PK_BF16;   // round the staged input to bf16
-  using G = OutGeom<WO, RWS>;
+  using G = OutGeom<WO, RWS, NS>;
   constexpr int OCC = G::OCC;
   extern __shared__ __attribute__((aligned(16))) float smo[];
   const int Cin = a.Cin, Ca = a.Ca;
-  float* img = smo;                                   // [OCC][IR][IP]
-  float* wl = smo + OCC * G::CSZ;                     // [Cin][9]
-  float2* gtab = reinterpret_cast<float2*>(wl + ((Cin * 9 + 1) & ~1));  // [Cin]
   const int tid = threadIdx.x, b = blockIdx.z;
+  const int grp = tid / G::NT, tl = tid - grp * G::NT;
+  float* img = smo + grp * OCC * G::CSZ;              // this group's [OCC][IR][IP]
+  float* wl = smo + NS * OCC * G::CSZ;                // [Cin][9]
+  float2* gtab = reinterpret_cast<float2*>(wl + ((Cin * 9 + 1) & ~1));  // [Cin]
   const int oy0 = blockIdx.x * G::ROWS;
   constexpr size_t plane = (size_t)WO * WO;
+  const int cq = ((Cin + NS - 1) / NS + OCC - 1) / OCC * OCC;   // channels per group
+  const int cbeg = grp * cq, cend = min(Cin, cbeg + cq);
 
-  for (int i = tid; i < Cin * 9; i += G::NT) {
+  for (int i = tid; i < Cin * 9; i += NS * G::NT) {
     const int ci = i / 9, tap = i - ci * 9;
     wl[i] = PK == PK_F32 ? packed_w_f32(a.wpk, ci, tap) : packed_w_bf16(a.wpk, ci, tap, PK == PK_SPLIT);
   }
   if constexpr (ACT != ACT_NONE) {
-    for (int c = tid; c < Cin; c += G::NT) gtab[c] = a.gn[(size_t)b * Cin + c];
+    for (int c = tid; c < Cin; c += NS * G::NT) gtab[c] = a.gn[(size_t)b * Cin + c];
   }
-  for (int r = tid; r < OCC * G::IR; r += G::NT) {
+  for (int r = tl; r < OCC * G::IR; r += G::NT) {
     img[r * G::IP + 3] = 0.f;
     img[r * G::IP + 4 + WO] = 0.f;
   }
 
-  const int py = tid / G::TPR, px4 = tid - py * G::TPR;
+  const int py = tl / G::TPR, px4 = tl - py * G::TPR;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   // staging in two phases: the next chunk's float4 loads are issued into
   // registers before the current chunk's fma chains, so the global-load
-  // latency hides behind them (one staging phase per chunk, load -> transform
-  // -> compute in series, left the layer latency-bound at one workgroup per CU)
+  // latency hides behind them
   constexpr int NQ = OCC * G::IR * G::TPR;                   // float4 quads per chunk
   constexpr int NPT = (NQ + G::NT - 1) / G::NT;
   float4 raw[NPT];
   auto load = [&](int c0) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int e = tid + k * G::NT;
+      const int e = tl + k * G::NT;
       const int c = e / (G::IR * G::TPR), rem = e - c * (G::IR * G::TPR);
       const int r = rem / G::TPR, q = rem - r * G::TPR;
       const int cg = c0 + c, iy = oy0 - 1 + r;
       raw[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < NQ && cg < Cin && iy >= 0 && iy < WO) {
+      if (e < NQ && cg < cend && iy >= 0 && iy < WO) {
         const float* src = cg < Ca ? a.srcA + ((size_t)b * Ca + cg) * plane
                                    : a.srcB + ((size_t)b * a.Cb + (cg - Ca)) * plane;
         raw[k] = *reinterpret_cast<const float4*>(src + iy * WO + 4 * q);
@@ -112,13 +121,13 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
   auto stage = [&](int c0) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int e = tid + k * G::NT;
+      const int e = tl + k * G::NT;
       if (e >= NQ) continue;
       const int c = e / (G::IR * G::TPR), rem = e - c * (G::IR * G::TPR);
       const int r = rem / G::TPR, q = rem - r * G::TPR;
       const int cg = c0 + c, iy = oy0 - 1 + r;
       float4 v = raw[k];
-      if (cg < Cin && iy >= 0 && iy < WO) {
+      if (cg < cend && iy >= 0 && iy < WO) {
         if constexpr (ACT != ACT_NONE) {
           const float2 g = gtab[cg];
           v.x = fmaf(v.x, g.x, g.y);
@@ -142,13 +151,17 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
       *reinterpret_cast<float4*>(img + (c * G::IR + r) * G::IP + 4 + 4 * q) = v;
     }
   };
-  load(0);
-  for (int c0 = 0; c0 < Cin; c0 += OCC) {
+  // every group runs the same number of chunks (workgroup-wide barriers); a
+  // group past Cin stages zeros and skips the fma chains
+  const int nchunk = cq / OCC;
+  load(cbeg);
+  for (int k = 0; k < nchunk; ++k) {
+    const int c0 = cbeg + k * OCC;
     __syncthreads();  // tables visible / previous chunk consumed
     stage(c0);
     __syncthreads();
-    if (c0 + OCC < Cin) load(c0 + OCC);
-    const int nc = Cin - c0 < OCC ? Cin - c0 : OCC;
+    if (k + 1 < nchunk) load(c0 + OCC);
+    const int nc = cend - c0 < OCC ? cend - c0 : OCC;
     for (int c = 0; c < nc; ++c) {
       const float* wp = wl + (c0 + c) * 9;
 #pragma unroll
@@ -163,6 +176,26 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
         acc[2] = fmaf(w0, m.y, acc[2]); acc[2] = fmaf(w1, m.z, acc[2]); acc[2] = fmaf(w2, m.w, acc[2]);
         acc[3] = fmaf(w0, m.z, acc[3]); acc[3] = fmaf(w1, m.w, acc[3]); acc[3] = fmaf(w2, rr, acc[3]);
       }
+    }
+  }
+  if constexpr (NS > 1) {
+    // the groups' partial sums through LDS (the staging buffers are free now),
+    // added in a fixed order by group 0
+    __syncthreads();
+    float4* red = reinterpret_cast<float4*>(smo);
+    red[grp * G::NT + tl] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    if (grp != 0) return;
+    float4 t[NS];
+#pragma unroll
+    for (int g2 = 0; g2 < NS; ++g2) t[g2] = red[g2 * G::NT + tl];
+    if constexpr (NS == 2) {
+      acc[0] = t[0].x + t[1].x; acc[1] = t[0].y + t[1].y; acc[2] = t[0].z + t[1].z; acc[3] = t[0].w + t[1].w;
+    } else {
+      acc[0] = (t[0].x + t[1].x) + (t[2].x + t[3].x);
+      acc[1] = (t[0].y + t[1].y) + (t[2].y + t[3].y);
+      acc[2] = (t[0].z + t[1].z) + (t[2].z + t[3].z);
+      acc[3] = (t[0].w + t[1].w) + (t[2].w + t[3].w);
     }
   }
 
@@ -181,30 +214,44 @@ __global__ __launch_bounds__(256) void conv_out_kernel(ConvArgs a) {
   *reinterpret_cast<float4*>(a.out + o) = v;
 }
 
-template <int ACT, int WO, int RWS, int BF>
+template <int ACT, int WO, int RWS, int BF, int NS>
 hipError_t launch_co(const ConvArgs& a, int B, hipStream_t s) {
-  using G = OutGeom<WO, RWS>;
-  const size_t lds = ((size_t)G::OCC * G::CSZ + (((size_t)a.Cin * 9 + 1) & ~(size_t)1)) * sizeof(float) +
+  using G = OutGeom<WO, RWS, NS>;
+  const size_t lds = ((size_t)NS * G::OCC * G::CSZ + (((size_t)a.Cin * 9 + 1) & ~(size_t)1)) * sizeof(float) +
                      (size_t)a.Cin * sizeof(float2);
+  static_assert((size_t)NS * G::NT * 16 <= (size_t)NS * G::OCC * G::CSZ * 4, "partials fit the staging buffers");
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)conv_out_kernel<ACT, WO, RWS, BF>,
+    (void)hipFuncSetAttribute((const void*)conv_out_kernel<ACT, WO, RWS, BF, NS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((unsigned)(WO / G::ROWS), 1u, (unsigned)B);
-  conv_out_kernel<ACT, WO, RWS, BF><<<grid, G::NT, lds, s>>>(a);
+  conv_out_kernel<ACT, WO, RWS, BF, NS><<<grid, NS * G::NT, lds, s>>>(a);
   return hipGetLastError();
 }
 
-// rows per workgroup: 256 threads (16 rows; 8 at W = 128; the whole image at
-// W = 16).  Measured on a U2 B=64 step (64x64): 16 rows (256 workgroups)
-// 60.5 us, 4 rows (1024 one-wave workgroups) 70.5 us -- per-workgroup weight
-// gathers and the halo re-reads cost more than the lost occupancy; U3 B=256:
-// 163 us (the one-pixel-per-thread kernel before: 244 us).
+// channel groups per workgroup (ERTD_CONV_OUT_NS, A/B; 1 = one 256-thread group)
+static int conv_out_ns() {
+  static const int v = [] {
+    const char* e = getenv("ERTD_CONV_OUT_NS");
+    const int n = e ? atoi(e) : 4;
+    return n == 1 || n == 2 ? n : 4;
+  }();
+  return v;
+}
+
+// rows per workgroup: 256 threads per channel group (16 rows; 8 at W = 128;
+// the whole image at W = 16).  Measured on a U2 B=64 step (64x64), one group:
+// 16 rows (256 workgroups) 60.5 us, 4 rows (1024 one-wave workgroups) 70.5 us
+// -- per-workgroup weight gathers and the halo re-reads cost more than the
+// lost occupancy; U3 B=256: 163 us (the one-pixel-per-thread kernel before: 244 us).
 template <int ACT, int WO, int BF>
 hipError_t launch_co_r(const ConvArgs& a, int B, hipStream_t s) {
   constexpr int TPR = WO / 4;
   constexpr int R = (256 / TPR) < WO ? (256 / TPR) : WO;
-  return launch_co<ACT, WO, R, BF>(a, B, s);
+  const int ns = conv_out_ns();
+  if (ns == 1) return launch_co<ACT, WO, R, BF, 1>(a, B, s);
+  if (ns == 2) return launch_co<ACT, WO, R, BF, 2>(a, B, s);
+  return launch_co<ACT, WO, R, BF, 4>(a, B, s);
 }
 
 template <int ACT, int BF>
