@@ -255,11 +255,19 @@ __global__ __launch_bounds__(256) void dense_kernel(DenseArgs a) {
   const int o = blockIdx.x * 256 + tid;
   if (o >= a.O) return;
   float acc = 0.f;
-  // 16 weight loads in flight per batch: a load per k-step consumed at once
-  // waited a full memory latency each; the K % 16 tail continues the same
-  // k-ordered chain (any ch the config check accepts, e.g. ch = 8 or 24)
-  const int K16 = K & ~15;
-  for (int k0 = 0; k0 < K16; k0 += 16) {
+  // 64 (then 16) weight loads in flight per batch: a load per k-step consumed
+  // at once waited a full memory latency each (K = 256: 4 latencies instead of
+  // 16, same k-ordered chain, bitwise equal); the K % 16 tail continues the
+  // same chain (any ch the config check accepts, e.g. ch = 8 or 24)
+  const int K64 = K & ~63, K16 = K & ~15;
+  for (int k0 = 0; k0 < K64; k0 += 64) {
+    float w[64];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) w[j] = a.wt[(size_t)(k0 + j) * a.O + o];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) acc = fmaf(xin[k0 + j], w[j], acc);
+  }
+  for (int k0 = K64; k0 < K16; k0 += 16) {
     float w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = a.wt[(size_t)(k0 + j) * a.O + o];
