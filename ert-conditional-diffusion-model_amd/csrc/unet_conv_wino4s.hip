@@ -17,7 +17,10 @@
 //     column half bit 4, tile bits 0-3), do GroupNorm + SiLU + B^T d B exactly
 //     as conv_wino4_kernel's producers (the half exchange is v_permlane16_swap:
 //     the halves are 16 lanes apart here);
-//   * 512 threads, 256 VGPRs per wave (2 waves per SIMD), 36 KB of LDS.
+//   * XS = 1: 512 threads, 256 VGPRs per wave (2 waves per SIMD), 36 KB of LDS;
+//   * XS = 2 (the default): each co block's 36 xi are split over two MFMA
+//     waves (8 MFMA waves, 768 threads, 163 VGPRs, 36 + 64 KB of LDS); the
+//     halves' partial output tiles meet in an LDS exchange buffer (below).
 // Item = (co group of 64, block of 16 consecutive tiles of one sample); the
 // output transform, bias / emb / residual epilogue and the GroupNorm partials
 // (one part per 16 tiles, as conv_wino4_kernel) are per MFMA wave.  No K split.
@@ -31,7 +34,7 @@ namespace unet {
 
 namespace {
 
-constexpr int NMW = 4;                        // MFMA waves (one per SIMD)
+constexpr int NMW = 4;                        // co blocks (MFMA waves at XS = 1, one per SIMD)
 constexpr int NPW = 4;                        // producer waves
 constexpr int CCH = 8;                        // input channels per chunk (2 MFMA k-steps)
 constexpr int NX = 36;
