@@ -127,6 +127,8 @@ hipError_t launch_pack_conv_wino4(const float* w, int cin, int cout, float* dst,
                                   bool flipT = false);
 hipError_t launch_conv_wino4(int act, const ConvArgs& a, int B, hipStream_t s, int cus);
 int wino4_tile_items(int cout, int wo, int B);
+// the F(4x4) register-weight kernel splits its K (given ConvArgs::ksplit_buf)
+bool wino4s_ksplit(int cin, int cout, int wo, int B);
 bool wino4_ksplit(int cin, int cout, int wo, int B);
 // F(4x4) with register-resident weights (unet_conv_wino4s.hip): items of 64 co x
 // 16 tiles (the 16x16 level fills the CUs at B = 64 without a K split); same

@@ -657,7 +657,7 @@ bool wino4s_ok(int cin, int ca, int cout, int wo, int B) {
   if (e == 2) return true;
   if (e == 3) return wo != 16;
   if (e == 4 && wo != 16) return true;
-  return wo == 16 && wino4s_items(cout, wo, B) >= cu_count();
+  return wo == 16 && (wino4s_items(cout, wo, B) >= cu_count() || wino4s_ksplit(cin, cout, wo, B));
 }
 
 bool wino4_ok(int cin, int ca, int cout, int wo, int B) {
@@ -669,7 +669,7 @@ bool wino4_ok(int cin, int ca, int cout, int wo, int B) {
 }
 
 bool wino4_ksplit(int cin, int cout, int wo, int B) {
-  if (wino4s_ok(cin, cin, cout, wo, B)) return false;
+  if (wino4s_ok(cin, cin, cout, wo, B)) return wino4s_ksplit(cin, cout, wo, B);
   const int nchunk = cin / 4;
   return nchunk % 2 == 0 && nchunk >= 4 && wino4_tile_items(cout, wo, B) < ksplit_items() * cu_count();
 }

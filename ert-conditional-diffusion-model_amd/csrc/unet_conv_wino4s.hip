@@ -83,14 +83,17 @@ __device__ __forceinline__ void at6(const f32x2 (&m)[6], f32x2 (&y)[4]) {
   y[3] = fmac(m[3], 0.125f, fmac(m[4], -8.f, d + m[5]));
 }
 
-// item it -> (co group, 16-tile block): co group fastest
+// item it -> (K half, co group, 16-tile block): the K halves of a (co group,
+// block) adjacent, then co group, then block
 struct Item {
-  int cog, blk;
+  int cog, blk, half;
 };
-__device__ __forceinline__ Item item_of(int it, int ncog) {
+__device__ __forceinline__ Item item_of(int it, int ncog, int ksp) {
   Item r;
-  r.cog = it % ncog;
-  r.blk = it / ncog;
+  r.half = it % ksp;
+  const int pr = it / ksp;
+  r.cog = pr % ncog;
+  r.blk = pr / ncog;
   return r;
 }
 
@@ -105,7 +108,7 @@ __device__ __forceinline__ Item item_of(int it, int ncog) {
 // of its rows, the halves are exchanged through LDS across the item's last
 // barrier, and each wave finishes two of the lane's four channels
 template <int WO, int ACT, bool UP, int XS>
-__global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvArgs a, int nitems) {
+__global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvArgs a, int nitems, int ksp) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* vbuf = smem;                  // [2][V_FL]
 
@@ -119,7 +122,10 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Cin = a.Cin, Ca = a.Ca;
-  const int nchunk = Cin / CCH;
+  // ksp = 2 (XS = 2 only): an item runs half of the input channels, the
+  // second half's sums go to a.ksplit_buf (no bias / emb / residual) and are
+  // added by a separate pass -- layers whose items would fill only half the CUs
+  const int nchunk = Cin / CCH / ksp;          // chunks per item
   const int ncog = a.Cout / 64;
   const int bid = blockIdx.x, G = gridDim.x;
   const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;
@@ -138,11 +144,12 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     float2 raw[NRS][6];
     float2 gnv[NRS];
     f32x4 pad[NRS];
-    int cur_g = 0, cur_k = 0, cur_b = 0, cur_il = 0;
+    int cur_g = 0, cur_k = 0, cur_b = 0, cur_il = 0, cur_k0 = 0;
     unsigned roff[6];   // per window row (UP: per distinct source row, 4)
     f32x4 cur_pad;
     auto set_item = [&](int il) {
-      const Item itm = item_of(bid + il * G, ncog);
+      const Item itm = item_of(bid + il * G, ncog, ksp);
+      cur_k0 = itm.half * nchunk;
       const int flat0 = itm.blk * 16;
       cur_b = flat0 / TS;
       const int tg = flat0 % TS + t;
@@ -165,7 +172,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     };
     const int glast = gtot - 1;
     auto load_next = [&](const int set) {
-      const int cg = cur_k * CCH + 2 * q;     // wave-uniform first channel of the pair
+      const int cg = (cur_k0 + cur_k) * CCH + 2 * q;   // wave-uniform first channel of the pair
       pad[set] = cur_pad;
       if constexpr (ACT != ACT_NONE) gnv[set] = a.gn[(size_t)cur_b * Cin + cg + chb];
       const bool inA = cg < Ca;               // Ca even: both channels on one side
@@ -316,7 +323,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   int u_il = 0, u_ks = 0;
   int u_base = 0;                              // byte offset of (cog, ks = 0) of item u_il
   auto u_item = [&](int il) {
-    const Item itm = item_of(bid + il * G, ncog);
+    const Item itm = item_of(bid + il * G, ncog, ksp);
     u_base = itm.cog * nks * 36864;
   };
   auto u_advance = [&]() {
@@ -427,7 +434,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
       continue;
     }
     // ---- output transform: lane l holds M[xi] of co = 16 cb + 4 (l >> 4) + i, tile l & 15
-    const Item itm = item_of(bid + il * G, ncog);
+    const Item itm = item_of(bid + il * G, ncog, ksp);
     const int flatw = itm.blk * 16;
     const int smpl = flatw / TS;
     const bool has_eb = a.ebias != nullptr, has_res = a.res != nullptr, has_bias = a.bias != nullptr;
@@ -531,18 +538,20 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   const int nks = Cin / 4;
   const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.wpk_wino4), (short)0, (int)((size_t)NX * a.Cout * Cin * 4), 0x00020000);
-  int u_il = 0, u_ks = 0, u_base = 0;
+  // U cursor over the item's k-steps [u_ks0, u_end) (its K half)
+  int u_il = 0, u_ks = 0, u_end = 0, u_base = 0;
   auto u_item = [&](int il) {
-    const Item itm = item_of(bid + il * G, ncog);
+    const Item itm = item_of(bid + il * G, ncog, ksp);
     u_base = itm.cog * nks * 36864;
+    u_ks = itm.half * nchunk * 2;
+    u_end = u_ks + nchunk * 2;
   };
   auto u_advance = [&]() {
-    if (++u_ks == nks) {
+    if (++u_ks == u_end) {
       if (u_il + 1 < nloc) {
-        u_ks = 0;
         u_item(++u_il);
       } else {
-        u_ks = nks - 1;
+        u_ks = u_end - 1;
       }
     }
   };
@@ -659,13 +668,15 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
           y[1][r][x + 1] = q1.y;
         }
     }
-    const Item itm = item_of(bid + il * G, ncog);
+    const Item itm = item_of(bid + il * G, ncog, ksp);
     const int flatw = itm.blk * 16;
     const int smpl = flatw / TS;
-    const bool has_eb = a.ebias != nullptr, has_res = a.res != nullptr, has_bias = a.bias != nullptr;
+    const bool part2 = itm.half != 0;          // second K half: raw sums to ksplit_buf
+    const bool has_eb = !part2 && a.ebias != nullptr, has_res = !part2 && a.res != nullptr,
+               has_bias = !part2 && a.bias != nullptr;
     const unsigned smp = (unsigned)(a.Cout * HW * 4);
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        a.out + (size_t)smpl * a.Cout * HW, (short)0, smp, 0x00020000);
+        (part2 ? a.ksplit_buf : a.out) + (size_t)smpl * a.Cout * HW, (short)0, smp, 0x00020000);
     const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
         has_res ? const_cast<float*>(a.res) + (size_t)smpl * a.Cout * HW : nullptr, (short)0, smp,
         0x00020000);
@@ -696,7 +707,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[i][r] = y[i][r] + rv[i][r];
     }
-    if (a.gnp) {
+    if (a.gnp && !part2) {
       float2 pr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -744,21 +755,50 @@ static int wino4s_xs() {
   return v;
 }
 
+}  // namespace
+
+// ERTD_WINO4S_KSPLIT=0: no K split (a 16x16 layer whose items fill only half
+// the CUs then runs F(2x2), as before)
+static int wino4s_ks_env() {
+  static const int v = [] {
+    const char* e = getenv("ERTD_WINO4S_KSPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// the xi-split kernel splits its K in two halves when its items fill half the
+// CUs or more but not all of them (the 16x16 level of the B = 32 train step:
+// 128 items of 64 co x 16 tiles for 256 CUs), given an even chunk count >= 4
+bool wino4s_ksplit(int cin, int cout, int wo, int B) {
+  if (!wino4s_ks_env() || wino4s_xs() != 2 || wo != 16 || cin % CCH || cout % 64) return false;
+  const int nchunk = cin / CCH;
+  const int items = wino4s_items(cout, wo, B), cus = device_cu_count();
+  return nchunk % 2 == 0 && nchunk >= 4 && items < cus && 2 * items >= cus;
+}
+
+namespace {
+
 template <int WO, int ACT, bool UP, int XS>
-hipError_t launch_wo4x(const ConvArgs& a, int B, hipStream_t s, int cus) {
+hipError_t launch_wo4x(const ConvArgs& a, int B, hipStream_t s, int cus, int ksp) {
   constexpr size_t lds = WLDS + (XS == 2 ? (size_t)4 * 2 * 8 * 256 * sizeof(float) : 0);
   static std::atomic<unsigned long long> attr{0};
   set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS>, (int)lds, attr);
-  const int nitems = wino4s_items(a.Cout, WO, B);
+  const int nitems = wino4s_items(a.Cout, WO, B) * ksp;
   const int grid = nitems < cus ? nitems : cus;
-  conv_wino4s_kernel<WO, ACT, UP, XS><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems);
-  return hipGetLastError();
+  conv_wino4s_kernel<WO, ACT, UP, XS><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || ksp == 1) return e;
+  return launch_add_inplace(a.out, a.ksplit_buf, (size_t)B * a.Cout * WO * WO, s);
 }
 
 template <int WO, int ACT, bool UP>
 hipError_t launch_wo4s(const ConvArgs& a, int B, hipStream_t s, int cus) {
-  if (wino4s_xs() == 2 && a.Cin >= 16) return launch_wo4x<WO, ACT, UP, 2>(a, B, s, cus);
-  return launch_wo4x<WO, ACT, UP, 1>(a, B, s, cus);
+  if (wino4s_xs() == 2 && a.Cin >= 16) {
+    const int ksp = !UP && a.ksplit_buf && wino4s_ksplit(a.Cin, a.Cout, WO, B) ? 2 : 1;
+    return launch_wo4x<WO, ACT, UP, 2>(a, B, s, cus, ksp);
+  }
+  return launch_wo4x<WO, ACT, UP, 1>(a, B, s, cus, 1);
 }
 
 template <int ACT>
