@@ -7,10 +7,28 @@
 // (B, C, H, W), contiguous.  The sampled variable x stays (B, H*W) = (B, P),
 // the reference's (B, param_dim) contract.
 #pragma once
+#include <cstdlib>
+
 #include "ertd_common.h"
+
+// Schedule knobs for same-box A/B: the shipped library compiles every default
+// in and reads no environment variable; only a diagnostic build (-DERTD_DIAG:
+// build.py --diag, tools/build_variant.sh) reads ERTD_<name> at first use.
+#ifdef ERTD_DIAG
+#define ERTD_KNOB(name, dflt) (::ertd::unet::diag_knob("ERTD_" name, (dflt)))
+#else
+#define ERTD_KNOB(name, dflt) (dflt)
+#endif
 
 namespace ertd {
 namespace unet {
+
+#ifdef ERTD_DIAG
+inline int diag_knob(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+#endif
 
 constexpr int NTHR = 256;   // conv workgroup: 4 waves, each a 64 (cout) x 64 (pixel) tile
 constexpr double GN_EPS = 1e-5;   // GroupNorm eps (oracle/unet_torch.py)

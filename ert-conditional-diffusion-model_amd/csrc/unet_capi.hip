@@ -250,8 +250,7 @@ struct Walk {
   bool has_pend = false;
   static bool fuse_gn_env() {
     static const bool v = [] {
-      const char* e = getenv("ERTD_UNET_BF16_FUSEGN");
-      return e ? atoi(e) != 0 : true;
+      return ERTD_KNOB("UNET_BF16_FUSEGN", 1) != 0;
     }();
     return v;
   }
@@ -267,8 +266,7 @@ struct Walk {
   std::map<const float*, PartRec> parts;
   static bool gn_fuse_env() {
     static const bool v = [] {
-      const char* e = getenv("ERTD_UNET_GNFUSE");
-      return e ? atoi(e) != 0 : true;
+      return ERTD_KNOB("UNET_GNFUSE", 1) != 0;
     }();
     return v;
   }
@@ -1196,8 +1194,8 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
   // branch's convs queue behind it and slow it (U2 B=64: 154.9 steps/s single
   // chain vs 152.6 forked); the bf16 path keeps it (U3 B=256: 94.0 vs 93.1).
   // ERTD_UNET_SIDE=0/1 overrides (A/B).
-  const char* sv = getenv("ERTD_UNET_SIDE");
-  const bool side = sv ? atoi(sv) != 0 : bf_prec(c->precision);
+  const int sv = ERTD_KNOB("UNET_SIDE", -1);
+  const bool side = sv >= 0 ? sv != 0 : bf_prec(c->precision);
   if (e == hipSuccess && side) {
     e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evf, hipEventDisableTiming);

@@ -52,8 +52,7 @@ namespace unet {
 // ERTD_UNET_TPX=1|2 forces the wave tile (diagnostics); 0 = automatic
 static int conv_tpx_override() {
   static int v = [] {
-    const char* e = getenv("ERTD_UNET_TPX");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("UNET_TPX", 0);
   }();
   return v;
 }
@@ -423,8 +422,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(ConvArgs a) {
 // ERTD_UNET_STAGE=0|1 picks the staging schedule (diagnostics); default 1
 static int conv_stage() {
   static int v = [] {
-    const char* e = getenv("ERTD_UNET_STAGE");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("UNET_STAGE", 1);
   }();
   return v;
 }
@@ -464,8 +462,7 @@ static hipError_t launch_p(const ConvArgs& a, int B, hipStream_t s) {
   if (tpx == 0) tpx = ((KS == 3 && MODE == MODE_S1) || MODE == MODE_UPP || KS == 1) ? 2 : 1;
   // ERTD_UNET_TPX1=1|2 picks the 1x1 convs' wave tile alone (A/B); 0 = the above
   static const int t1 = [] {
-    const char* e = getenv("ERTD_UNET_TPX1");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("UNET_TPX1", 0);
   }();
   if (KS == 1 && t1 > 0) tpx = t1;
   (void)wg2;
@@ -491,8 +488,7 @@ static hipError_t launch_w(const ConvArgs& a, int B, hipStream_t s) {
 // ERTD_UNET_WCO=1 forces 64-cout workgroups everywhere (diagnostics); 0 = automatic
 static int conv_wco_override() {
   static int v = [] {
-    const char* e = getenv("ERTD_UNET_WCO");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("UNET_WCO", 0);
   }();
   return v;
 }

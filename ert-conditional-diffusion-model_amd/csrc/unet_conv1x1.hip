@@ -161,8 +161,7 @@ hipError_t launch_p1(const ConvArgs& a, int B, hipStream_t s) {
 // chunks, 3 = at every eligible size (A/B)
 bool conv1x1_ok(const ConvArgs& a, int act, int B) {
   static const int env = [] {
-    const char* e = getenv("ERTD_CONV1X1");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("CONV1X1", 1);
   }();
   if (!env || act != ACT_NONE || a.res || a.ebias || a.gnp) return false;
   const int HW = a.Wo * a.Wo;
@@ -178,8 +177,7 @@ hipError_t launch_conv1x1(const ConvArgs& a, int B, hipStream_t s) {
   // 512-px items where they fill the CUs, else 256
   const long long items512 = (long long)B * HW / 512 * (a.Cout / 64);
   static const int env = [] {
-    const char* e = getenv("ERTD_CONV1X1");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("CONV1X1", 1);
   }();
   if (env == 2) {
     if (items512 >= device_cu_count()) return launch_p1<512, 8>(a, B, s);

@@ -654,8 +654,7 @@ static hipError_t launch_hgd(const ConvArgs& a, int B, hipStream_t s) {
 // (tools/build_variant.sh ... "-DERTD_DIAG"), never in the shipped one
 static int bf16_dbg() {
   static int v = [] {
-    const char* e = getenv("ERTD_BF16_DBG");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("BF16_DBG", 0);
   }();
   return v;
 }
@@ -683,8 +682,7 @@ static hipError_t launch_hg(const ConvArgs& a, int B, hipStream_t s) {
 // ERTD_UNET_BF16_PRE=0 keeps the register staging for stride-1 convs (diagnostics)
 static int convh_pre() {
   static int v = [] {
-    const char* e = getenv("ERTD_UNET_BF16_PRE");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("UNET_BF16_PRE", 1);
   }();
   return v;
 }
@@ -693,8 +691,7 @@ static int convh_pre() {
 // stride-1/upsample convs (diagnostics); 0 = automatic (512 at W = 32, 64)
 static int convh_tpx_override() {
   static int v = [] {
-    const char* e = getenv("ERTD_UNET_BF16_TPX");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("UNET_BF16_TPX", 0);
   }();
   return v;
 }
@@ -771,8 +768,7 @@ static hipError_t launch_hw(const ConvArgs& a, int B, hipStream_t s) {
   if constexpr (KS == 1) {
     // ERTD_UNET_BF16_TPX1=2: 256-pixel tiles for the 1x1 convs (A/B)
     static const int t1 = [] {
-      const char* e = getenv("ERTD_UNET_BF16_TPX1");
-      return e ? atoi(e) : 1;
+      return ERTD_KNOB("UNET_BF16_TPX1", 1);
     }();
     if (t1 == 2) return launch_hwt<KS, MODE, ACT, 2, SP>(a, B, s);
     return launch_hwt<KS, MODE, ACT, 1, SP>(a, B, s);

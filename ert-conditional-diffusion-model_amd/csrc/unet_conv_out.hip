@@ -232,8 +232,7 @@ hipError_t launch_co(const ConvArgs& a, int B, hipStream_t s) {
 // channel groups per workgroup (ERTD_CONV_OUT_NS, A/B; 1 = one 256-thread group)
 static int conv_out_ns() {
   static const int v = [] {
-    const char* e = getenv("ERTD_CONV_OUT_NS");
-    const int n = e ? atoi(e) : 4;
+    const int n = ERTD_KNOB("CONV_OUT_NS", 4);
     return n == 1 || n == 2 ? n : 4;
   }();
   return v;

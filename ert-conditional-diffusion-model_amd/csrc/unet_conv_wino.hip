@@ -80,8 +80,7 @@ __device__ __forceinline__ unsigned wlds_addr(const void* p) {
 
 int wino_env() {
   static int v = [] {
-    const char* e = getenv("ERTD_UNET_WINO");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("UNET_WINO", 1);
   }();
   return v;
 }
@@ -529,8 +528,7 @@ __global__ __launch_bounds__(WT) void conv_wino_kernel(ConvArgs a, int nitems, i
 // (tools/build_variant.sh ... "-DERTD_DIAG"), never in the shipped one
 int wino_dbg() {
   static int v = [] {
-    const char* e = getenv("ERTD_WINO_DBG");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("WINO_DBG", 0);
   }();
   return v;
 }
@@ -549,8 +547,7 @@ __global__ void add_inplace_kernel(float* __restrict__ out, const float* __restr
 // K split when a layer has fewer tile items than ERTD_WINO_KSPLIT x CUs (default 1)
 int ksplit_items() {
   static int v = [] {
-    const char* e = getenv("ERTD_WINO_KSPLIT");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("WINO_KSPLIT", 1);
   }();
   return v;
 }
@@ -632,8 +629,7 @@ hipError_t launch_add_inplace(float* out, const float* part, size_t n, hipStream
 // ERTD_WINO4_W16=1: F(4x4) at 16x16 for every even batch (K split), A/B only
 static int wino4_w16_env() {
   static int v = [] {
-    const char* e = getenv("ERTD_WINO4_W16");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("WINO4_W16", 0);
   }();
   return v;
 }
@@ -644,8 +640,7 @@ static int wino4_w16_env() {
 // (same box): 204.3 steps/s off, 222.1 (1), 224.2 (2), 205.9 (3).
 static int wino4s_env() {
   static int v = [] {
-    const char* e = getenv("ERTD_WINO4S");
-    return e ? atoi(e) : 4;
+    return ERTD_KNOB("WINO4S", 4);
   }();
   return v;
 }

@@ -675,8 +675,7 @@ hipError_t launch_wo4d(const ConvArgs& a, int B, hipStream_t s, int cus) {
 // (tools/build_variant.sh ... "-DERTD_DIAG"), never in the shipped one
 int wino4_dbg() {
   static int v = [] {
-    const char* e = getenv("ERTD_WINO4_DBG");
-    return e ? atoi(e) : 0;
+    return ERTD_KNOB("WINO4_DBG", 0);
   }();
   return v;
 }

@@ -749,8 +749,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
 // item boundary only after a barrier that every wave passes between the two uses
 static int wino4s_xs() {
   static const int v = [] {
-    const char* e = getenv("ERTD_WINO4S_XS");
-    return e ? atoi(e) : 2;
+    return ERTD_KNOB("WINO4S_XS", 2);
   }();
   return v;
 }
@@ -761,8 +760,7 @@ static int wino4s_xs() {
 // the CUs then runs F(2x2), as before)
 static int wino4s_ks_env() {
   static const int v = [] {
-    const char* e = getenv("ERTD_WINO4S_KSPLIT");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("WINO4S_KSPLIT", 1);
   }();
   return v;
 }
@@ -818,8 +816,7 @@ int wino4s_items(int cout, int wo, int B) { return (wo / 4) * (wo / 4) / 16 * B 
 // ERTD_WINO4S_UP=0 keeps the sub-pixel direct kernel for the Upsample convs (A/B)
 bool wino4s_up_ok(int cin, int ca, int cout, int wo, int B) {
   static const int env = [] {
-    const char* e = getenv("ERTD_WINO4S_UP");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("WINO4S_UP", 1);
   }();
   return env != 0 && wino4s_ok(cin, ca, cout, wo, B) && (wo == 16 || wo == 32 || wo == 64);
 }

@@ -306,10 +306,6 @@ int n_cu() {
   return v;
 }
 
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 
 struct Plan {
   int Ho, R, nco, nci, ntiles, nchunks, cps, nsplit;
@@ -334,7 +330,7 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
   if (ks == 1 && Ho * Ho < PXC) return false;
   // about 4 workgroups per CU, >= 4 chunks per range (measured optimum at
   // U2 B=32 of the partial write + reduce traffic vs occupancy: tools/wgrad_sweep.sh)
-  static const int wpc = env_int("ERTD_WGRAD_WPC", 4), min_cps = env_int("ERTD_WGRAD_CPS", 4);
+  static const int wpc = ERTD_KNOB("WGRAD_WPC", 4), min_cps = ERTD_KNOB("WGRAD_CPS", 4);
   const int want = (wpc * n_cu() + p->ntiles - 1) / p->ntiles;
   int cps = (p->nchunks + want - 1) / want;
   if (cps < min_cps) cps = min_cps;

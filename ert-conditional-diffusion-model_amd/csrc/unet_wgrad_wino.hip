@@ -298,8 +298,7 @@ __global__ __launch_bounds__(256) void wgw_final_kernel(WgwArgs a, float* dw, in
 
 int wgw_env() {
   static const int v = [] {
-    const char* e = getenv("ERTD_WGRAD_WINO");
-    return e ? atoi(e) : 1;
+    return ERTD_KNOB("WGRAD_WINO", 1);
   }();
   return v;
 }
@@ -316,8 +315,7 @@ bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
   const int base = NX * (Cout / 64) * (Cin / 64);
   const int nq = T / 16;                         // 16-k blocks
   static const int target = [] {                 // ERTD_WGW_TASKS: wave-task target (A/B)
-    const char* e = getenv("ERTD_WGW_TASKS");
-    const int v = e ? atoi(e) : 2048;
+    const int v = ERTD_KNOB("WGW_TASKS", 2048);
     return v > 0 ? v : 2048;
   }();
   int nks = (target + base - 1) / base;          // ~2048 wave tasks (8 waves per CU)

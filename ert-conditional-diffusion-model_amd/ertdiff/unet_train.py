@@ -35,7 +35,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 from typing import Dict, Optional
 
 import torch
@@ -128,7 +127,7 @@ def _packs_of(model, B) -> _PackRegistry:
 class _K:
     """Thin wrappers: each is one or two HIP kernel launches (raise on error)."""
 
-    def __init__(self, dev, packs: Optional[_PackRegistry] = None):
+    def __init__(self, dev, packs: Optional[_PackRegistry] = None, defer: bool = True):
         self.dev = dev
         self.lib = _lib.lib()
         self.s = _lib.stream_of(dev)
@@ -137,8 +136,8 @@ class _K:
         self.packs = packs
         # GroupNorm dgamma/dbeta row reductions, launched together by
         # flush_reductions() at the end of the backward walk (nothing reads them
-        # before the optimizer); ERTD_DEFER_REDUCE=0 launches each one in place
-        self.deferred = [] if os.environ.get("ERTD_DEFER_REDUCE", "1") != "0" else None
+        # before the optimizer); defer=False launches each one in place
+        self.deferred = [] if defer else None
 
     def empty(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)

@@ -227,12 +227,17 @@ def test_unet_sampler_golden_fixture_shape(unet_sampler_kat):
 
 
 def test_shipped_library_has_no_diagnostic_variants():
-    """The wrong-result ablation variants (ERTD_*_DBG knobs) exist only in a
-    diagnostic build (-DERTD_DIAG): an inherited environment variable cannot
-    change what the shipped library computes."""
+    """The wrong-result ablation variants (ERTD_*_DBG knobs) and every schedule
+    A/B knob exist only in a diagnostic build (-DERTD_DIAG, csrc/unet.h
+    ERTD_KNOB): the shipped library reads no ERTD_* environment variable, so
+    an inherited variable cannot move it onto an untested path.  (ERTD_LIB_PATH
+    is read by the Python loader, not by the library.)"""
     data = open(_lib.LIB_PATH, "rb").read()
-    for knob in (b"ERTD_WINO4_DBG", b"ERTD_WINO_DBG", b"ERTD_BF16_DBG"):
-        assert knob not in data, knob
+    names = sorted(set(re.findall(rb"ERTD_[A-Z0-9_]{2,}", data)))
+    assert names == [], names
+    assert b"getenv" not in data
+    src = open(os.path.join(ROOT, "ert-conditional-diffusion-model_amd", "ertdiff", "unet_train.py")).read()
+    assert "environ" not in src
 
 
 def test_conv2d_workspace_covers_launch_scratch():

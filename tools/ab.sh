@@ -5,11 +5,13 @@
 #
 # Runs tools/unet_probe.py once per value of $VAR (each run under its own
 # time limit; stops at the first failure) and prints the probe's summary line.
-# Knobs read by the library: ERTD_UNET_SIDE (skip-conv graph branch),
-# ERTD_UNET_TPX / ERTD_UNET_WCO / ERTD_UNET_STAGE (fp32 conv tiling),
-# ERTD_UNET_BF16_FUSEGN (fused bf16 GN prologue), ERTD_UNET_WINO (Winograd).
+# The knobs (ERTD_UNET_SIDE, ERTD_WINO4S*, ERTD_UNET_TPX, ...: csrc/unet.h
+# ERTD_KNOB) are read only by the diagnostic build, which this script loads:
+# build it first on the CPU side (build.py --diag).  VAR=ERTD_LIB_PATH compares
+# variant libraries (tools/build_variant.sh) instead.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
+[ "${VAR:-}" != ERTD_LIB_PATH ] && export ERTD_LIB_PATH=$PWD/ert-conditional-diffusion-model_amd/ertdiff/libertdiff_hip_diag.so
 VAR=${VAR:?set VAR to the environment variable to vary}
 for v in ${VALUES:?set VALUES}; do
   env "$VAR=$v" timeout -k 10 300 python3 tools/unet_probe.py --config "${CFG:-U2}" --B "${B:-64}" \

@@ -1,12 +1,13 @@
 #!/bin/bash
 # Winograd conv chunk-time breakdown (diagnostic): ERTD_WINO_DBG variants of one
 # 64->64 64x64 B=64 GN+SiLU layer under rocprofv3 --kernel-trace; prints the
-# conv_wino_kernel average per variant.
+# conv_wino_kernel average per variant.  The variants exist only in the
+# diagnostic build (build.py --diag), which this script loads.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 for v in ${VALUES:-0 1 2 4 8 6 7}; do
   d=gpurun_out/wdbg_$v; rm -rf "$d"
-  env "${DBGVAR:-ERTD_WINO_DBG}=$v" timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$d" -o run \
+  env ERTD_LIB_PATH=$PWD/ert-conditional-diffusion-model_amd/ertdiff/libertdiff_hip_diag.so "${DBGVAR:-ERTD_WINO_DBG}=$v" timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$d" -o run \
     -- python3 tools/conv_probe.py ${PROBE_ARGS:-} > "$d.log" 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "[dbg=$v] rc=$rc"; tail -3 "$d.log"; exit $rc; }
   f=$(find "$d" -name '*kernel_trace.csv' | head -1)
