@@ -86,9 +86,13 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
                    long long cstride, int B, int L, int num_steps, int t_first, int n_run,
                    const float* c1, const float* c2, const float* sigma, const float* freq,
                    const float* noise, uint64_t seed, uint32_t member_offset, int mode,
-                   int precision, float* x_inout, void* ws, size_t ws_bytes, hipStream_t s) {
+                   int precision, float* x_inout, void* ws, size_t ws_bytes, hipStream_t s,
+                   int ncond = 0, int id_period = 0) {
   if (!weights_ok(w) || !packed || !cond || !c1 || !c2 || !sigma || !freq || !x_inout || !ws)
     return ERTD_EINVAL;
+  // ncond > 0 (ertd_sample_conditions): member b = realisation b / ncond of
+  // condition b % ncond, Philox id member_id(member_offset, b, ncond, id_period)
+  if (ncond < 0 || (ncond > 0 && (B % ncond || id_period < ncond || cstride == 0))) return ERTD_EINVAL;
   if (B < 1 || L < 1 || num_steps < 1 ||
       (mode != ERTD_MODE_HOISTED && mode != ERTD_MODE_FAITHFUL && mode != ERTD_MODE_FAITHFUL_STEPS))
     return ERTD_EINVAL;
@@ -100,12 +104,17 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
   const int t_last = t_first - n_run + 1;
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
   if (mode == ERTD_MODE_HOISTED) {
-    ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, cstride, B, L, precision,
+    // the encoder depends on the condition only: once per condition (ncond
+    // rows, each member reads row b % ncond) -- bitwise the rows it would
+    // compute per member
+    const int nenc = ncond > 0 ? ncond : B;
+    ERTD_TRY(launch_encoder_strips(packed, w->enc0_b, w->enc2_b, cond, cstride, nenc, L, precision,
                                    W.partial, s));
-    ERTD_TRY(launch_hoist_prep(*w, packed, W.partial, S, L2, B, W.U, W.cond_emb, s));
+    ERTD_TRY(launch_hoist_prep(*w, packed, W.partial, S, L2, nenc, W.U, W.cond_emb, s));
     ERTD_TRY(launch_time_table(*w, packed, freq, t_last, n_run, W.V, s));
     ERTD_TRY(launch_hoisted_sampler(*w, packed, W.U, W.V, c1, c2, sigma, noise, num_steps, t_first,
-                                    n_run, seed, member_offset, B, x_inout, s));
+                                    n_run, seed, member_offset, B, x_inout, s, ncond, id_period,
+                                    ncond));
     return ERTD_OK;
   }
   // Faithful mode: every step re-runs the full condition encoder and the
@@ -133,6 +142,8 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
       fa.noise = noise;
       fa.seed = seed;
       fa.member_offset = member_offset;
+      fa.ncond = ncond;
+      fa.id_period = id_period;
       fa.x = x_inout;
       fa.part = W.ring;
       fa.cnt = W.sync;
@@ -165,6 +176,8 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
   a.num_steps = num_steps;
   a.seed = seed;
   a.member_offset = member_offset;
+  a.ncond = ncond;
+  a.id_period = id_period;
   a.B = B;
   a.x_out = x_inout;
   // Each step's encoder launch also computes v(t) (the time branch, identical
@@ -174,7 +187,7 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
     a.t_scalar = t;
     tr.t = t;
     ERTD_TRY(launch_encoder_strips_t(packed, w->enc0_b, w->enc2_b, cond, cstride, B, L, precision,
-                                     W.partial, tr, s));
+                                     W.partial, tr, s, ncond));
     ERTD_TRY(launch_head_step(*w, packed, a, W.V, s));
   }
   return ERTD_OK;
@@ -334,12 +347,13 @@ int ertd_postprocess(const float* u, long long rows, int P, double a, double b,
                             (hipStream_t)stream));
 }
 
-int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const float* cond,
-                            long long cond_stride, int B, int L, int num_steps, int t_first,
-                            int n_run, const float* c1, const float* c2, const float* sigma,
-                            const float* freq, const float* noise, uint64_t seed,
-                            uint32_t member_offset, int mode, int precision, float* x_inout,
-                            void* ws, size_t ws_bytes, ertd_plan** plan) {
+}  // extern "C"
+
+namespace {
+
+// one sampler call captured as a graph on the plan's own stream
+template <class Enqueue>
+int capture_plan(ertd_plan** plan, Enqueue&& enqueue) {
   if (!plan) return ERTD_EINVAL;
   *plan = nullptr;
   ertd_plan* p = new (std::nothrow) ertd_plan();
@@ -354,9 +368,7 @@ int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const fl
     ertd_plan_destroy(p);
     return (int)e;
   }
-  const int r = enqueue_sample(w, packed, cond, cond_stride, B, L, num_steps, t_first, n_run, c1,
-                               c2, sigma, freq, noise, seed, member_offset, mode, precision,
-                               x_inout, ws, ws_bytes, p->stream);
+  const int r = enqueue(p->stream);
   e = hipStreamEndCapture(p->stream, &p->graph);
   if (r != ERTD_OK || e != hipSuccess) {
     ertd_plan_destroy(p);
@@ -369,6 +381,62 @@ int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const fl
   }
   *plan = p;
   return ERTD_OK;
+}
+
+// ertd_sample_conditions' geometry checks; returns B = n_cond * n_samples or 0
+int conditions_batch(int n_cond, int n_samples, long long id_period) {
+  if (n_cond < 1 || n_samples < 1 || id_period < n_cond || id_period > 0x7fffffff) return 0;
+  const long long B = (long long)n_cond * n_samples;
+  return B > (1 << 30) ? 0 : (int)B;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const float* cond,
+                            long long cond_stride, int B, int L, int num_steps, int t_first,
+                            int n_run, const float* c1, const float* c2, const float* sigma,
+                            const float* freq, const float* noise, uint64_t seed,
+                            uint32_t member_offset, int mode, int precision, float* x_inout,
+                            void* ws, size_t ws_bytes, ertd_plan** plan) {
+  return capture_plan(plan, [&](hipStream_t s) {
+    return enqueue_sample(w, packed, cond, cond_stride, B, L, num_steps, t_first, n_run, c1, c2,
+                          sigma, freq, noise, seed, member_offset, mode, precision, x_inout, ws,
+                          ws_bytes, s);
+  });
+}
+
+int ertd_sample_conditions(const ertd_weights* w, const float* packed, const float* cond, int n_cond,
+                           int n_samples, long long id_period, int L, int num_steps, int t_first,
+                           int n_run, const float* c1, const float* c2, const float* sigma,
+                           const float* freq, const float* noise, uint64_t seed,
+                           uint32_t member_offset, int mode, int precision, float* x_inout, void* ws,
+                           size_t ws_bytes, void* stream) {
+  const int B = conditions_batch(n_cond, n_samples, id_period);
+  if (!B) return ERTD_EINVAL;
+  return enqueue_sample(w, packed, cond, (long long)CIN * L, B, L, num_steps, t_first, n_run, c1, c2,
+                        sigma, freq, noise, seed, member_offset, mode, precision, x_inout, ws,
+                        ws_bytes, (hipStream_t)stream, n_cond, (int)id_period);
+}
+
+int ertd_sample_conditions_plan_create(const ertd_weights* w, const float* packed, const float* cond,
+                                       int n_cond, int n_samples, long long id_period, int L,
+                                       int num_steps, int t_first, int n_run, const float* c1,
+                                       const float* c2, const float* sigma, const float* freq,
+                                       const float* noise, uint64_t seed, uint32_t member_offset,
+                                       int mode, int precision, float* x_inout, void* ws,
+                                       size_t ws_bytes, ertd_plan** plan) {
+  const int B = conditions_batch(n_cond, n_samples, id_period);
+  if (!B) {
+    if (plan) *plan = nullptr;
+    return ERTD_EINVAL;
+  }
+  return capture_plan(plan, [&](hipStream_t s) {
+    return enqueue_sample(w, packed, cond, (long long)CIN * L, B, L, num_steps, t_first, n_run, c1,
+                          c2, sigma, freq, noise, seed, member_offset, mode, precision, x_inout, ws,
+                          ws_bytes, s, n_cond, (int)id_period);
+  });
 }
 
 int ertd_plan_launch(ertd_plan* plan, void* stream) {

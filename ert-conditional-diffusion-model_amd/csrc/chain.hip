@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   if ((int)blockIdx.x < B) {
     // ======================= chain block: member b =======================
     const int b = blockIdx.x;
-    const uint32_t member = a.member_offset + (uint32_t)b;
+    const uint32_t member = member_id(a.member_offset, b, a.ncond, a.id_period);
     const int xj = tid >> 1, xc = tid & 1;                             // mlp.0 x-part
     const int eo = tid >> 3, ehf = (tid >> 2) & 1, ei = tid & 3;       // mlp.2 chains
     const bool updater = ehf == 0 && ei == 0 && eo < P;
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     const unsigned long long wt1_ = __builtin_amdgcn_s_memrealtime();
     if (tid == 0 && b == 0 && item < 4096) g_item[item][1] = wt1_;
 #endif
-    enc_strip_fp32<false>(sm.enc, pk, w.enc0_b + z0, w.enc2_b + z0, a.cond, a.cstride, a.L, L1, L2, b, s,
+    enc_strip_fp32<false>(sm.enc, pk, w.enc0_b + z0, w.enc2_b + z0, a.cond, a.cstride, a.L, L1, L2, b, cond_row(b, a.ncond), s,
                           nullptr, nullptr, tid_i);
     WACC(2, wt1_);
 #ifdef ERTD_CHAIN_STAMPS

@@ -48,7 +48,7 @@ __device__ __forceinline__ void enc_strip_fp32(EncSmem& sm, const float* __restr
                                                const float* __restrict__ b1,
                                                const float* __restrict__ b2,
                                                const float* __restrict__ cond, long long cstride,
-                                               int L, int L1, int L2, int b, int strip,
+                                               int L, int L1, int L2, int b, int crow, int strip,
                                                float* __restrict__ a1out,
                                                unsigned char* __restrict__ m2out, int tid) {
   const int lane = tid & 63, wave = tid >> 6;
@@ -60,7 +60,7 @@ __device__ __forceinline__ void enc_strip_fp32(EncSmem& sm, const float* __restr
   for (int s = 0; s < STEPS1; ++s) a1[s] = packed[PACK_W1 + s * 64 + lane];
 
   // ---- stage cond[b][:, 4j0-3 : 4j0-3+260] into the 4-phase image (zero padded)
-  const float* cb = cond + (long long)b * cstride;
+  const float* cb = cond + (long long)crow * cstride;   // crow: b, or b % ncond
   if constexpr ((ERTD_ENC_ABLATE & 1) != 0) {
     for (int c = 0; c < CIN; ++c) sm.X[tid & 3][c][tid >> 2] = (float)(c + b);
   } else {

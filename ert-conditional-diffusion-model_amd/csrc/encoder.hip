@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
                                                        int S, float* __restrict__ partial,
                                                        float* __restrict__ a1out,
                                                        unsigned char* __restrict__ m2out,
-                                                       int nstrip, TimeRowArgs tr) {
+                                                       int nstrip, TimeRowArgs tr, int ncond) {
   __shared__ EncSmem sm;
   const int tid = threadIdx.x;
   if (!TRAIN && (int)blockIdx.x >= nstrip) {
@@ -153,7 +153,8 @@ __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__
     return;
   }
   const int b = blockIdx.x / S, strip = blockIdx.x - b * S;
-  enc_strip_fp32<TRAIN>(sm, packed, b1, b2, cond, cstride, L, L1, L2, b, strip, a1out, m2out, tid);
+  enc_strip_fp32<TRAIN>(sm, packed, b1, b2, cond, cstride, L, L1, L2, b, cond_row(b, ncond), strip, a1out,
+                        m2out, tid);
   if (tid < C2) partial[((size_t)b * S + strip) * C2 + tid] = sm.red[0][tid] + sm.red[1][tid];
   if (!TRAIN && tr.V) {
     // Warm this XCD's L2 with a slice of the weights the next head_step reads
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256) void enc_bf16_kernel(const float* __restrict__
                                                        const float* __restrict__ cond,
                                                        long long cstride, int L, int L1, int L2,
                                                        int S,
-                                                       float* __restrict__ partial) {
+                                                       float* __restrict__ partial, int ncond) {
   __shared__ EncSmemH sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(256) void enc_bf16_kernel(const float* __restrict__
   const int j0 = strip * J;
   const bf16x8* ph = reinterpret_cast<const bf16x8*>(packed + PACKH_OFF);
 
-  const float* cb = cond + (long long)b * cstride;
+  const float* cb = cond + (long long)cond_row(b, ncond) * cstride;
   stage_cond(sm.X, cb, L, 4 * j0 - 3, tid, [](float v) { return f2bf(v); });
   __syncthreads();
 
@@ -292,29 +293,29 @@ __global__ __launch_bounds__(256) void enc_bf16_kernel(const float* __restrict__
 
 hipError_t launch_encoder_strips(const float* packed, const float* b1, const float* b2,
                                  const float* cond, long long cstride, int B, int L, int precision,
-                                 float* partial, hipStream_t s) {
+                                 float* partial, hipStream_t s, int ncond) {
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
   const dim3 grid((unsigned)(B * S));
   if (precision == ERTD_PREC_BF16)
-    enc_bf16_kernel<<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S, partial);
+    enc_bf16_kernel<<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S, partial, ncond);
   else
     enc_fp32_kernel<false><<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S,
-                                                 partial, nullptr, nullptr, B * S, TimeRowArgs{});
+                                                 partial, nullptr, nullptr, B * S, TimeRowArgs{}, ncond);
   return hipGetLastError();
 }
 
 hipError_t launch_encoder_strips_t(const float* packed, const float* b1, const float* b2,
                                    const float* cond, long long cstride, int B, int L,
                                    int precision, float* partial, const TimeRowArgs& tr,
-                                   hipStream_t s) {
+                                   hipStream_t s, int ncond) {
   if (precision == ERTD_PREC_BF16) {  // bf16 strips + the time row as its own launch
-    hipError_t e = launch_encoder_strips(packed, b1, b2, cond, cstride, B, L, precision, partial, s);
+    hipError_t e = launch_encoder_strips(packed, b1, b2, cond, cstride, B, L, precision, partial, s, ncond);
     if (e != hipSuccess) return e;
     return launch_time_table(tr.w, packed, tr.freq, tr.t, 1, tr.V, s);
   }
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
   enc_fp32_kernel<false><<<dim3((unsigned)(B * S + 1)), 256, 0, s>>>(
-      packed, b1, b2, cond, cstride, L, L1, L2, S, partial, nullptr, nullptr, B * S, tr);
+      packed, b1, b2, cond, cstride, L, L1, L2, S, partial, nullptr, nullptr, B * S, tr, ncond);
   return hipGetLastError();
 }
 
@@ -324,7 +325,7 @@ hipError_t launch_encoder_train(const float* packed, const float* b1, const floa
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
   enc_fp32_kernel<true><<<dim3((unsigned)(B * S)), 256, 0, s>>>(
       packed, b1, b2, cond, (long long)CIN * L, L, L1, L2, S, partial, a1, m2, B * S,
-      TimeRowArgs{});
+      TimeRowArgs{}, 0);
   return hipGetLastError();
 }
 

@@ -201,9 +201,11 @@ hipError_t launch_pack_encoder_convs(const float* w0, const float* w2, float* pa
 hipError_t launch_encoder_train(const float* packed, const float* b1, const float* b2,
                                 const float* cond, int B, int L, float* partial, float* a1,
                                 unsigned char* m2, hipStream_t s);
+// ncond > 0: member b reads condition row b % ncond (a many-condition launch,
+// ertd_sample_conditions); 0: row b
 hipError_t launch_encoder_strips(const float* packed, const float* b1, const float* b2,
                                  const float* cond, long long cstride, int B, int L,
-                                 int precision, float* partial, hipStream_t s);
+                                 int precision, float* partial, hipStream_t s, int ncond = 0);
 // conv part of the encoder backward given g = dL/d(pool mean) / L2 (B, 64)
 // (train.hip; the U-Net train step)
 size_t encoder_bwd_ws_floats(int B, int L);
@@ -213,6 +215,17 @@ hipError_t launch_encoder_conv_backward(const float* packed, const float* cond, 
                                         hipStream_t s);
 // Same, plus one extra block computing the time row v(t) = W0t.relu(Wt.e(t)+bt)
 // into V[t] (faithful sampler: the row the next head_step launch consumes).
+// Member b of a many-condition launch (ertd_sample_conditions): realisation
+// r = b / ncond of local condition b % ncond; its Philox member id is
+// member_offset + r * id_period + b % ncond (id_period = the global condition
+// count, so a rank holding a slice of the conditions keeps every member's
+// global id).  ncond <= 0: a plain launch, id = member_offset + b.
+__host__ __device__ inline uint32_t member_id(uint32_t member_offset, int b, int ncond, int id_period) {
+  if (ncond <= 0) return member_offset + (uint32_t)b;
+  const int r = b / ncond;
+  return member_offset + (uint32_t)r * (uint32_t)id_period + (uint32_t)(b - r * ncond);
+}
+__host__ __device__ inline int cond_row(int b, int ncond) { return ncond > 0 ? b % ncond : b; }
 struct TimeRowArgs {
   ertd_weights w;
   const float* freq;
@@ -222,7 +235,7 @@ struct TimeRowArgs {
 hipError_t launch_encoder_strips_t(const float* packed, const float* b1, const float* b2,
                                    const float* cond, long long cstride, int B, int L,
                                    int precision, float* partial, const TimeRowArgs& tr,
-                                   hipStream_t s);
+                                   hipStream_t s, int ncond = 0);
 struct HeadArgs {
   const float* partial; int S; int L2;
   const float* freq;
@@ -230,6 +243,7 @@ struct HeadArgs {
   const float* c1; const float* c2; const float* sigma; const float* noise;
   int num_steps; uint64_t seed; uint32_t member_offset; int B;
   float* x_out; float* eps_out; float* cond_emb_out; float* t_emb_out;
+  int ncond; int id_period;      // Philox ids of a many-condition launch (member_id); 0 = plain
 };
 hipError_t launch_head(const ertd_weights& w, const float* packed, const HeadArgs& a, hipStream_t s);
 // faithful step: per-member condition branch + step for a.t_scalar using V[t]
@@ -243,7 +257,8 @@ hipError_t launch_hoisted_sampler(const ertd_weights& w, const float* packed, co
                                   const float* V, const float* c1, const float* c2,
                                   const float* sigma, const float* noise, int num_steps,
                                   int t_first, int n_run, uint64_t seed, uint32_t member_offset,
-                                  int B, float* x, hipStream_t s);
+                                  int B, float* x, hipStream_t s, int ncond = 0, int id_period = 0,
+                                  int u_rows = 0);
 hipError_t launch_timestep_embedding(const int64_t* t, int B, int dim, const float* freq,
                                      float* out, hipStream_t s);
 hipError_t launch_q_sample(const float* x0, const int64_t* t, const float* noise,
@@ -259,6 +274,7 @@ struct FaithfulChainArgs {
   int n_run; int t_first; int num_steps;
   const float* c1; const float* c2; const float* sigma; const float* freq; const float* noise;
   uint64_t seed; uint32_t member_offset;
+  int ncond; int id_period;      // condition row b % ncond, Philox member_id (0 = plain)
   float* x;                      // (B, P) in/out
   float* part;                   // R ring slots of (B, S, 64) strip partials
   // sync words, one per SYNC_PAD-word line:

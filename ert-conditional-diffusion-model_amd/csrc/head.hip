@@ -66,7 +66,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void head_kernel(ertd_weights w,
     xv = o < P ? a.x_in[(size_t)b * P + o] : 0.f;
     bo = o < P ? w.mlp2_b[o] : 0.f;
     if (!a.eps_out) {
-      z = step_noise(a.noise, a.num_steps, ts, a.B, b, P, o, a.seed, a.member_offset + (uint32_t)b);
+      z = step_noise(a.noise, a.num_steps, ts, a.B, b, P, o, a.seed, member_id(a.member_offset, b, a.ncond, a.id_period));
       c1 = a.c1[ts];
       c2 = a.c2[ts];
       sig = a.sigma[ts];
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(HEAD_STEP_THREADS) void head_step_kernel(
   if (step_wave) {  // the step's weights and inputs, requested at kernel start
     load_step_regs(R, packed, w.mlp2_b, P, lane);
     xv = o < P ? a.x_in[(size_t)b * P + o] : 0.f;
-    z = step_noise(a.noise, a.num_steps, ts, a.B, b, P, o, a.seed, a.member_offset + (uint32_t)b);
+    z = step_noise(a.noise, a.num_steps, ts, a.B, b, P, o, a.seed, member_id(a.member_offset, b, a.ncond, a.id_period));
     c1 = a.c1[ts];
     c2 = a.c2[ts];
     sig = a.sigma[ts];
@@ -263,7 +263,8 @@ __global__ __launch_bounds__(256) void hoisted_sampler_kernel(
     ertd_weights w, const float* __restrict__ packed, const float* __restrict__ U,
     const float* __restrict__ V, const float* __restrict__ c1, const float* __restrict__ c2,
     const float* __restrict__ sigma, const float* __restrict__ noise, int num_steps, int t_first,
-    int n_run, uint64_t seed, uint32_t member_offset, int B, float* __restrict__ x) {
+    int n_run, uint64_t seed, uint32_t member_offset, int B, float* __restrict__ x, int ncond,
+    int id_period, int u_rows) {
   __shared__ float hbuf[4][H];
   __shared__ float xbuf[4][PMAX];
   const int lane = threadIdx.x & 63;
@@ -272,10 +273,13 @@ __global__ __launch_bounds__(256) void hoisted_sampler_kernel(
   const int P = w.param_dim;
   StepRegs R;
   load_step_regs(R, packed, w.mlp2_b, P, lane);
-  const float u_lo = U[(size_t)b * H + lane];
-  const float u_hi = U[(size_t)b * H + 64 + lane];
+  // u_rows > 0: one condition row per condition (the encoder ran once per
+  // condition), member b reads row b % u_rows
+  const int ur = u_rows > 0 ? b % u_rows : b;
+  const float u_lo = U[(size_t)ur * H + lane];
+  const float u_hi = U[(size_t)ur * H + 64 + lane];
   const int o = lane >> 1;
-  const uint32_t member = member_offset + (uint32_t)b;
+  const uint32_t member = member_id(member_offset, b, ncond, id_period);
   float xv = o < P ? x[(size_t)b * P + o] : 0.f;
   float xs[PMAX];
   for (int t = t_first; t > t_first - n_run; --t) {
@@ -294,10 +298,11 @@ hipError_t launch_hoisted_sampler(const ertd_weights& w, const float* packed, co
                                   const float* V, const float* c1, const float* c2,
                                   const float* sigma, const float* noise, int num_steps,
                                   int t_first, int n_run, uint64_t seed, uint32_t member_offset,
-                                  int B, float* x, hipStream_t s) {
+                                  int B, float* x, hipStream_t s, int ncond, int id_period,
+                                  int u_rows) {
   hoisted_sampler_kernel<<<(B + 3) / 4, 256, 0, s>>>(w, packed, U, V, c1, c2, sigma, noise,
                                                       num_steps, t_first, n_run, seed,
-                                                      member_offset, B, x);
+                                                      member_offset, B, x, ncond, id_period, u_rows);
   return hipGetLastError();
 }
 

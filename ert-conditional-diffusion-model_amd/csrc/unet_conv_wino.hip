@@ -652,7 +652,12 @@ bool wino4s_ok(int cin, int ca, int cout, int wo, int B) {
   if (e == 2) return true;
   if (e == 3) return wo != 16;
   if (e == 4 && wo != 16) return true;
-  return wo == 16 && (wino4s_items(cout, wo, B) >= cu_count() || wino4s_ksplit(cin, cout, wo, B));
+  if (wo != 16) return false;
+  if (wino4s_items(cout, wo, B) >= cu_count()) return true;
+  // the K-split schedule (half the CUs' worth of items): only where every caller
+  // that sizes scratch (want_split: conv_wino_ok && wino_ksplit_wanted) hands the
+  // kernel its ksplit_buf -- a concatenated input with Ca % 8 != 0 runs F(2x2)
+  return wino4s_ksplit(cin, cout, wo, B) && conv_wino_ok(cin, ca, cout, wo);
 }
 
 bool wino4_ok(int cin, int ca, int cout, int wo, int B) {

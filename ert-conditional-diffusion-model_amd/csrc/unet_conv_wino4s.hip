@@ -23,7 +23,14 @@
 //     halves' partial output tiles meet in an LDS exchange buffer (below).
 // Item = (co group of 64, block of 16 consecutive tiles of one sample); the
 // output transform, bias / emb / residual epilogue and the GroupNorm partials
-// (one part per 16 tiles, as conv_wino4_kernel) are per MFMA wave.  No K split.
+// (one part per 16 tiles, as conv_wino4_kernel) are per MFMA wave.
+// K split (ksp = 2, XS = 2 only, never for the Upsample convs): where the items
+// fill half the CUs or more but not all (wino4s_ksplit: the 16x16 level of the
+// B = 32 train step), an item is (K half, co group, block) with the two halves
+// of a (co group, block) adjacent; half 0 sweeps channels [0, Cin/2) and writes
+// out with bias / emb / residual, half 1 sweeps [Cin/2, Cin) and writes its raw
+// sums to ksplit_buf (no bias / emb / residual, no GroupNorm partials: a split
+// layer emits none), and add_inplace_kernel adds them afterwards.
 #include <cstdlib>
 #include <type_traits>
 
@@ -793,7 +800,11 @@ hipError_t launch_wo4x(const ConvArgs& a, int B, hipStream_t s, int cus, int ksp
 template <int WO, int ACT, bool UP>
 hipError_t launch_wo4s(const ConvArgs& a, int B, hipStream_t s, int cus) {
   if (wino4s_xs() == 2 && a.Cin >= 16) {
-    const int ksp = !UP && a.ksplit_buf && wino4s_ksplit(a.Cin, a.Cout, WO, B) ? 2 : 1;
+    // the split geometry (wino4s_ok's second case) always comes with its buffer:
+    // without one the kernel would run unsplit on half the CUs -- refuse instead
+    const bool spl = !UP && wino4s_ksplit(a.Cin, a.Cout, WO, B) && wino4s_items(a.Cout, WO, B) < cus;
+    if (spl && !a.ksplit_buf) return hipErrorInvalidValue;
+    const int ksp = spl ? 2 : 1;
     return launch_wo4x<WO, ACT, UP, 2>(a, B, s, cus, ksp);
   }
   return launch_wo4x<WO, ACT, UP, 1>(a, B, s, cus, 1);
@@ -818,7 +829,9 @@ bool wino4s_up_ok(int cin, int ca, int cout, int wo, int B) {
   static const int env = [] {
     return ERTD_KNOB("WINO4S_UP", 1);
   }();
-  return env != 0 && wino4s_ok(cin, ca, cout, wo, B) && (wo == 16 || wo == 32 || wo == 64);
+  // (at 16x16 only where the items fill the CUs: the Upsample conv has no K split)
+  return env != 0 && wino4s_ok(cin, ca, cout, wo, B) && (wo == 16 || wo == 32 || wo == 64) &&
+         (wo != 16 || wino4s_items(cout, wo, B) >= device_cu_count());
 }
 
 hipError_t launch_conv_wino4s(int act, const ConvArgs& a, int B, hipStream_t s, int cus) {

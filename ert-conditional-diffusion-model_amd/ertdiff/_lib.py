@@ -75,6 +75,11 @@ SIGNATURES = {
     "ertd_sample_plan_create": (_I, [_W, _VP, _VP, ctypes.c_longlong, _I, _I, _I, _I, _I, _VP, _VP,
                                      _VP, _VP, _VP, _U64, _U32, _I, _I, _VP, _VP, _SZ,
                                      ctypes.POINTER(_VP)]),
+    "ertd_sample_conditions": (_I, [_W, _VP, _VP, _I, _I, _LL, _I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP,
+                                    _U64, _U32, _I, _I, _VP, _VP, _SZ, _VP]),
+    "ertd_sample_conditions_plan_create": (_I, [_W, _VP, _VP, _I, _I, _LL, _I, _I, _I, _I, _VP, _VP, _VP,
+                                                _VP, _VP, _U64, _U32, _I, _I, _VP, _VP, _SZ,
+                                                ctypes.POINTER(_VP)]),
     "ertd_train_forward": (_I, [_W, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _SZ,
                                 _VP]),
     "ertd_train_backward": (_I, [_W, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _SZ, _VP]),

@@ -112,3 +112,38 @@ def sample_ensemble(model, condition: Optional[torch.Tensor], n_members: int, T:
     else:
         local = torch.empty(0, P, dtype=torch.float32, device=device)
     return gather_members(local, n_members, group) if gather else local
+
+
+@torch.no_grad()
+def sample_conditions_sharded(model, conditions, n_samples: int, T: int, betas, alphas, alpha_bar,
+                              *, seed: int, num_steps=None, temperature: float = 1.0,
+                              mode: str = "hoisted", device=None, group=None,
+                              _sampler: Optional[Callable] = None) -> Tuple[torch.Tensor, int, int]:
+    """The test-set evaluation (ERT_Conditional_Diffusion.py:1042-1069) sharded
+    over the ranks of one node: rank r takes the condition slice
+    [c0, c1) = member_range(N, world, r) of the HOST array `conditions`
+    (N, 14, L) -- a host-side scatter, no collective -- copies
+    only that slice to its device and runs every realisation of it as one
+    sampler launch (ertdiff.sample_conditions) with condition offset c0 and
+    id period N, so every member keeps its global Philox id r * N + c.
+
+    Returns (local, c0, c1): this rank's (n_samples, c1 - c0, P) block of the
+    (n_samples, N, P) `Uncertainty_params` array; the caller concatenates the
+    blocks along dim 1 (per-device D2H).  ``_sampler`` replaces the device
+    sampler in the CPU (gloo) tests of this host logic."""
+    rank, world = _dist_info(group)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    N = conditions.shape[0]
+    c0, c1 = member_range(N, world, rank)
+    if _sampler is None:
+        from .sampler import sample_conditions
+        _sampler = sample_conditions
+    P = model.param_dim
+    if c1 == c0:
+        return torch.empty(n_samples, 0, P, dtype=torch.float32, device=device), c0, c1
+    local_cond = torch.as_tensor(conditions[c0:c1], dtype=torch.float32).to(device).contiguous()
+    local = _sampler(model, local_cond, n_samples, T, betas, alphas, alpha_bar, P, device,
+                     num_steps=num_steps, temperature=temperature, mode=mode, seed=seed,
+                     cond_offset=c0, n_conditions_total=N)
+    return local, c0, c1

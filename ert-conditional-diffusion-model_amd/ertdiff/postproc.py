@@ -11,6 +11,7 @@ validity mask.
 
     postprocess(u, scaler, limits)          -> params (rows, P) f32, valid (rows,) bool
     sample_realisations(model, cond, n, ...) -> params (n, B, P), valid (n, B), u (n, B, P)
+        (batched=True: the n x B members as ONE sampler launch, sample_conditions)
     compact(params, valid)                  -> check_param_bounds' output per realisation
 """
 from __future__ import annotations
@@ -21,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .sampler import sample_model
+from .sampler import sample_conditions, sample_model
 
 
 def _scaler_vectors(scaler, P: int, dev) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -76,25 +77,43 @@ def postprocess(u: torch.Tensor, scaler, limits, a: float = 0.0, b: float = 1.0,
 @torch.no_grad()
 def sample_realisations(model, condition, n_samples: int, T, betas, alphas, alpha_bar,
                         param_dim: int, device, scaler, limits, a: float = 0.0, b: float = 1.0,
-                        **sample_kw):
+                        *, batched: bool = False, **sample_kw):
     """The reference's uncertainty loop (:398-410 / :1052-1064) with the
-    post-processing on device: n_samples calls of sample_model, each followed
-    by ertd_postprocess into slice r of an (n_samples, B, P) buffer.
+    post-processing on device.
+
+    batched=False: n_samples calls of sample_model, each followed by
+    ertd_postprocess into slice r of an (n_samples, B, P) buffer (the
+    reference's loop shape).  batched=True (noise="philox", one condition per
+    member): ONE sampler launch over all n_samples x B members
+    (sample_conditions) and one ertd_postprocess over the whole array.
 
     Returns (params, valid, unconstrained): physical-unit parameters
     (n_samples, B, P), the bounds mask (n_samples, B) and the raw sampler
     outputs (the reference's params_realizations_norm).  With noise="philox"
-    each realisation r is keyed by seed + r.  All three stay on the device."""
+    realisation r's members are Philox member ids r*B .. r*B+B-1 under the one
+    seed -- the ids of the batched launch, so both forms return the same bits.
+    All three stay on the device."""
     dev = _lib.require_device(condition)
     B = sample_kw.get("n_members") or condition.shape[0]
+    seed = int(sample_kw.pop("seed", 0))
+    if sample_kw.get("noise") == "philox" and sample_kw.get("member_offset"):
+        raise RuntimeError("ertdiff: sample_realisations assigns the member ids itself (r * B + b)")
+    if batched:
+        if sample_kw.get("noise") != "philox" or sample_kw.get("shared_condition"):
+            raise RuntimeError("ertdiff: batched realisations need noise='philox' and (B, 14, L) conditions")
+        kw = {k: v for k, v in sample_kw.items() if k in ("num_steps", "temperature", "mode", "precision")}
+        unc = sample_conditions(model, condition, n_samples, T, betas, alphas, alpha_bar, param_dim,
+                                device, seed=seed, **kw)
+        params, valid = postprocess(unc, scaler, limits, a, b)
+        return params, valid, unc
     unc = torch.empty(n_samples, B, param_dim, dtype=torch.float32, device=dev)
     params = torch.empty_like(unc)
     valid = torch.empty(n_samples, B, dtype=torch.uint8, device=dev)
-    seed = int(sample_kw.pop("seed", 0))
     for r in range(n_samples):
         kw = dict(sample_kw)
         if kw.get("noise") == "philox":
-            kw["seed"] = seed + r
+            kw["seed"] = seed
+            kw["member_offset"] = r * B
         unc[r] = sample_model(model, condition, T, betas, alphas, alpha_bar, param_dim, device,
                               **kw)
         postprocess(unc[r], scaler, limits, a, b, out=params[r], valid=valid[r])

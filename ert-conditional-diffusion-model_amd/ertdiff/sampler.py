@@ -196,6 +196,92 @@ def sample_model(model, condition, T, betas, alphas, alpha_bar, param_dim, devic
     return x
 
 
+def conditions_x_T(n_cond: int, n_samples: int, P: int, n: int, seed: int, cond_offset: int,
+                   id_period: int, device) -> torch.Tensor:
+    """x_T of a many-condition launch: realisation r's rows are the Philox
+    draws of members cond_offset + r * id_period + (0 .. n_cond-1)."""
+    x = torch.empty(n_samples * n_cond, P, dtype=torch.float32, device=device)
+    for r in range(n_samples):
+        x[r * n_cond:(r + 1) * n_cond] = philox_normal(n_cond, P, n, 1, seed, cond_offset + r * id_period,
+                                                       device)
+    return x
+
+
+class _Conditions:
+    """Geometry of a many-condition launch (ertd_sample_conditions)."""
+
+    def __init__(self, prep, n_samples, cond_offset, n_conditions_total):
+        self.n_cond = prep.cond.shape[0]
+        self.n_samples = int(n_samples)
+        self.cond_offset = int(cond_offset)
+        self.period = self.n_cond if n_conditions_total is None else int(n_conditions_total)
+        if self.n_samples < 1 or self.cond_offset < 0 or self.period < self.cond_offset + self.n_cond:
+            raise RuntimeError("ertdiff: need n_samples >= 1 and cond_offset + n_cond <= n_conditions_total")
+        if prep.stride == 0:
+            raise RuntimeError("ertdiff: a many-condition launch reads (n_cond, 14, L) conditions")
+        self.B = self.n_cond * self.n_samples
+
+    def args(self, prep, x, noise, seed, mode, t_first, n_run, ws):
+        tb = prep.tables
+        return (ctypes.byref(prep.w), prep.packed.data_ptr(), prep.cond.data_ptr(), self.n_cond,
+                self.n_samples, self.period, prep.L, prep.num_steps, t_first, n_run, tb[0].data_ptr(),
+                tb[1].data_ptr(), tb[2].data_ptr(), prep.freq.data_ptr(), _lib.ptr(noise),
+                int(seed) & (2**64 - 1), self.cond_offset & 0xFFFFFFFF, _MODES[mode], prep.prec,
+                x.data_ptr(), ws.data_ptr(), ws.numel())
+
+
+@torch.no_grad()
+def sample_conditions(model, conditions, n_samples: int, T, betas, alphas, alpha_bar, param_dim,
+                      device, num_steps=None, temperature=1.0, *, mode: str = "hoisted",
+                      seed: int = 0, cond_offset: int = 0,
+                      n_conditions_total: Optional[int] = None,
+                      noise: Union[str, torch.Tensor] = "philox",
+                      precision: Optional[str] = None) -> torch.Tensor:
+    """The reference's test-set uncertainty evaluation (ERT_Conditional_Diffusion.py
+    :1042-1069: `uncertainty_samples` calls of sample_model per test batch) as
+    ONE sampler launch over every (realisation, condition) pair.
+
+    conditions: (n_cond, 14, L).  Returns x_0 as (n_samples, n_cond, P) -- the
+    reference's `Uncertainty_params` layout (:1073), unconstrained space.
+    Member (r, c) is Philox member id cond_offset + r * n_conditions_total + c
+    (n_conditions_total defaults to n_cond), i.e. realisation r draws exactly
+    what sample_model(..., noise="philox", seed=seed, member_offset=
+    r * n_conditions_total + cond_offset) draws for these conditions -- so a
+    rank holding the condition slice [cond_offset, cond_offset + n_cond) of N
+    computes exactly its columns of the whole evaluation.  mode="hoisted" runs
+    the condition encoder once per condition; "faithful" re-runs it per member
+    and step as the reference does.  noise: "philox", or an injected
+    (num_steps, n_samples * n_cond, P) tensor."""
+    if mode not in _MODES:
+        raise ValueError(f"mode must be one of {list(_MODES)}")
+    dev = _lib.require_device(conditions)
+    model = as_ertdiff_model(model, dev)
+    if model.param_dim != param_dim:
+        raise RuntimeError(f"ertdiff: param_dim={param_dim} but the model predicts {model.param_dim}")
+    prep = _Prepared(model, conditions, T, betas, alphas, alpha_bar, num_steps, temperature,
+                     precision or model.precision, False)
+    geo = _Conditions(prep, n_samples, cond_offset, n_conditions_total)
+    n = prep.num_steps
+    inj = None
+    if isinstance(noise, torch.Tensor):
+        inj = _lib.f32c(noise, "noise")
+        if tuple(inj.shape) != (n, geo.B, param_dim):
+            raise RuntimeError(f"ertdiff: noise must be (num_steps={n}, {geo.B}, {param_dim})")
+        x = inj[0].clone()
+    elif noise == "philox":
+        x = conditions_x_T(geo.n_cond, geo.n_samples, param_dim, n, seed, geo.cond_offset, geo.period,
+                           dev)
+    else:
+        raise ValueError("noise must be 'philox' or a tensor")
+    ws = prep.workspace(geo.B)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().ertd_sample_conditions(*geo.args(prep, x, inj, seed, mode, n - 1, n, ws),
+                                                     _lib.stream_of(dev)), "sample_conditions")
+    if mode != "hoisted" and sample_status(ws, geo.B, prep.L, n) != 0:
+        raise RuntimeError("ertdiff: the persistent faithful sampler timed out; x is not valid")
+    return x.view(geo.n_samples, geo.n_cond, param_dim)
+
+
 class SamplerPlan:
     """A captured hipGraph of ``n_run`` sampler steps starting at ``t_first``.
 
@@ -208,7 +294,11 @@ class SamplerPlan:
     def __init__(self, model, condition, T, betas, alphas, alpha_bar, *, num_steps=None,
                  t_first=None, n_run=None, temperature=1.0, mode="faithful", seed=0,
                  member_offset=0, B=None, precision=None, shared_condition=False,
-                 noise: Optional[torch.Tensor] = None):
+                 noise: Optional[torch.Tensor] = None, n_samples: Optional[int] = None,
+                 n_conditions_total: Optional[int] = None):
+        """n_samples: a many-condition plan (ertd_sample_conditions_plan_create):
+        condition (n_cond, 14, L), B = n_samples * n_cond members in the
+        sample_conditions layout, member_offset = the condition offset."""
         dev = _lib.require_device(condition)
         model = as_ertdiff_model(model, dev)
         self.prep = _Prepared(model, condition, T, betas, alphas, alpha_bar, num_steps,
@@ -216,7 +306,9 @@ class SamplerPlan:
         n = self.prep.num_steps
         self.t_first = n - 1 if t_first is None else int(t_first)
         self.n_run = (self.t_first + 1) if n_run is None else int(n_run)
-        self.B = B if B is not None else self.prep.cond.shape[0]
+        self.geo = None if n_samples is None else _Conditions(self.prep, n_samples, member_offset,
+                                                              n_conditions_total)
+        self.B = self.geo.B if self.geo else (B if B is not None else self.prep.cond.shape[0])
         self.noise = None if noise is None else _lib.f32c(noise, "noise")
         self.x = torch.zeros(self.B, model.param_dim, dtype=torch.float32, device=dev)
         self.ws = self.prep.workspace(self.B)
@@ -226,10 +318,15 @@ class SamplerPlan:
         self.dev = dev
         self._plan = ctypes.c_void_p()
         with torch.cuda.device(dev):
-            _lib.check(_lib.lib().ertd_sample_plan_create(
-                *self.prep.args(self.B, self.x, self.noise, seed, member_offset, mode,
-                                self.t_first, self.n_run, self.ws), ctypes.byref(self._plan)),
-                "sample_plan_create")
+            if self.geo:
+                _lib.check(_lib.lib().ertd_sample_conditions_plan_create(
+                    *self.geo.args(self.prep, self.x, self.noise, seed, mode, self.t_first, self.n_run,
+                                   self.ws), ctypes.byref(self._plan)), "sample_conditions_plan_create")
+            else:
+                _lib.check(_lib.lib().ertd_sample_plan_create(
+                    *self.prep.args(self.B, self.x, self.noise, seed, member_offset, mode,
+                                    self.t_first, self.n_run, self.ws), ctypes.byref(self._plan)),
+                    "sample_plan_create")
 
     def launch(self, stream: Optional[torch.cuda.Stream] = None):
         s = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
@@ -239,10 +336,15 @@ class SamplerPlan:
     def enqueue_direct(self, stream: Optional[torch.cuda.Stream] = None):
         """Same work as launch() but as eager launches (no graph), for comparison."""
         s = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
-        args = self.prep.args(self.B, self.x, self.noise, self.seed, self.member_offset,
-                              self.mode, self.t_first, self.n_run, self.ws)
         with torch.cuda.device(self.dev):
-            _lib.check(_lib.lib().ertd_sample(*args, s), "sample")
+            if self.geo:
+                _lib.check(_lib.lib().ertd_sample_conditions(
+                    *self.geo.args(self.prep, self.x, self.noise, self.seed, self.mode, self.t_first,
+                                   self.n_run, self.ws), s), "sample_conditions")
+            else:
+                _lib.check(_lib.lib().ertd_sample(
+                    *self.prep.args(self.B, self.x, self.noise, self.seed, self.member_offset,
+                                    self.mode, self.t_first, self.n_run, self.ws), s), "sample")
 
     def status(self) -> int:
         """0, or the timeout code of the last faithful replay (synchronizes)."""

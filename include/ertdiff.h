@@ -186,6 +186,36 @@ int ertd_sample_plan_create(const ertd_weights* w, const float* packed, const fl
 int ertd_plan_launch(ertd_plan* plan, void* stream);
 int ertd_plan_destroy(ertd_plan* plan);
 
+/* The reference's test-set uncertainty evaluation (ERT_Conditional_Diffusion.py
+ * :1042-1069: every test condition x `uncertainty_samples` calls of
+ * sample_model) as ONE sampler launch of B = n_cond * n_samples members.
+ *   cond (n_cond, 14, L) contiguous; member j = realisation r = j / n_cond of
+ *     condition c = j % n_cond, so x_inout (B, P) is the (n_samples, n_cond, P)
+ *     `Uncertainty_params` layout (:1073) as it fills.
+ *   Philox id of member j: member_offset + r * id_period + c.  One device:
+ *     id_period = n_cond, member_offset = 0 (ids 0..B-1, realisation r's
+ *     members r*N .. r*N+N-1: the same draws as sample_model with
+ *     member_offset = r*N).  A rank holding conditions [c0, c0+n_cond) of N
+ *     passes member_offset = c0, id_period = N: every member keeps its global
+ *     id, so the result is bitwise invariant to how the conditions are split.
+ *   ERTD_MODE_HOISTED runs the condition encoder once per CONDITION (n_cond
+ *     strip sets, not B); the faithful modes re-run it per member and step as
+ *     the reference does.  Workspace: ertd_workspace_bytes(B, L, P, num_steps,
+ *     ERTD_OP_SAMPLE).  Other arguments as ertd_sample.                      */
+int ertd_sample_conditions(const ertd_weights* w, const float* packed, const float* cond, int n_cond,
+                           int n_samples, long long id_period, int L, int num_steps, int t_first,
+                           int n_run, const float* c1, const float* c2, const float* sigma,
+                           const float* freq, const float* noise, uint64_t seed,
+                           uint32_t member_offset, int mode, int precision, float* x_inout, void* ws,
+                           size_t ws_bytes, void* stream);
+int ertd_sample_conditions_plan_create(const ertd_weights* w, const float* packed, const float* cond,
+                                       int n_cond, int n_samples, long long id_period, int L,
+                                       int num_steps, int t_first, int n_run, const float* c1,
+                                       const float* c2, const float* sigma, const float* freq,
+                                       const float* noise, uint64_t seed, uint32_t member_offset,
+                                       int mode, int precision, float* x_inout, void* ws,
+                                       size_t ws_bytes, ertd_plan** plan);
+
 /* ---- training (ERT_Conditional_Diffusion.py:305-320) ---------------------------
  * Workspace: ertd_workspace_bytes(B, L, P, 0, ERTD_OP_TRAIN).  The forward
  * stores the activations the backward reads there: keep it between the two.

@@ -31,10 +31,12 @@ def synth_uniform(shape, seed: int) -> np.ndarray:
     return u.astype(np.float32).reshape(shape)
 
 
-def synth_normal(shape, seed: int) -> np.ndarray:
-    """N(0,1) float32 by Box-Muller on two independent hash streams."""
+def synth_normal(shape, seed: int, start: int = 0) -> np.ndarray:
+    """N(0,1) float32 by Box-Muller on two independent hash streams.  start:
+    flat index of the first element, so a big array can be made in slices
+    (synth_normal(s, seed, k * n) == synth_normal((K, *s), seed)[k])."""
     n = int(np.prod(shape))
-    idx = np.arange(n, dtype=np.uint64)
+    idx = np.arange(start, start + n, dtype=np.uint64)
     z1 = _splitmix64(idx, seed)
     z2 = _splitmix64(idx, seed + 7919)
     u1 = ((z1 >> np.uint64(11)).astype(np.float64) + 1.0) * (1.0 / (1 << 53))

@@ -149,3 +149,58 @@ def test_dp_gradient_mean_gloo(world):
         want = sum(res[r][0][i] for r in range(world)) / world
         for r in range(world):
             np.testing.assert_allclose(res[r][1][i], want, rtol=1e-6, atol=1e-7)
+
+
+def fake_conditions_sampler(model, cond, n_samples, T, betas, alphas, alpha_bar, P, device, *,
+                            num_steps, temperature, mode, seed, cond_offset, n_conditions_total):
+    """Stand-in for ertdiff.sample_conditions: member (r, c) depends on its
+    condition's content, the seed and its GLOBAL Philox id r * N + cond_offset + c."""
+    nc = cond.shape[0]
+    ids = (torch.arange(n_samples)[:, None] * n_conditions_total + cond_offset
+           + torch.arange(nc)[None, :]).float()
+    csum = cond.reshape(nc, -1).sum(1)[None, :]
+    return (csum + seed + ids * 10)[..., None] + torch.arange(P, dtype=torch.float32)
+
+
+def _cond_worker(rank, world, port, N, q):
+    from ertdiff.ensemble import sample_conditions_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = 23
+        conds = np.arange(N * 14 * L, dtype=np.float32).reshape(N, 14, L) / 1000  # every rank's host copy
+        local, c0, c1 = sample_conditions_sharded(_Model(), conds, 4, 10, None, None, None, seed=5,
+                                                  device=torch.device("cpu"),
+                                                  _sampler=fake_conditions_sampler)
+        q.put((rank, local.numpy(), c0, c1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N", [(2, 509), (2, 3), (3, 8)])
+def test_sharded_conditions_gloo(world, N):
+    """The test-set evaluation sharded by condition slice (a
+    host-side scatter, no collective): each rank's (n_samples, c1 - c0, P)
+    block, concatenated along the condition axis, equals the one-process
+    (n_samples, N, P) array -- every member keeps its global id r * N + c."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cond_worker, args=(r, world, port, N, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    L = 23
+    conds = torch.from_numpy(np.arange(N * 14 * L, dtype=np.float32).reshape(N, 14, L) / 1000)
+    expect = fake_conditions_sampler(_Model(), conds, 4, 10, None, None, None, _Model.param_dim, None,
+                                     num_steps=None, temperature=1.0, mode="hoisted", seed=5,
+                                     cond_offset=0, n_conditions_total=N).numpy()
+    spans = [(c0, c1) for _, _, c0, c1 in res]
+    assert spans == [member_range(N, world, r) for r in range(world)]
+    got = np.concatenate([local for _, local, _, _ in res], axis=1)
+    assert got.shape == (4, N, _Model.param_dim)
+    assert (got == expect).all()

@@ -68,7 +68,37 @@ def test_sample_realisations(gpu_model, postproc_chain_kat, cuda_dev):
     assert params.shape == (3, 4, 29) and valid.shape == (3, 4)
     for r in range(3):
         x = ertdiff.sample_model(gpu_model, cond, T, *sched, 29, cuda_dev, noise="philox",
-                                 seed=7 + r, mode="faithful")
+                                 seed=7, member_offset=4 * r, mode="faithful")
         assert torch.equal(x, unc[r])
         o, m = ertdiff.postprocess(x, (k["min_"], k["scale_"]), k["limits"])
         assert torch.equal(o, params[r]) and torch.equal(m, valid[r])
+    # the n_samples x B members as ONE launch: the same bits
+    pb, vb, ub = ertdiff.sample_realisations(
+        gpu_model, cond, 3, T, *sched, 29, cuda_dev, (k["min_"], k["scale_"]), k["limits"],
+        noise="philox", seed=7, mode="faithful", batched=True)
+    assert torch.equal(ub, unc) and torch.equal(pb, params) and torch.equal(vb, valid)
+
+
+@pytest.mark.parametrize("mode", ["hoisted", "faithful", "faithful_steps"])
+def test_sample_conditions_one_launch(gpu_model, mode, cuda_dev):
+    """The test-set evaluation (ERT_Conditional_Diffusion.py:1042-1069): every
+    condition x n_samples realisations as ONE sampler launch
+    (ertd_sample_conditions) == the per-realisation sample_model loop with
+    member ids r * N + c, bit for bit, in every schedule; and the condition
+    slices a sharded run gives each rank ([0, 2) and [2, 5) of N = 5, condition
+    offset + id period N) concatenate to the same array."""
+    from synth import synth_uniform
+    N, ns, T = 5, 3, 9
+    cond = torch.from_numpy(synth_uniform((N, 14, 301), 83)).to(cuda_dev)
+    sched = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    full = ertdiff.sample_conditions(gpu_model, cond, ns, T, *sched, 29, cuda_dev, mode=mode, seed=11)
+    assert full.shape == (ns, N, 29)
+    for r in range(ns):
+        x = ertdiff.sample_model(gpu_model, cond, T, *sched, 29, cuda_dev, noise="philox", seed=11,
+                                 member_offset=r * N, mode=mode)
+        assert torch.equal(x, full[r]), r
+    parts = [ertdiff.sample_conditions(gpu_model, cond[c0:c1].contiguous(), ns, T, *sched, 29, cuda_dev,
+                                       mode=mode, seed=11, cond_offset=c0, n_conditions_total=N)
+             for c0, c1 in ((0, 2), (2, 5))]
+    assert torch.equal(torch.cat(parts, 1), full)
+    assert float((full[0] - full[1]).abs().max()) > 0     # realisations differ

@@ -55,13 +55,18 @@ def test_unet_forward_vs_oracle(name, B, L, ts, cuda_dev):
     assert err < 1e-5, err
 
 
+def _cus(dev):
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
 def test_unet_u2_b64_forward_headline_path_random_affine(cuda_dev):
     """The exact headline kernel path (configs[1]: U2, B = 64, L = 4693): at
-    B = 64 the Winograd layers run unsplit (F(4x4) ksp = 1 at 64x64 / 32x32,
-    unsplit F(2x2) at 16x16) -- the variants the bench times -- against the
-    spec, with trained-model-like GroupNorm gamma/beta (random per channel),
-    so a gamma/beta tensor wired to the wrong GroupNorm, or a concatenated
-    input's gamma in the wrong channel order, fails here."""
+    B = 64 every ResBlock 3x3 conv runs the register-weight F(4x4) kernel
+    unsplit (at 16x16 its 64 co x 16 tile items are 64 x 4 = 256 >= the CUs) --
+    the variants the bench times -- against the spec, with trained-model-like
+    GroupNorm gamma/beta (random per channel), so a gamma/beta tensor wired to
+    the wrong GroupNorm, or a concatenated input's gamma in the wrong channel
+    order, fails here."""
     name, B, L = "U2", 64, 4693
     cfg = U.CONFIGS[name]
     W = U.init_weights(cfg, 11, affine="random")
@@ -78,22 +83,35 @@ def test_unet_u2_b64_forward_headline_path_random_affine(cuda_dev):
 
 
 def test_unet_forward_batch_split_consistency(cuda_dev):
-    """U2 at B=128 runs its 16x16 ResBlock convs by Winograd F(4x4) (tile items
-    fill the CUs); the same members as two B=64 batches run them by F(2x2).
-    Both sides are held to the spec at 1e-5 (test above); here the B=128 path
-    end to end against the split one (the spec at B=128 is minutes of CPU)."""
+    """Two different dispatches of the 16x16 ResBlock convs on the same members:
+    at B = CUs / 4 (64 on 256 CUs, the headline) the register-weight F(4x4)
+    kernel's 64 co x 16 tile items fill the CUs and run unsplit; each half
+    (B = CUs / 8) has half as many items and splits its K in two (half 1's sums
+    to the K-split buffer, added afterwards) -- another summation order, same
+    math.  The two must agree to rounding, and one member of each against the
+    spec (test above for the whole B = 64 batch)."""
+    cus = _cus(cuda_dev)
     m = ertdiff.ConditionalUNet.from_config("U2", seed=3).to(cuda_dev).eval()
     cfg = U.CONFIGS["U2"]
-    B = 128
-    x = torch.from_numpy(synth_normal((B, cfg.param_dim), 131)).to(cuda_dev)
-    cond = torch.from_numpy(synth_uniform((B, 14, 257), 132)).to(cuda_dev)
-    t = torch.arange(B, device=cuda_dev) * 7 % 1000
+    W = U.init_weights(cfg, 3)
+    B = cus // 4
+    x = torch.from_numpy(synth_normal((B, cfg.param_dim), 131))
+    cond = torch.from_numpy(synth_uniform((B, 14, 257), 132))
+    t = torch.arange(B) * 7 % 1000
+    xd, cd, td = x.to(cuda_dev), cond.to(cuda_dev), t.to(cuda_dev)
+    h = B // 2
     with torch.no_grad():
-        full = m(x, t, cond)
-        split = torch.cat([m(x[:64], t[:64], cond[:64]), m(x[64:], t[64:], cond[64:])])
-    err = RN.rel_l2(full.cpu().double().numpy(), split.cpu().double().numpy())
-    record_error("unet_forward_U2_B128_vs_split", err)
+        full = m(xd, td, cd).cpu()
+        split = torch.cat([m(xd[:h], td[:h], cd[:h]), m(xd[h:], td[h:], cd[h:])]).cpu()
+        ref = U.forward(x[h - 1:h + 1], t[h - 1:h + 1], cond[h - 1:h + 1], W, cfg)
+    err = RN.rel_l2(full.double().numpy(), split.double().numpy())
+    record_error(f"unet_forward_U2_B{B}_vs_two_halves", err)
+    assert not torch.equal(full, split)      # different schedules: not the same sums
     assert err < 1e-5, err
+    for got, name in ((full, "unsplit"), (split, "ksplit")):
+        e = RN.rel_l2(got[h - 1:h + 1].double().numpy(), ref.double().numpy())
+        record_error(f"unet_forward_U2_{name}_members_vs_spec", e)
+        assert e < 1e-5, (name, e)
 
 
 SAMPLER_TOL = 1e-4
@@ -105,6 +123,14 @@ SAMPLER_TOL = 1e-4
 # at step 1000 -- the latter is the spec-vs-spec gap itself (1.5e-3,
 # test_host.test_unet_sampler_golden_fixture_shape)
 BF16_SAMPLER_TOL = {"bf16_spec": 1e-3, "fp32_spec": 3e-3}
+
+
+def _noise(T, B, P, seed, dev):
+    """synth_normal((T, B, P), seed) on the device, made one step at a time."""
+    out = torch.empty(T, B, P, dtype=torch.float32, device=dev)
+    for k in range(T):
+        out[k] = torch.from_numpy(synth_normal((B, P), seed, k * B * P))
+    return out
 
 
 def _run_golden_chain(kat, key, dev, precision=None):
@@ -120,7 +146,7 @@ def _run_golden_chain(kat, key, dev, precision=None):
     m = _model_from_spec(name, W, dev, precision=precision or ("bf16" if bf16 else "fp32"))
     P = m.param_dim
     cond = torch.from_numpy(synth_uniform((B, 14, L), cseed)).to(dev)
-    noise = torch.from_numpy(synth_normal((T, B, P), nseed)).to(dev)
+    noise = _noise(T, B, P, nseed, dev)
     sched = ertdiff.get_diffusion_schedule(T, device=dev)
     x = noise[0].clone()
     done, out = 0, {}
@@ -145,6 +171,60 @@ def test_unet_u2_sampler_full_chain_vs_golden(unet_sampler_kat, cuda_dev):
         err = RN.rel_l2(x, unet_sampler_kat[f"u2_fp32_x{k}"].astype(np.float64))
         record_error(f"unet_sampler_U2_fp32_step{k}", err)
         assert err < SAMPLER_TOL, (k, err)
+
+
+def test_unet_u2_b64_sampler_full_chain_vs_golden(cuda_dev):
+    """configs[1] exactly -- U2, fp32, B = 64, L = 4693, random GroupNorm affine
+    -- over a full T = 1000 chain with injected noise: the kernel dispatch the
+    bench times (unsplit register-weight F(4x4) at every level), <= 1e-4 rel-L2
+    against the spec at steps 1, 10, 100 and 1000
+    (tests/golden/unet_sampler_b64_kat.npz)."""
+    from conftest import load_golden
+    kat = load_golden("unet_sampler_b64_kat.npz")
+    xs = _run_golden_chain(kat, "u2_b64_aff", cuda_dev)
+    for k, x in xs.items():
+        err = RN.rel_l2(x, kat[f"u2_b64_aff_x{k}"].astype(np.float64))
+        record_error(f"unet_sampler_U2_B64_aff_step{k}", err)
+        assert err < SAMPLER_TOL, (k, err)
+
+
+# The bf16 configs at their per-GPU bench batch (configs[2]: U3 B = 256;
+# configs[4]: U5 B = 64) -- the tile counts, K splits and workgroup grids of the
+# bench, which the B <= 2 golden chains do not reach -- over a 10-step chain
+# (T = 10 schedule, injected noise) against the spec on members spread over the
+# batch (the spec's members are independent: GroupNorm and attention are per
+# sample, so the spec run on those members alone is the batch's reference).
+BATCH_CASES = [("U3", "bf16", 256, 1001), ("U3", "bf16x3", 256, 1001),
+               ("U5", "bf16", 64, 513), ("U5", "bf16x3", 64, 513), ("U5", "fp32", 64, 513)]
+# 10 steps; per-forward budgets of test_unet_bf16_forward / test_unet_bf16x3_forward
+BATCH_TOL = {"bf16": (1.2e-2, 1.6e-2), "bf16x3": (None, 1e-4), "fp32": (None, 1e-4)}
+
+
+@pytest.mark.parametrize("name,precision,B,L", BATCH_CASES)
+def test_unet_bench_batch_chain_vs_spec(name, precision, B, L, cuda_dev):
+    cfg = U.CONFIGS[name]
+    T = 10
+    W = U.init_weights(cfg, 15, affine="random")
+    m = _model_from_spec(name, W, cuda_dev, precision=precision)
+    P = m.param_dim
+    cond = torch.from_numpy(synth_uniform((B, 14, L), 161))
+    noise = torch.from_numpy(synth_normal((T, B, P), 162))
+    sched = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    xs = ertdiff.sample_model(m, cond.to(cuda_dev), T, *sched, P, cuda_dev, noise=noise.to(cuda_dev)).cpu()
+    assert bool(torch.isfinite(xs).all())
+    idx = [0, B // 2 + 1, B - 1]
+    got = xs[idx].double().numpy()
+    tol16, tol32 = BATCH_TOL[precision]
+    with torch.no_grad():
+        ref32 = U.sample(cond[idx], W, cfg, T, noise[:, idx])
+        e32 = RN.rel_l2(got, ref32.double().numpy())
+        record_error(f"unet_chain10_{name}_B{B}_{precision}_vs_fp32spec", e32)
+        assert e32 < tol32, e32
+        if tol16 is not None:
+            ref16 = U.sample(cond[idx], W, cfg, T, noise[:, idx], bf16=True)
+            e16 = RN.rel_l2(got, ref16.double().numpy())
+            record_error(f"unet_chain10_{name}_B{B}_{precision}_vs_bf16spec", e16)
+            assert e16 < tol16, e16
 
 
 def test_unet_u3_bf16_sampler_full_chain_vs_golden(unet_sampler_kat, cuda_dev):

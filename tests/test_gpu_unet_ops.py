@@ -95,9 +95,10 @@ def test_conv2d(Ca, Cb, Cout, H, ks, mode, act, precision, cuda_dev):
 
 # The exact variants the headline (U2, B = 64) and the train step (B = 32) run:
 # (Cin, Cout, H) per Winograd level at B = 32 and 64, with bias, per-sample
-# embedding add and residual.  At B = 64: F(4x4) ksp = 1 at 64x64 and 32x32,
-# unsplit F(2x2) at 16x16; at B = 32 the 32x32 F(4x4) and 16x16 F(2x2) layers
-# split their K in two halves (tile items < CUs).
+# embedding add and residual.  On 256 CUs: at B = 64 every level runs the
+# register-weight F(4x4) kernel unsplit (64 co x 16 tile items: 1024 / 256 /
+# 256 at 64x64 / 32x32 / 16x16); at B = 32 the 64x64 and 32x32 levels too (512 /
+# 256 items), the 16x16 level (128 items) with its K split in two halves.
 HEADLINE_CASES = [(64, 64, 64), (128, 128, 32), (384, 128, 32), (256, 256, 16), (512, 256, 16)]
 
 
@@ -115,6 +116,82 @@ def test_conv2d_headline_variants(Cin, Cout, H, B, cuda_dev):
     ref = _ref_conv(x, w, b, "same", "gn_silu", gn, False) + eb[:, :, None, None] + res
     err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
     record_error(f"conv2d_headline_{Cin}_{Cout}_{H}_B{B}", err)
+    assert err < 1e-5, err
+
+
+def _cus(dev):
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+KSPLIT_CASES = [  # (Ca, Cb, Cout, act, emb, residual): 16x16, B = CUs / 8, always a bias
+    (256, 256, 256, "gn_silu", True, True),       # concatenated input, both halves of K on different tensors
+    (384, 128, 256, "none", True, True),          # ACT_NONE with a residual
+    (256, 0, 256, "gn", False, False),            # GroupNorm without SiLU, bias only
+]
+
+
+@pytest.mark.parametrize("Ca,Cb,Cout,act,eb,resid", KSPLIT_CASES)
+def test_conv2d_wino4s_ksplit(Ca, Cb, Cout, act, eb, resid, cuda_dev):
+    """The register-weight F(4x4) kernel's K split (unet_conv_wino4s.hip,
+    ksp = 2): at 16x16 with B = CUs / 8 its 64 co x 16 tile items fill half
+    the CUs, so each item is split into two K halves (half 1's raw sums to the
+    K-split buffer, added in place afterwards); B chosen from the device's CU
+    count so the split geometry is hit on any part.  Against torch <= 1e-5, and
+    against the unsplit dispatch of the same samples (B = CUs / 4: items fill
+    the CUs) to rounding (<= 3e-6)."""
+    cus = _cus(cuda_dev)
+    B, H = cus // 8, 16
+    seed = Ca + 3 * Cb + Cout
+    x = _rand((B, Ca, H, H), seed)
+    x2 = _rand((B, Cb, H, H), seed + 1) if Cb else None
+    w = _rand((Cout, Ca + Cb, 3, 3), seed + 2, 1.0 / np.sqrt(9 * (Ca + Cb)))
+    b = _rand((Cout,), seed + 3, 0.1)
+    gn = None
+    if act != "none":
+        gn = torch.stack([_rand((B, Ca + Cb), seed + 4, 0.3) + 1.0, _rand((B, Ca + Cb), seed + 5, 0.2)], -1)
+    e = _rand((B, Cout), seed + 6) if eb else None
+    res = _rand((B, Cout, H, H), seed + 7) if resid else None
+    d = lambda v: None if v is None else v.to(cuda_dev)
+    out = conv2d(d(x), d(w), d(b), act=act, gn=d(gn), x2=d(x2), ebias=d(e), res=d(res)).cpu()
+    xin = x if x2 is None else torch.cat([x, x2], 1)
+    ref = _ref_conv(xin, w, b, "same", act, gn, False)
+    if eb:
+        ref = ref + e[:, :, None, None]
+    if resid:
+        ref = ref + res
+    err = RN.rel_l2(out.double().numpy(), ref.double().numpy())
+    record_error(f"conv2d_wino4s_ksplit_{Ca}_{Cb}_{Cout}_{act}_B{B}", err)
+    assert err < 1e-5, err
+    # the same samples twice over (B = CUs / 4): unsplit items, another summation order
+    cat = lambda v: None if v is None else torch.cat([v, v])
+    full = conv2d(d(cat(x)), d(w), d(b), act=act, gn=d(cat(gn)), x2=d(cat(x2)),
+                  ebias=d(cat(e)), res=d(cat(res))).cpu()
+    assert not torch.equal(full[:B], out)
+    # (each side carries F(4x4)'s ~1e-6 rounding: measured 1.0e-6 apart)
+    assert RN.rel_l2(full[:B].double().numpy(), out.double().numpy()) < 3e-6
+
+
+def test_conv_input_grad_wino4s_ksplit_accumulate(cuda_dev):
+    """The train step's 16x16 input-gradient conv at B = CUs / 8 through the
+    register-weight F(4x4) kernel with its K split, accumulating into the
+    existing gradient (accumulate = 1: the residual operand aliases the
+    output) -- against float64 autograd <= 1e-5."""
+    from ertdiff import _lib
+    cus = _cus(cuda_dev)
+    B, Cin, Cout, H = cus // 8, 256, 256, 16
+    g = torch.Generator().manual_seed(91)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5
+    dy = torch.randn(B, Cout, H, H, generator=g)
+    prev = torch.randn(B, Cin, H, H, generator=g)
+    ref = torch.nn.grad.conv2d_input((B, Cin, H, H), w.double(), dy.double(), padding=1) + prev.double()
+    lib = _lib.lib()
+    n = lib.ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, 3, 0)
+    ws = torch.empty(n, dtype=torch.uint8, device=cuda_dev)
+    dx = prev.to(cuda_dev)
+    assert lib.ertd_conv_input_grad(dy.to(cuda_dev).data_ptr(), B, H, w.to(cuda_dev).data_ptr(), Cout, Cin, 3, 0,
+                                    dx.data_ptr(), 1, ws.data_ptr(), n, _lib.stream_of(cuda_dev)) == 0
+    err = RN.rel_l2(dx.cpu().double().numpy(), ref.numpy())
+    record_error(f"conv_input_grad_wino4s_ksplit_B{B}", err)
     assert err < 1e-5, err
 
 

@@ -246,8 +246,8 @@ def test_conv2d_workspace_covers_launch_scratch():
     pre-transformed input image (caller-owned, include/ertdiff.h)."""
     lib = _lib.load()
     fp32, bf16 = _lib.PREC_FP32, _lib.PREC_BF16
-    # 256 -> 256 at 16x16, B = 32: 128 F(2x2) tile items < 256 CUs -> K split (at
-    # B = 64 the F(4x4) register-weight kernel has 256 items and no split)
+    # 256 -> 256 at 16x16, B = 32: 128 register-weight F(4x4) tile items fill half
+    # of 256 CUs -> K split (at B = 64 the same kernel has 256 items and no split)
     small = lib.ertd_conv2d_workspace_bytes(256, 256, 3, fp32, 64, 16, 0)
     split = lib.ertd_conv2d_workspace_bytes(256, 256, 3, fp32, 32, 16, 0)
     assert split >= 32 * 256 * 16 * 16 * 4
