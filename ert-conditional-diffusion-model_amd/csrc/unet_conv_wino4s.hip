@@ -55,6 +55,9 @@ constexpr int NRS = 3;                        // producer register sets
 #ifndef WINO4S_PD
 #define WINO4S_PD 2                           // V operand read-ahead (xi pairs)
 #endif
+#ifndef WINO4S_PACK
+#define WINO4S_PACK 1                         // producer stage on packed fp32 pairs
+#endif
 // Ablations for a diagnostic build only (tools/build_variant.sh ... -DWINO4S_ABL=n;
 // results WRONG, never in the shipped library): bit 0 the producers skip the
 // activation and transform, bit 1 every U load reads the first k-step (L2-hot),
@@ -81,6 +84,21 @@ __device__ __forceinline__ void bt6(const float (&d)[6], float (&o)[6]) {
   o[3] = __builtin_fmaf(2.f, e, c);
   o[4] = __builtin_fmaf(-0.5f, e, c);
   o[5] = __builtin_fmaf(1.5f, c, __builtin_fmaf(-2.f, d[3], d[1] + d[5]));
+}
+// bt6 on two columns at once (packed fp32: the same fma / add sequence per
+// element as bt6, so the same bits)
+__device__ __forceinline__ f32x2 pfma(f32x2 a, float c, f32x2 b) {
+  return __builtin_elementwise_fma(a, f32x2{c, c}, b);
+}
+__device__ __forceinline__ void bt6p(const f32x2 (&d)[6], f32x2 (&o)[6]) {
+  const f32x2 c = d[4] - d[2], e = d[3] - d[1];
+  const f32x2 u = d[4] - d[1], v = d[4] + d[1];
+  o[0] = pfma(e, 1.5f, pfma(d[2], -2.f, d[0] + d[4]));
+  o[1] = pfma(d[3], 2.5f, pfma(d[2], 0.5f, u));
+  o[2] = pfma(d[3], 0.5f, pfma(d[2], -2.5f, v));
+  o[3] = pfma(e, 2.f, c);
+  o[4] = pfma(e, -0.5f, c);
+  o[5] = pfma(c, 1.5f, pfma(d[3], -2.f, d[1] + d[5]));
 }
 __device__ __forceinline__ void at6(const f32x2 (&m)[6], f32x2 (&y)[4]) {
   const f32x2 s = m[1] + m[2], d = m[1] - m[2];
@@ -215,6 +233,40 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     // 2+2h and the outer one): the lane transforms its own two columns and takes
     // the outer column's transform from the neighbouring tile's lane (B^T is
     // linear, so transforming before the exchange skips the third column's bt6)
+#if WINO4S_PACK
+    // the lane's two own columns as one packed pair through GroupNorm, SiLU,
+    // the row padding and the column transform (v_pk_* on f32x2: the same fma /
+    // mul / add per element as the scalar form, so the same bits); exp and rcp
+    // have no packed form.  act2[ab][i] = transformed row i of (col a, col b),
+    // actn[ab][i] = that of the outer column (from the neighbour lane)
+    f32x2 act2[2][6];
+    float actn[2][6];
+    auto act_stage = [&](const int set, const int ab) {
+      f32x2 m[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        m[r] = f32x2{raw[set][r].x, raw[set][r].y};
+        if constexpr (ACT != ACT_NONE) {
+          m[r] = __builtin_elementwise_fma(m[r], f32x2{gnv[set].x, gnv[set].x}, f32x2{gnv[set].y, gnv[set].y});
+          if constexpr (ACT == ACT_GN_SILU) {
+            // __expf(-y) = exp2(y * -log2 e): the same v_mul + v_exp as the scalar code
+            f32x2 e = m[r] * f32x2{-1.44269504088896340736f, -1.44269504088896340736f};
+            e = f32x2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)} + f32x2{1.0f, 1.0f};
+            m[r] = m[r] * f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+          }
+        }
+      }
+      m[0] = m[0] * f32x2{pad[set].x, pad[set].x};
+      m[5] = m[5] * f32x2{pad[set].y, pad[set].y};
+      bt6p(m, act2[ab]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const float give = h ? act2[ab][i].y : act2[ab][i].x;
+        const float nb = __int_as_float(__builtin_amdgcn_ds_bpermute(nbaddr, __float_as_int(give)));
+        actn[ab][i] = nb * pad[set].z;
+      }
+    };
+#else
     float act[2][3][6];
     auto act_stage = [&](const int set, const int ab) {
       float cx[6], cy[6];
@@ -246,12 +298,22 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
         act[ab][2][i] = nb * pad[set].z;
       }
     };
+#endif
     auto tr_stage = [&](const int ab, float* vb) {
       float w[6][3];
+#if WINO4S_PACK
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        w[i][0] = act2[ab][i].x;
+        w[i][1] = act2[ab][i].y;
+        w[i][2] = actn[ab][i];
+      }
+#else
 #pragma unroll
       for (int c = 0; c < 3; ++c)
 #pragma unroll
         for (int i = 0; i < 6; ++i) w[i][c] = act[ab][c][i];
+#endif
       // rows 0-2 to the lower half (h = 0), 3-5 to the upper: the rows of 16
       // lanes pair (0,1), (2,3) -- afterwards row[a][j] is row 3h+a of window column j
       float row[3][6];

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(512) void probe(int mode, unsigned long long* out, 
           for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
         }
         for (int j = 0; j < 4; ++j) keep += acc[j][0];
-      } else if constexpr (KIND >= 4) {
+      } else if constexpr (KIND == 4 || KIND == 5) {
         // the MFMA wave itself interleaves NV fma (KIND 4) / exp (KIND 5)
         // fillers per MFMA (independent chains), no partner wave
         f32x4 acc[8] = {};
@@ -81,11 +81,22 @@ __global__ __launch_bounds__(512) void probe(int mode, unsigned long long* out, 
         for (int j = 0; j < NV; ++j) {
           if constexpr (KIND == 2) {
             v[j & 15] = __builtin_amdgcn_exp2f(v[j & 15]) * 0.5f;
-          } else if constexpr (KIND == 1) {
-            f32x2 p{v[j & 15], v[(j + 1) & 15]};
+          } else if constexpr (KIND == 6) {
+            v[j & 15] = __builtin_amdgcn_exp2f(v[j & 15]);
+          } else if constexpr (KIND == 7) {
+            v[j & 15] = __builtin_amdgcn_rcpf(v[j & 15]);
+          } else if constexpr (KIND == 8) {   // independent pairs, packed mul
+            const int k = 2 * (j & 7);
+            f32x2 p{v[k], v[k + 1]};
+            p = p * f32x2{0.999f, 0.998f};
+            v[k] = p.x;
+            v[k + 1] = p.y;
+          } else if constexpr (KIND == 1) {   // independent pairs (v[2k], v[2k+1]), k = j % 8
+            const int k = 2 * (j & 7);
+            f32x2 p{v[k], v[k + 1]};
             p = __builtin_elementwise_fma(p, f32x2{0.999f, 0.998f}, f32x2{0.001f, 0.002f});
-            v[j & 15] = p.x;
-            v[(j + 1) & 15] = p.y;
+            v[k] = p.x;
+            v[k + 1] = p.y;
           } else {
             v[j & 15] = __builtin_fmaf(v[j & 15], 0.999f, 0.001f);
           }
@@ -143,6 +154,13 @@ int main() {
   run<2, 5>("f32 MFMA w/ 2 exp fillers", 1, d, sink, ncu);
   run<4, 5>("f32 MFMA w/ 4 exp fillers", 1, d, sink, ncu);
   run<4, 4>("f32 MFMA w/ 4 fma + partner", 3, d, sink, ncu);
+  // round 4: partner-wave costs of packed fp32, bare transcendentals
+  trio<32, 1>("f32 MFMA + 32 pk_fma", d, sink, ncu);
+  trio<32, 8>("f32 MFMA + 32 pk_mul", d, sink, ncu);
+  trio<32, 6>("f32 MFMA + 32 exp", d, sink, ncu);
+  trio<32, 7>("f32 MFMA + 32 rcp", d, sink, ncu);
+  trio<64, 0>("f32 MFMA + 64 fma", d, sink, ncu);
+  trio<64, 1>("f32 MFMA + 64 pk_fma", d, sink, ncu);
   hipFree(d);
   hipFree(sink);
   return 0;
