@@ -42,6 +42,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ert-conditional-diffusion-model_amd"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -82,6 +83,10 @@ def parse():
                     help="skip the configs[4] measurement (U5 128x128, bf16, 64 members per GPU)")
     ap.add_argument("--no-reference", action="store_true",
                     help="skip the reference-model (R2) measurement in extra")
+    ap.add_argument("--no-evaluation", action="store_true",
+                    help="skip the reference model's test-set evaluation (509 conditions x 50 realisations)")
+    ap.add_argument("--eval-faithful-steps", type=int, default=4,
+                    help="steps of the faithful evaluation schedule timed (its full run is extrapolated)")
     ap.add_argument("--ref-steps", type=int, default=2000)
     ap.add_argument("--ref-warmup", type=int, default=1000,
                     help="untimed R2 steps (a multiple of T keeps every chain launch T steps long)")
@@ -640,6 +645,93 @@ def bench_reference(a, rank, world, dev):
     return out
 
 
+def bench_evaluation(a, rank, world, dev, cpu_steps_per_s=None, cpu_B=None):
+    """The reference's test-set uncertainty evaluation (ERT_Conditional_Diffusion.py
+    :1036-1086: every one of the N_test = 509 test conditions x 50 realisations of
+    sample_model at T = 500 (:290), then inverse transforms + bounds check into the
+    (50, 509, 29) Uncertainty_params array) on the reference's own denoiser.
+    Sharded by condition slice: rank r takes conditions member_range(509, world, r)
+    of the host array (a host-side scatter, no collective) and runs all of its
+    realisations as ONE sampler launch (ertd_sample_conditions, member ids
+    r * 509 + c: the same bits for any world size); strong scaling.  hoisted
+    mode (the condition encoder once per condition) runs the whole evaluation
+    in the timed region, post-processing included; faithful mode (the encoder
+    per member and step, the reference's cost) times a few steps of the
+    per-step schedule at the full 25,450-member width and extrapolates."""
+    from ertdiff.ensemble import member_range
+    from ertdiff.sampler import conditions_x_T
+    N, ns, T = 509, 50, 500
+    c0, c1 = member_range(N, world, rank)
+    nc = c1 - c0
+    torch.manual_seed(42)
+    model = ertdiff.ConditionalDiffusionModel(P, 128).to(dev).eval()
+    host = torch.rand(N, 14, L_MEAS, generator=torch.Generator().manual_seed(1043))   # every rank's copy
+    cond = host[c0:c1].to(dev).contiguous()
+    sched = ertdiff.get_diffusion_schedule(T, device=dev)
+    mn, sc = np.zeros(P), np.full(P, 2.0)
+    lim = np.stack([np.full(P, -1.0), np.full(P, 1.0)], 1)
+    x_T = conditions_x_T(nc, ns, P, T, 3042, c0, N, dev)
+    hp = ertdiff.SamplerPlan(model, cond, T, *sched, mode="hoisted", seed=3042, member_offset=c0,
+                             n_samples=ns, n_conditions_total=N)
+    for _ in range(2):                                  # build + warm
+        hp.x.copy_(x_T)
+        hp.launch()
+    params, valid = ertdiff.postprocess(hp.x.view(ns, nc, P), (mn, sc), lim)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    hp.launch()
+    ertdiff.postprocess(hp.x.view(ns, nc, P), (mn, sc), lim, out=params, valid=valid.view(torch.uint8))
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    member_steps = N * ns * T
+    out = {"workload": f"test-set evaluation: {N} conditions x {ns} realisations x T={T} "
+                       f"(ConditionalDiffusionModel(29,128), cond (N,14,{L_MEAS}) fp32), "
+                       f"condition slices over {world} GPU(s), one sampler launch per rank",
+           "hoisted_evaluation_s": round(el, 4),
+           "hoisted_member_steps_per_s": round(member_steps / el, 1),
+           "postprocess": "ertd_postprocess over the (50, N, 29) block inside the timed region",
+           "finite": bool(torch.isfinite(hp.x).all())}
+    del hp
+    if a.eval_faithful_steps > 0:
+        fp = ertdiff.SamplerPlan(model, cond, T, *sched, mode="faithful", seed=3042, member_offset=c0,
+                                 n_samples=ns, n_conditions_total=N, t_first=T - 1,
+                                 n_run=a.eval_faithful_steps)
+        fp.x.copy_(x_T)
+        fp.launch()
+        barrier(world)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fp.x.copy_(x_T)
+        fp.launch()
+        torch.cuda.synchronize(dev)
+        barrier(world)
+        fel = time.perf_counter() - t0
+        if world > 1:
+            e = torch.tensor([fel], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            fel = float(e.item())
+        per = fel / a.eval_faithful_steps
+        out["faithful_ms_per_step"] = round(per * 1e3, 3)
+        out["faithful_evaluation_s_projected"] = round(per * T, 2)
+        out["faithful_member_steps_per_s"] = round(N * ns / per, 1)
+        out["faithful_step_tflops"] = round(STEP_FLOP_PER_MEMBER * N * ns / per / 1e12, 2)
+        del fp
+    if cpu_steps_per_s:
+        # the reference's loop on the CPU (extra.reference_model.cpu_baseline:
+        # faithful sample_model at B members) -> the same member-step rate here
+        cpu_ms = cpu_steps_per_s * cpu_B
+        out["cpu_evaluation_s_projected"] = round(member_steps / cpu_ms, 1)
+        out["cpu_basis"] = (f"extra.reference_model.cpu_baseline ({cpu_steps_per_s} steps/s at B={cpu_B}, "
+                            f"faithful) x {N * ns * T} member-steps")
+    return out
+
+
 def cpu_unet_baseline(name, seconds, B, T, threads=None):
     """The U-Net spec (oracle/unet_torch.py) on PyTorch-CPU, bounded sample."""
     from oracle import unet_torch as U
@@ -964,6 +1056,9 @@ def main():
         extra["kde_mode"] = bench_kde(dev, world, rank, cpu=not a.no_cpu_baseline)
     if not a.no_reference:
         extra["reference_model"] = bench_reference(a, rank, world, dev)
+    if not a.no_evaluation:
+        rc = extra.get("reference_model", {}).get("cpu_baseline") or {}
+        extra["reference_evaluation"] = bench_evaluation(a, rank, world, dev, rc.get("value"), a.batch)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "denoising-steps/sec",
