@@ -899,6 +899,11 @@ class UNetTrainPlan:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self.loss, self.grads, self._tape = self._body()
+        # the graph addresses the pack registry's per-call-site workspaces and its
+        # descriptor table: hold them, so a later eager step that rebuilds the
+        # registry (new parameters, a new call site) cannot free them under it
+        reg = _packs_of(model, self.B)
+        self._captured_packs = ([e[0] for e in reg.entries.values()], reg.table)
         for nm, p in zip(self.names, self.params):
             self.grads[nm] = self.grads[nm].view_as(p)
 
