@@ -55,6 +55,9 @@ constexpr int NRS = 3;                        // producer register sets
 #ifndef WINO4S_PD
 #define WINO4S_PD 2                           // V operand read-ahead (xi pairs)
 #endif
+#ifndef WINO4S_MPRIO
+#define WINO4S_MPRIO 1                        // s_setprio of the xh = 1 MFMA waves (0 = none): +0.3-0.7 % U2 B=64
+#endif
 #ifndef WINO4S_PACK
 #define WINO4S_PACK 1                         // producer stage on packed fp32 pairs
 #endif
@@ -602,6 +605,9 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   // =================== MFMA waves, xi split over two waves ===================
   constexpr int NP = 9;                        // xi pairs per wave
   const int cb = wave & 3, xh = wave >> 2;
+#if WINO4S_MPRIO
+  if (xh) __builtin_amdgcn_s_setprio(WINO4S_MPRIO);   // static priority for the younger MFMA half
+#endif
   float* xbuf = smem + 2 * V_FL;               // [4 cb][2 receiver][8][64 lanes][4]
   f32x4 acc[2 * NP];
   const int nks = Cin / 4;
