@@ -94,6 +94,8 @@ hipError_t launch_gn_partials(const float* x, int C, int HW, int np, float2* out
 // parts per (sample, channel) the kernel launch_conv would dispatch emits into
 // ConvArgs::gnp (0 = none: the Winograd layers without a K split do)
 int conv_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B);
+// the same for the bf16 / split-bf16 convs (unet_conv_bf16.hip)
+int conv_bf16_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B);
 int wino_gn_parts(const ConvArgs& a, int B);
 
 // sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), the same bits in

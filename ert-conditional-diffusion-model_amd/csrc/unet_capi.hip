@@ -270,7 +270,10 @@ struct Walk {
     }();
     return v;
   }
-  bool gn_parts_on() const { return c->precision == ERTD_PREC_FP32 && gn_fuse_env(); }
+  // every precision: the fp32 Winograd and the bf16 pre-transformed-image
+  // convs emit partials of their outputs; bf16 then applies GN(+SiLU) in the
+  // image pass (act_bf16_kernel) without reading the activation for statistics
+  bool gn_parts_on() const { return gn_fuse_env(); }
   const PartRec& parts_of(const float* X, int C, int HW) {
     auto it = parts.find(X);
     if (it != parts.end()) return it->second;
@@ -335,7 +338,8 @@ struct Walk {
       q.wpk_wino = L->offw.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
       q.wpk_wino4 = L->offw4.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
       q.ksplit_buf = want_split ? reinterpret_cast<float*>(16) : nullptr;
-      const int np = conv_gn_parts(ks, mode, act, q, B);
+      const int np = bf_prec(c->precision) ? conv_bf16_gn_parts(ks, mode, act, q, B)
+                                           : conv_gn_parts(ks, mode, act, q, B);
       if (np > 0) {
         gnp = (float2*)alloc((size_t)B * Cout * np * 2);
         parts[out] = PartRec{gnp, np};

@@ -39,6 +39,17 @@ __device__ __forceinline__ unsigned lds_addr_h(const void* p) {
 
 __host__ __device__ constexpr int convh_ck(int ks) { return ks == 3 ? 16 : 32; }
 
+// fp32 sum over the 64 lanes of a wave in a fixed order, the same bits in
+// every lane: row sums by DPP (row16_sum), then (r0 + r1) + (r2 + r3)
+__device__ __forceinline__ float wave_sum_f(float v) {
+  v = row16_sum(v);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 // SP = operand planes: 1 = bf16, 2 = split bf16 (x = hi + lo, both bf16 RNE;
 // every product as lo_a*hi_b + hi_a*lo_b + hi_a*hi_b on the MFMA, fp32
 // accumulate: ~2^-16 relative per product instead of bf16's 2^-8).  A split
@@ -397,6 +408,21 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
       if (has_eb) v = v + e.y;
       if (has_res) v = v + rv[i % RV][j];
       *reinterpret_cast<f32x4*>(a.out + ((size_t)b * a.Cout + co) * HWo + p0 + 4 * q) = v;
+      if constexpr (G::BM % 256 == 0 && (G::BM / 4) % 64 == 0) {
+        // GroupNorm partials of the output (conv_bf16_gn_parts): with 256- or
+        // 512-px tiles one wave's 64 lanes x 4 px are 256 px of one channel (cl
+        // is wave-uniform); each 16-lane DPP row -- 64 consecutive px -- is one
+        // part, {sum, M2 about the part mean} as the fp32 epilogues emit them
+        // (row sums only: no cross-row readlanes, 4x the parts for the finalize)
+        if (a.gnp) {
+          const float sm = row16_sum((v[0] + v[1]) + (v[2] + v[3]));
+          const float mu = sm * (1.0f / 64.0f);
+          const float d0 = v[0] - mu, d1 = v[1] - mu, d2 = v[2] - mu, d3 = v[3] - mu;
+          const float m2 = row16_sum(fmaf(d3, d3, fmaf(d2, d2, fmaf(d1, d1, d0 * d0))));
+          if ((lane & 15) == 0)
+            a.gnp[((size_t)b * a.Cout + co) * (HWo / 64) + (p0 + 4 * q) / 64] = make_float2(sm, m2);
+        }
+      }
     }
   }
 }
@@ -424,7 +450,10 @@ __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G1
   const int HWs = UPS ? a.Ws * a.Ws : HW;
   const int p = UPS ? ((po / a.Wo) >> 1) * a.Ws + ((po % a.Wo) >> 1) : po;
   const long long r = i4 / HW4;
-  const int g = (int)(r % G16), b = (int)(r / G16);
+  // a wave's 64 pixels lie in one (sample, 16-channel group) (HW4 % 64 == 0 for
+  // every image here): (b, g) wave-uniform, so the GN table is read by scalar loads
+  const int g = __builtin_amdgcn_readfirstlane((int)(r % G16));
+  const int b = __builtin_amdgcn_readfirstlane((int)(r / G16));
   const int Cin = a.Cin, Ca = a.Ca;
   float v[16][PX];
 #pragma unroll
@@ -722,6 +751,7 @@ static hipError_t launch_pre_w4(const ConvArgs& a, int B, hipStream_t s) {
 template <int SP>
 static hipError_t launch_act_img(const ConvArgs& a, int act, bool up, int B, hipStream_t s) {
   const int HW = a.Wo * a.Wo, G16 = (a.Cin + 15) / 16;
+  if ((HW / (up ? 4 : 1)) % 64) return hipErrorInvalidValue;   // a wave = one (sample, group)
   const long long n = (long long)B * G16 * HW;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   const unsigned blocks4 = (unsigned)((n / 4 + 255) / 256);   // the UPS kernel: 4 pixels per thread
@@ -803,8 +833,20 @@ static hipError_t launch_conv_h(int ks, int mode, int act, const ConvArgs& a, in
   return hipErrorInvalidValue;
 }
 
+// parts per (sample, channel) of the GroupNorm partials the dispatched bf16
+// conv emits (the pre-transformed-image 3x3 / Upsample convs: 256- and
+// 512-px output tiles; parts of 64 px), 0 = none
+int conv_bf16_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B) {
+  (void)B;
+  if (a.Cout == 1 || ks != 3 || a.Ho != a.Wo || (a.Wo * a.Wo) % 256) return 0;
+  const bool pre = convh_pre() == 1 && ((mode == MODE_S1 && act != ACT_NONE) || (mode == MODE_UP && act == ACT_NONE));
+  if (!pre || convh_tpx_override() == 1) return 0;
+  return a.Wo * a.Wo / 64;
+}
+
 hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
+  if (a.gnp && (!a.bimg || conv_bf16_gn_parts(ks, mode, act, a, B) == 0)) return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;
   // conv_in / conv_out are fp32-VALU kernels: bf16 rounds their operands,
