@@ -436,13 +436,17 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void 
 // UPS: nearest x2 upsample folded in (output pixel (y, x) reads source
 // (y/2, x/2)), so an Upsample conv becomes a stride-1 conv on the image.
 // SP = 2: split-bf16 records [16 hi][16 lo] (64 B per pixel)
+#ifndef ACT_PXG
+#define ACT_PXG 1
+#endif
 template <int ACT, bool UPS = false, int SP = 1>
 __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G16, int HW) {
   // UPS: four horizontally adjacent output pixels per thread -- one float2 of
   // the source row per channel plane, four 32-B records stored contiguously
   // (U3 B=256 upsample images 129 -> 95 us); the GN(+SiLU) images keep one
-  // pixel per thread (four measured slower: 332 -> 384 us, longer chains)
-  constexpr int PX = UPS ? 4 : 1;
+  // pixel per thread (ACT_PXG: two measured 109.5 -> 99.5 U3 B=256 steps/s,
+  // four 332 -> 384 us per image, longer chains)
+  constexpr int PX = UPS ? 4 : ACT_PXG;
   const long long i4 = (long long)blockIdx.x * 256 + threadIdx.x;
   const int HW4 = HW / PX;
   if (i4 >= (long long)B * G16 * HW4) return;
@@ -468,6 +472,10 @@ __global__ __launch_bounds__(256) void act_bf16_kernel(ConvArgs a, int B, int G1
         const float2 t = *reinterpret_cast<const float2*>(src + p);
         v[j][0] = v[j][1] = t.x;
         v[j][PX - 2] = v[j][PX - 1] = t.y;
+      } else if constexpr (PX == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(src + p);
+        v[j][0] = t.x;
+        v[j][1] = t.y;
       } else {
         v[j][0] = src[p];
       }
@@ -751,9 +759,9 @@ static hipError_t launch_pre_w4(const ConvArgs& a, int B, hipStream_t s) {
 template <int SP>
 static hipError_t launch_act_img(const ConvArgs& a, int act, bool up, int B, hipStream_t s) {
   const int HW = a.Wo * a.Wo, G16 = (a.Cin + 15) / 16;
-  if ((HW / (up ? 4 : 1)) % 64) return hipErrorInvalidValue;   // a wave = one (sample, group)
+  if ((HW / (up ? 4 : ACT_PXG)) % 64) return hipErrorInvalidValue;   // a wave = one (sample, group)
   const long long n = (long long)B * G16 * HW;
-  const unsigned blocks = (unsigned)((n + 255) / 256);
+  const unsigned blocks = (unsigned)((n / ACT_PXG + 255) / 256);
   const unsigned blocks4 = (unsigned)((n / 4 + 255) / 256);   // the UPS kernel: 4 pixels per thread
   if (up) act_bf16_kernel<ACT_NONE, true, SP><<<blocks4, 256, 0, s>>>(a, B, G16, HW);
   else if (act == ACT_GN_SILU) act_bf16_kernel<ACT_GN_SILU, false, SP><<<blocks, 256, 0, s>>>(a, B, G16, HW);
