@@ -65,6 +65,13 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 #ifndef CHAIN_MAX_BPC
 #define CHAIN_MAX_BPC 5  // resident blocks per CU used at most
 #endif
+// strips per claimed work item: a worker runs SPI consecutive strips of one
+// (member, step) back to back and publishes them with ONE drain + arrival
+// (the publish -- write-through stores, vmcnt(0), a barrier, an atomic round
+// trip -- cost ~1.4 us per strip, ~10 % of a worker's time, at SPI = 1)
+#ifndef CHAIN_SPI
+#define CHAIN_SPI 2
+#endif
 constexpr uint64_t SPIN_TIMEOUT_TICKS = 50000000ull;  // 0.5 s of s_memrealtime (100 MHz)
 
 // A zero the compiler cannot see through: loads addressed with it stay inside
@@ -208,6 +215,7 @@ struct ChainSmem {
   int abort;  // worker: set once, never cleared
   int seen;   // worker: chain progress last observed by lane 0 (written before a barrier)
   int next;   // worker: the item claimed for after the current one
+  float keep[CHAIN_SPI][C2];  // worker: each strip's channel sums until the item's publish
 };
 
 }  // namespace
@@ -363,7 +371,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   __syncthreads();
   const int wid = blockIdx.x - B - 1;
   const int b = wid % B;
-  const unsigned n_items = (unsigned)a.n_run * (unsigned)S;
+  const int NPS = (S + CHAIN_SPI - 1) / CHAIN_SPI;   // work items per step
+  const unsigned n_items = (unsigned)a.n_run * (unsigned)NPS;
   const int L1 = conv_len(a.L), L2 = conv_len(L1);
   gu32* claim = (gu32*)(a.claim + (size_t)b * SYNC_PAD);
   if (tid == 0)
@@ -377,8 +386,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     // claim the following item now; its ticket returns while this one runs
     unsigned nxt = 0;
     if (tid == 0) nxt = __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int i = (int)(item / (unsigned)S);
-    const int s = (int)(item - (unsigned)i * S);
+    const int i = (int)(item / (unsigned)NPS);
+    const int s0 = (int)(item - (unsigned)i * NPS) * CHAIN_SPI;
+    const int ns = S - s0 < CHAIN_SPI ? S - s0 : CHAIN_SPI;   // strips of this item
     const int z0 = opaque0();
     const int tid_i = opaque_tid();
     const float* pk = packed + z0;
@@ -404,8 +414,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     const unsigned long long wt1_ = __builtin_amdgcn_s_memrealtime();
     if (tid == 0 && b == 0 && item < 4096) g_item[item][1] = wt1_;
 #endif
-    enc_strip_fp32<false>(sm.enc, pk, w.enc0_b + z0, w.enc2_b + z0, a.cond, a.cstride, a.L, L1, L2, b, cond_row(b, a.ncond), s,
-                          nullptr, nullptr, tid_i);
+    // one inlined strip body (a second inlined copy spills), run ns times,
+    // with fresh opaque offsets so its weight loads are not hoisted out of the
+    // loop; keep[u][tid] is written and later read by the same thread
+#pragma unroll 1
+    for (int u = 0; u < ns; ++u) {
+      const int zu = opaque0(), tu = opaque_tid();
+      enc_strip_fp32<false>(sm.enc, packed + zu, w.enc0_b + zu, w.enc2_b + zu, a.cond, a.cstride, a.L, L1, L2, b,
+                            cond_row(b, a.ncond), s0 + u, nullptr, nullptr, tu);
+      if (tid < C2) sm.keep[u][tid] = sm.enc.red[0][tid] + sm.enc.red[1][tid];
+    }
     WACC(2, wt1_);
 #ifdef ERTD_CHAIN_STAMPS
     const unsigned long long wt2_ = __builtin_amdgcn_s_memrealtime();
@@ -416,17 +434,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     // publish: write-through partial stores, drained by every storing wave,
     // then one relaxed arrival; the last arriver reads them with sc1 loads
     // (no release/acquire fences: Guideline 16, form R1)
-    if (tid < C2) st_sc1(part + ((size_t)b * S + s) * C2 + tid, sm.enc.red[0][tid] + sm.enc.red[1][tid]);
+    if (tid < C2) {
+#pragma unroll 1
+      for (int u = 0; u < ns; ++u) st_sc1(part + ((size_t)b * S + s0 + u) * C2 + tid, sm.keep[u][tid]);
+    }
     drain();
     __syncthreads();
     if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add((gu32*)(a.cnt + ((size_t)slot * B + b) * SYNC_PAD), 1u,
+      const unsigned old = __hip_atomic_fetch_add((gu32*)(a.cnt + ((size_t)slot * B + b) * SYNC_PAD), (unsigned)ns,
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned pv = ld_relaxed(a.progress + (size_t)b * SYNC_PAD);  // same round trip as the arrival
       seen_reg = pv > seen_reg ? pv : seen_reg;
       sm.seen = (int)seen_reg;
       sm.next = (int)nxt;
-      sm.flag = old == (unsigned)(S * (i / R + 1) - 1);
+      sm.flag = old + (unsigned)ns == (unsigned)(S * (i / R + 1));
     }
     __syncthreads();
     WACC(3, wt2_);

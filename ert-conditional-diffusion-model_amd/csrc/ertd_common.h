@@ -287,7 +287,10 @@ struct FaithfulChainArgs {
   float* uring;                  // (R, B, 128) condition rows u_i[b]
   float* V;                      // (n_run, 128) time rows v(t_first - i)
 };
-constexpr int CHAIN_RING = 8;
+#ifndef ERTD_CHAIN_RING
+#define ERTD_CHAIN_RING 16  // (a -D override is for same-box variant A/Bs only)
+#endif
+constexpr int CHAIN_RING = ERTD_CHAIN_RING;
 // Every sync word of the chain sits alone in a 128-B line: words polled or
 // updated by hundreds of blocks serialize per line (measured: progress words
 // of 16 members sharing one line slowed every memory access on the chip 3-5x).

@@ -113,9 +113,10 @@ def test_faithful_equals_hoisted_bitwise(gpu_model, cuda_dev):
 
 
 @pytest.mark.parametrize("B,L,T", [(1, 1, 3), (3, 37, 20), (5, 250, 17), (2, 4694, 9),
-                                   (7, 1003, 40), (40, 4693, 12)])
+                                   (7, 1003, 40), (40, 4693, 12), (4, 2600, 35)])
 def test_faithful_schedules_bitwise(B, L, T, gpu_model, cuda_dev):
-    """The persistent chain (ring of 8 slots: T > 8 wraps it), the per-step
+    """The persistent chain (ring of 16 slots: T > 16 wraps it; work items of
+    two strips, the last one a single strip when S is odd), the per-step
     schedule and the hoisted sampler agree bit for bit on ragged shapes, with
     injected (reference-order) noise."""
     cond = torch.from_numpy(synth_uniform((B, 14, L), 500 + L)).to(cuda_dev)

@@ -79,16 +79,17 @@ int main(int argc, char** argv) {
   static unsigned long long it[4096][4];
   CK(hipMemcpyFromSymbol(it, HIP_SYMBOL(g_item), sizeof(it)));
   printf("member 0 items around step 100 (us rel. chain0 step-0 wait start): item step strip | start poll-done strip-done pub | chain0 step(i) wait-start ready end\n");
-  for (int k = 19 * 100; k < 19 * 104; ++k) {
-    const int i = k / 19;
-    printf("  %5d %4d %2d | %9.1f %9.1f %9.1f %9.1f | %9.1f %9.1f %9.1f\n", k, i, k % 19, rl(it[k][0]), rl(it[k][1]), rl(it[k][2]), rl(it[k][3]),
+  const int NPS = (S + CHAIN_SPI - 1) / CHAIN_SPI;  // work items per step
+  for (int k = NPS * 100; k < NPS * 104; ++k) {
+    const int i = k / NPS;
+    printf("  %5d %4d %2d | %9.1f %9.1f %9.1f %9.1f | %9.1f %9.1f %9.1f\n", k, i, (k % NPS) * CHAIN_SPI, rl(it[k][0]), rl(it[k][1]), rl(it[k][2]), rl(it[k][3]),
            rl(cst[0][i][0]), rl(cst[0][i][1]), rl(cst[0][i][2]));
   }
   double tot[8] = {}; int nw = grid - B - 1;
   for (int k = 0; k < nw && k < 2048; ++k) for (int j = 0; j < 8; ++j) tot[j] += wacc[k][j];
   const double items = tot[5];
   printf("workers: items %.0f (%.1f/worker), last-arrivals %.0f, progress polls %.0f\n", items, items / nw, tot[6], tot[0]);
-  printf("  per strip item: wait %.2f us, strip %.2f us, publish %.2f us; per last arrival cond row %.2f us\n",
+  printf("  per work item (%d strips): wait %.2f us, strip %.2f us, publish %.2f us; per last arrival cond row %.2f us\n", CHAIN_SPI,
          tot[1] / items / 100, tot[2] / items / 100, tot[3] / items / 100, tot[4] / std::max(1.0, tot[6]) / 100);
   printf("  worker span avg %.2f ms\n", tot[7] / nw / 1e5);
   return 0;
