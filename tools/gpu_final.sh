@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-end evidence at HEAD: pytest -m gpu, smoke, bench (default args), the
 # serialized U2 per-layer trace, rocprofv3 --kernel-trace --stats of a short bench
-# (U2 headline only), and the train-step kernel profile
+# (U2 headline only), the train-step kernel profile, and with PMC=1 the U2 B=64
+# fp32 PMC traffic pass.  SKIP_TESTS=1 / SKIP_BENCH=1 as in gpu_run.sh.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 bash tools/gpu_run.sh || exit $?
@@ -12,3 +13,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   --no-kde --no-reference --no-unet-train > gpurun_out/bprof.log 2>&1
 echo "[bench prof] rc=$?"
 bash tools/gpu_train_prof.sh
+[ "${PMC:-0}" = 1 ] && { CFG=U2 B=64 PREC=fp32 bash tools/unet_traffic.sh; echo "[u2 pmc] rc=$?"; }
+exit 0

@@ -63,6 +63,7 @@ rows = [r for r in csv.DictReader(open(sys.argv[1])) if any(k in r["Kernel_Name"
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 last = rows[-len(layers):]
 tot_t = tot_f = 0
+fam = {}   # kernel family -> [us, executed FLOP, peak]
 for (n, cin, cout, ks, wo), r in zip(layers, last):
     us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
     fl = 2 * cin * cout * ks * ks * wo * wo * B
@@ -83,9 +84,14 @@ for (n, cin, cout, ks, wo), r in zip(layers, last):
     tot_f += fl
     peak = 2500.0 if "conv_bf16_kernel<" in r["Kernel_Name"] else 157.3   # dense bf16 / fp32 MFMA peak
     tmpl = r["Kernel_Name"][r["Kernel_Name"].find("<"):r["Kernel_Name"].find(">") + 1]
+    k = r["Kernel_Name"][:r["Kernel_Name"].find("<")].split("::")[-1].split(" ")[-1]
+    a = fam.setdefault(k, [0.0, 0, peak, 0])
+    a[0] += us; a[1] += fl; a[3] += 1
     wgs = int(r["Grid_Size_X"]) // int(r.get("Workgroup_Size_X", 256) or 256) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
     print(f"{n:14s} {cin:4d}->{cout:4d} k{ks} {wo:3d}  {tmpl:22s} wg {wgs:5d}  {us:8.1f} us  "
           f"{fl / us / 1e6:7.1f} TF  {fl / us / 1e6 / peak * 100:5.1f}%  (alg {alg / us / 1e6:6.1f} TF)")
 print(f"total {tot_t:.0f} us, {tot_f / tot_t / 1e6:.1f} TF (executed FLOP; * = sub-pixel Upsample, "
       f"4 of 9 taps; w = Winograd F(2x2,3x3), 16 of 36 multiplies; W = F(4x4,3x3), 36 of 144; S = the same, register-weight schedule; "
       f"% of the fp32 peak, of the bf16 peak for bf16 kernels)")
+for k, (us, fl, peak, n) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
+    print(f"  {k:22s} {n:3d} launches {us:8.1f} us  {fl / us / 1e6:7.1f} TF executed  {fl / us / 1e6 / peak * 100:5.1f}% of peak")
