@@ -12,7 +12,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
     -- python3 tools/unet_probe.py --config $CFG --B $B --precision $PREC --steps $STEPS > gpurun_out/upmc_$c.log 2>&1
   rc=$?; echo "[pmc $c] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-cp -f profiles/kernel_traffic.json gpurun_out/kernel_traffic.json
+# several passes in one call accumulate into one file
+[ -f gpurun_out/kernel_traffic.json ] || cp -f profiles/kernel_traffic.json gpurun_out/kernel_traffic.json
 # the probe runs 7 forwards and 2 x STEPS sampler steps; forward = one step's kernels
 UNET_STEPS=$((7 + 2 * STEPS)) UNET_KEY=unet_${CFG}_B${B}_${PREC}_step \
   UNET_WORKLOAD="tools/unet_probe.py $CFG $PREC B=$B L=4693 (7 forwards + $((2 * STEPS)) sampler steps)" \
