@@ -177,6 +177,97 @@ __global__ __launch_bounds__(256) void wgw_d_kernel(WgwArgs a) {
   }
 }
 
+#ifndef WGW_LDS
+#define WGW_LDS 1  // 1: LDS-staged workgroup tiles (wgw_gemm_lds_kernel); 0: wave tasks (A/B)
+#endif
+
+// one workgroup per (xi, co block 64 MB, ci block 64 NB, K range).  Per 16-k
+// block the workgroup stages its D rows (64 MB) and V rows (64 NB) in LDS
+// once -- each lane one float4 per 256 row-quads, rows padded to 20 floats so
+// the fragment reads are conflict-free -- and wave (wm, wn) of the 2 x 2 wave
+// grid multiplies rows [32 MB wm, +32 MB) by columns [32 NB wn, +32 NB): every
+// operand byte crosses L2 -> CU once per workgroup instead of once per wave
+// (wgw_gemm_kernel), and the four waves read it from LDS.  Same K permutation,
+// fma order and K ranges as wgw_gemm_kernel: the partials are bitwise equal.
+template <int MB, int NB>
+__global__ __launch_bounds__(256) void wgw_gemm_lds_kernel(WgwArgs a) {
+  constexpr int RA = 64 * MB, RB = 64 * NB, PITCH = 20;   // rows per operand, floats per LDS row
+  constexpr int WI = 2 * MB, WJ = 2 * NB;                 // 16 x 16 blocks per wave
+  __shared__ __attribute__((aligned(16))) float lds[2][(RA + RB) * PITCH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int Cin = a.Ca + a.Cb;
+  const int ncb = Cin / RB, nmb = a.Cout / RA;
+  int r = blockIdx.x;
+  const int nb = r % ncb; r /= ncb;
+  const int mb = r % nmb; r /= nmb;
+  const int xi = r % NX;
+  const int ks = r / NX;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int q0 = ks * (a.kr / 16), q1 = min(q0 + a.kr / 16, a.T / 16);
+  // staging: thread tid moves row-quad f = tid + 256 u: row f >> 2, k-quad f & 3
+  const f32x4* Dsrc = reinterpret_cast<const f32x4*>(a.D + ((size_t)xi * a.Cout + mb * RA) * a.T);
+  const f32x4* Vsrc = reinterpret_cast<const f32x4*>(a.V + ((size_t)xi * Cin + nb * RB) * a.T);
+  const size_t T4 = (size_t)a.T / 4;
+  f32x4 stg[MB + NB];
+  auto gload = [&](int Q) {
+#pragma unroll
+    for (int u = 0; u < MB + NB; ++u) {
+      const int f = tid + 256 * u;
+      const int row = u < MB ? f >> 2 : (f - 256 * MB) >> 2, kq = f & 3;
+      stg[u] = (u < MB ? Dsrc : Vsrc)[(size_t)row * T4 + 4 * Q + kq];
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < MB + NB; ++u) {
+      const int f = tid + 256 * u;
+      const int row = u < MB ? f >> 2 : RA + ((f - 256 * MB) >> 2), kq = f & 3;
+      *reinterpret_cast<f32x4*>(&lds[buf][row * PITCH + 4 * kq]) = stg[u];
+    }
+  };
+  f32x4 acc[WI][WJ];
+#pragma unroll
+  for (int i = 0; i < WI; ++i)
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) acc[i][j] = f32x4{};
+  if (q0 < q1) {
+    gload(q0);
+    lstore(0);
+    __syncthreads();
+    for (int Q = q0; Q < q1; ++Q) {
+      const int buf = (Q - q0) & 1;
+      if (Q + 1 < q1) gload(Q + 1);
+      f32x4 av[WI], bv[WJ];
+#pragma unroll
+      for (int i = 0; i < WI; ++i)
+        av[i] = *reinterpret_cast<const f32x4*>(&lds[buf][(32 * MB * wm + 16 * i + c16) * PITCH + 4 * g]);
+#pragma unroll
+      for (int j = 0; j < WJ; ++j)
+        bv[j] = *reinterpret_cast<const f32x4*>(&lds[buf][(RA + 32 * NB * wn + 16 * j + c16) * PITCH + 4 * g]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < WI; ++i)
+#pragma unroll
+          for (int j = 0; j < WJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][k], bv[j][k], acc[i][j], 0, 0, 0);
+      if (Q + 1 < q1) lstore(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // lane holds rows co = RA mb + 32 MB wm + 16 i + 4 g + e, column ci = RB nb + 32 NB wn + 16 j + c16
+  float* P = a.P + (((size_t)ks * NX + xi) * a.Cout) * Cin;
+  const int co0 = RA * mb + 32 * MB * wm, ci0 = RB * nb + 32 * NB * wn;
+#pragma unroll
+  for (int i = 0; i < WI; ++i)
+#pragma unroll
+    for (int j = 0; j < WJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        P[(size_t)(co0 + 16 * i + 4 * g + e) * Cin + ci0 + 16 * j + c16] = acc[i][j][e];
+}
+
 // one wave per task (xi, co block 64, ci block 64, K range); 4 waves per workgroup
 __global__ __launch_bounds__(256) void wgw_gemm_kernel(WgwArgs a, int ntask) {
   const int lane = threadIdx.x & 63;
@@ -305,6 +396,7 @@ int wgw_env() {
 
 struct WgwPlan {
   int T, nks, kr;
+  int mb, nb;       // LDS path: workgroup tile (64 mb co) x (64 nb ci)
   size_t v, d, p;   // floats
 };
 
@@ -312,13 +404,23 @@ bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
   if (Cin % 64 || Cout % 64 || (H != 16 && H != 32 && H != 64) || B < 1) return false;
   const int T = B * (H / 4) * (H / 4);
   if (T % 16) return false;
-  const int base = NX * (Cout / 64) * (Cin / 64);
+  pl->mb = Cout % 128 == 0 ? 2 : 1;
+  pl->nb = Cin % 128 == 0 ? 2 : 1;
   const int nq = T / 16;                         // 16-k blocks
+#if WGW_LDS
+  const int base = NX * (Cout / (64 * pl->mb)) * (Cin / (64 * pl->nb));
+  static const int target = [] {                 // ERTD_WGW_TASKS: workgroup target (A/B)
+    const int v = ERTD_KNOB("WGW_TASKS", 512);
+    return v > 0 ? v : 512;
+  }();
+#else
+  const int base = NX * (Cout / 64) * (Cin / 64);
   static const int target = [] {                 // ERTD_WGW_TASKS: wave-task target (A/B)
     const int v = ERTD_KNOB("WGW_TASKS", 2048);
     return v > 0 ? v : 2048;
   }();
-  int nks = (target + base - 1) / base;          // ~2048 wave tasks (8 waves per CU)
+#endif
+  int nks = (target + base - 1) / base;          // ~2 workgroups (8 waves) per CU
   if (nks > nq) nks = nq;
   if (nks < 1) nks = 1;
   const int qpr = (nq + nks - 1) / nks;
@@ -364,8 +466,16 @@ hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const floa
   if (e != hipSuccess) return e;
   wgw_d_kernel<<<(unsigned)((nd + 255) / 256), 256, 0, s>>>(a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+#if WGW_LDS
+  const unsigned nwg = (unsigned)(pl.nks * NX * (Cout / (64 * pl.mb)) * (Cin / (64 * pl.nb)));
+  if (pl.mb == 2 && pl.nb == 2) wgw_gemm_lds_kernel<2, 2><<<nwg, 256, 0, s>>>(a);
+  else if (pl.mb == 2) wgw_gemm_lds_kernel<2, 1><<<nwg, 256, 0, s>>>(a);
+  else if (pl.nb == 2) wgw_gemm_lds_kernel<1, 2><<<nwg, 256, 0, s>>>(a);
+  else wgw_gemm_lds_kernel<1, 1><<<nwg, 256, 0, s>>>(a);
+#else
   const int ntask = pl.nks * NX * (Cout / 64) * (Cin / 64);
   wgw_gemm_kernel<<<(unsigned)((ntask + 3) / 4), 256, 0, s>>>(a, ntask);
+#endif
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const size_t nw = (size_t)Cout * Cin;
   if (pl.nks > 1) {

@@ -173,6 +173,8 @@ def test_unet_train_rejects_bf16(cuda_dev):
     (64, 0, 64, 64, 3, 0, 32),     # ... at the train step's B = 32 (Winograd F(4x4) wgrad)
     (384, 128, 256, 16, 3, 0, 32), # the widest decoder conv1 at B = 32
     (128, 64, 64, 32, 3, 0, 2),    # concat input, Cout < Cin
+    (128, 64, 128, 32, 3, 0, 2),   # Winograd wgrad tile 128 co x 64 ci (Cin % 128 != 0)
+    (64, 64, 64, 32, 3, 0, 2),     # ... 64 co x 128 ci
     (256, 0, 256, 16, 3, 0, 2),
     (1, 0, 32, 32, 3, 0, 2),       # conv_in: Cin = 1 (masked ci tile)
     (32, 0, 1, 32, 3, 0, 2),       # conv_out: Cout = 1 (masked co tile)
