@@ -175,7 +175,10 @@ hipError_t launch_conv1x1(const ConvArgs& a, int B, hipStream_t s);
 size_t wgrad_wino_ws_floats(int Cin, int Cout, int B, int H, int ks, int mode);
 hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B,
                              int H, int Cout, int mode, const float* gn, int act, float* dw,
-                             int accumulate, float* ws, hipStream_t s);
+                             int accumulate, float* ws, hipStream_t s, float* db = nullptr,
+                             float* db2 = nullptr);
+// the Winograd path can also return the conv's bias gradient (sum of dy)
+bool wgrad_wino_bias_ok(int Cin, int Cout, int B, int H, int ks, int mode);
 // packed floats of one conv's weights
 size_t conv_packed_floats(int cin, int cout, int ks);
 hipError_t launch_pack_conv(const float* w, int cin, int cout, int ks, float* dst, hipStream_t s,

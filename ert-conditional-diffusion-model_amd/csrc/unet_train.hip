@@ -76,6 +76,12 @@ __device__ __forceinline__ double wg_sum(double v, double* red, int tid) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -95,8 +101,9 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
     const float* __restrict__ xa, int Ca, const float* __restrict__ xb, int Cb, int HW, int groups,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float2* __restrict__ mr,
     int act, const float* __restrict__ dy, float* __restrict__ dxa, float* __restrict__ dxb,
-    int accumulate, float* __restrict__ dgb) {
+    int accumulate, float* __restrict__ dgb, float* __restrict__ csum, long long ldc) {
   __shared__ double part[2][GNB_CB][4];
+  __shared__ float cred[GNB_CB][4];
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int C = Ca + Cb, cpg = C / groups, HW4 = HW / 4;
   const int wpc = HW4 >= 256 ? 4 : (HW4 >= 128 ? 2 : 1);   // waves per channel
@@ -168,15 +175,29 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
     float4* dx = (float4*)(c < Ca ? dxa + ((size_t)b * Ca + c) * HW : dxb + ((size_t)b * Cb + c - Ca) * HW);
     const float4* d = (const float4*)(dy + ((size_t)b * C + c) * HW);
     const float ga = gamma[c], be = beta[c];
+    float cs = 0.f;
     for (int p = p0; p < HW4; p += pst) {
       const float4 xv = x[p], dv = d[p];
       float4 o = accumulate ? dx[p] : float4{0.f, 0.f, 0.f, 0.f};
-      float xh, dn;
-      dn = dxn_of(xv.x, dv.x, ga, be, xh); o.x += rstd * ((ga * dn - mA) - xh * mB);
-      dn = dxn_of(xv.y, dv.y, ga, be, xh); o.y += rstd * ((ga * dn - mA) - xh * mB);
-      dn = dxn_of(xv.z, dv.z, ga, be, xh); o.z += rstd * ((ga * dn - mA) - xh * mB);
-      dn = dxn_of(xv.w, dv.w, ga, be, xh); o.w += rstd * ((ga * dn - mA) - xh * mB);
+      float xh, dn, q0, q1, q2, q3;
+      dn = dxn_of(xv.x, dv.x, ga, be, xh); q0 = rstd * ((ga * dn - mA) - xh * mB); o.x += q0;
+      dn = dxn_of(xv.y, dv.y, ga, be, xh); q1 = rstd * ((ga * dn - mA) - xh * mB); o.y += q1;
+      dn = dxn_of(xv.z, dv.z, ga, be, xh); q2 = rstd * ((ga * dn - mA) - xh * mB); o.z += q2;
+      dn = dxn_of(xv.w, dv.w, ga, be, xh); q3 = rstd * ((ga * dn - mA) - xh * mB); o.w += q3;
       dx[p] = o;
+      cs += (q0 + q1) + (q2 + q3);
+    }
+    if (csum) {
+      cs = wave_sum_f(cs);
+      if (lane == 0) cred[cl][wl] = cs;   // cpg <= GNB_CB when csum is requested
+    }
+  }
+  if (csum) {
+    __syncthreads();
+    if (tid < cpg) {
+      const float s = wpc == 4 ? (cred[tid][0] + cred[tid][1]) + (cred[tid][2] + cred[tid][3])
+                               : (wpc == 2 ? cred[tid][0] + cred[tid][1] : cred[tid][0]);
+      csum[(size_t)b * ldc + g * cpg + tid] = s;
     }
   }
 }
@@ -625,19 +646,37 @@ int ertd_gn_act_apply(const float* x, int Ca, const float* x2, int Cb, int B, in
   return rcode(hipGetLastError());
 }
 
+static int gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                           const float* gamma, const float* beta, const float* mr, int act,
+                           const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
+                           float* csum, long long ldc, void* stream) {
+  const int C = Ca + Cb;
+  if (!x || !gamma || !beta || !mr || !dy || !dx || !dgb_part || B < 1 || Ca < 1 || Cb < 0 ||
+      (Cb > 0 && (!x2 || !dx2)) || groups < 1 || C % groups || HW < 4 || HW % 4 ||
+      (act != ACT_GN_SILU && act != ACT_GN) || (csum && (C / groups > GNB_CB || ldc < C)))
+    return ERTD_EINVAL;
+  const dim3 grid(groups, B);
+  hipStream_t s = (hipStream_t)stream;
+  gn_act_bwd_kernel<<<grid, 256, 0, s>>>(x, Ca, x2, Cb, HW, groups, gamma, beta, (const float2*)mr, act,
+                                         dy, dx, dx2, accumulate, dgb_part, csum, ldc);
+  return rcode(hipGetLastError());
+}
+
 int ertd_gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
                          const float* gamma, const float* beta, const float* mr, int act,
                          const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
                          void* stream) {
-  const int C = Ca + Cb;
-  if (!x || !gamma || !beta || !mr || !dy || !dx || !dgb_part || B < 1 || Ca < 1 || Cb < 0 ||
-      (Cb > 0 && (!x2 || !dx2)) || groups < 1 || C % groups || HW < 4 || HW % 4 ||
-      (act != ACT_GN_SILU && act != ACT_GN))
-    return ERTD_EINVAL;
-  gn_act_bwd_kernel<<<dim3(groups, B), 256, 0, (hipStream_t)stream>>>(
-      x, Ca, x2, Cb, HW, groups, gamma, beta, (const float2*)mr, act, dy, dx, dx2, accumulate,
-      dgb_part);
-  return rcode(hipGetLastError());
+  return gn_act_backward(x, Ca, x2, Cb, B, HW, groups, gamma, beta, mr, act, dy, dx, dx2, accumulate,
+                         dgb_part, nullptr, 0, stream);
+}
+
+int ertd_gn_act_backward_csum(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                              const float* gamma, const float* beta, const float* mr, int act,
+                              const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
+                              float* csum, long long ldc, void* stream) {
+  if (!csum) return ERTD_EINVAL;
+  return gn_act_backward(x, Ca, x2, Cb, B, HW, groups, gamma, beta, mr, act, dy, dx, dx2, accumulate,
+                         dgb_part, csum, ldc, stream);
 }
 
 int ertd_im2col(const float* x, int C, int B, int H, int ks, int mode, float* out, void* stream) {

@@ -414,4 +414,21 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
   return e == hipSuccess ? ERTD_OK : (int)e;
 }
 
+int ertd_conv_wgrad_bias(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
+                         int Cout, int ks, int mode, const float* gn, int act, float* dw, int accumulate,
+                         float* db, float* db2, void* ws, size_t ws_bytes, void* stream) {
+  if (!dy || !x || !dw || !db || !ws || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) || act < ACT_NONE ||
+      act > ACT_GN || (act != ACT_NONE && (!gn || mode != MODE_S1)))
+    return ERTD_EINVAL;
+  if (!wgrad_wino_bias_ok(Ca + Cb, Cout, B, H, ks, mode)) return ERTD_EINVAL;
+  if (ertd_conv_wgrad_ws_bytes(Ca + Cb, Cout, B, H, ks, mode) > ws_bytes) return ERTD_ENOSPC;
+  const hipError_t e = launch_wgrad_wino(dy, x, Ca, x2, Cb, B, H, Cout, mode, gn, act, dw, accumulate,
+                                         (float*)ws, (hipStream_t)stream, db, db2);
+  return e == hipSuccess ? ERTD_OK : (int)e;
+}
+
+int ertd_conv_wgrad_bias_ok(int Cin, int Cout, int B, int H, int ks, int mode) {
+  return wgrad_wino_bias_ok(Cin, Cout, B, H, ks, mode) ? 1 : 0;
+}
+
 }  // extern "C"

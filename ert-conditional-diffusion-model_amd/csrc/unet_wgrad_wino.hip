@@ -70,6 +70,7 @@ struct WgwArgs {
   float* D;             // [36][Cout][T]
   float* P;             // [nks][36][Cout][Cin]
   int T, nks, kr;       // tiles (K), K ranges, K per range (multiple of 16)
+  float* BP;            // [Cout][T / 256] bias-gradient partials (sums of dy), or null
 };
 // (H = the conv's output size; the Upsample convs read x at H / 2, nearest)
 
@@ -159,11 +160,13 @@ __global__ __launch_bounds__(256) void wgw_d_kernel(WgwArgs a) {
   const int b = t / ts, tt = t - b * ts, ty = tt / tpr, tx = tt - ty * tpr;
   const float* src = a.dy + ((size_t)b * a.Cout + co) * a.H * a.H + (4 * ty) * a.H + 4 * tx;
   float m[4][6];   // A applied along each row of the 4x4 tile
+  float tsum = 0.f;  // the tile's sum of dy (the fused bias gradient)
 #pragma unroll
   for (int y = 0; y < 4; ++y) {
     const float4 q = *reinterpret_cast<const float4*>(src + y * a.H);
     const float v[4] = {q.x, q.y, q.z, q.w};
     a4(v, m[y]);
+    tsum += (q.x + q.y) + (q.z + q.w);
   }
   const size_t xs = (size_t)a.T * a.Cout;
   float* out = a.D + (size_t)co * a.T + t;
@@ -174,6 +177,18 @@ __global__ __launch_bounds__(256) void wgw_d_kernel(WgwArgs a) {
     a4(v, o);
 #pragma unroll
     for (int y = 0; y < 6; ++y) out[(size_t)(6 * y + x) * xs] = o[y];
+  }
+  if (a.BP) {
+    // the conv's bias gradient rides along: the tile sums of the workgroup's
+    // 256 tiles (T % 256 == 0: one output channel per workgroup, no early
+    // return) in a fixed order
+    float s = tsum;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) a.BP[(size_t)co * (a.T / 256) + t / 256] = (red[0] + red[1]) + (red[2] + red[3]);
   }
 }
 
@@ -356,16 +371,34 @@ __global__ __launch_bounds__(256) void wgw_sum_kernel(WgwArgs a) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   float s = a.P[i];
-  for (int k = 1; k < a.nks; ++k) s += a.P[(size_t)k * n + i];
+  // batches of 8 independent loads, then the adds in k order (a serial
+  // load-add chain was latency-bound: 15.7 us for 15 partials of 147 K floats)
+  for (int k = 1; k < a.nks; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = k + u < a.nks ? a.P[(size_t)(k + u) * n + i] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k + u < a.nks) s += v[u];
+  }
   a.P[i] = s;
 }
 
 // dW[co][ci] = G^T dU G in float64 (one thread per (co, ci))
-__global__ __launch_bounds__(256) void wgw_final_kernel(WgwArgs a, float* dw, int accumulate) {
+__global__ __launch_bounds__(256) void wgw_final_kernel(WgwArgs a, float* dw, int accumulate, float* db,
+                                                        float* db2) {
   const int Cin = a.Ca + a.Cb;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t cc = (size_t)a.Cout * Cin;
   if (i >= cc) return;
+  if (db && i % Cin == 0) {   // bias gradient of channel co: its T / 256 partials in order
+    const size_t co = i / Cin;
+    const int nb = a.T / 256;
+    double s = 0.0;
+    for (int k = 0; k < nb; ++k) s += (double)a.BP[co * nb + k];
+    db[co] = (float)s;
+    if (db2) db2[co] = (float)s;
+  }
   double u[NX];
 #pragma unroll
   for (int x = 0; x < NX; ++x) u[x] = (double)a.P[(size_t)x * cc + i];
@@ -398,6 +431,7 @@ struct WgwPlan {
   int T, nks, kr;
   int mb, nb;       // LDS path: workgroup tile (64 mb co) x (64 nb ci)
   size_t v, d, p;   // floats
+  size_t bp;        // bias-gradient partials (0: T % 256 != 0, no fused bias gradient)
 };
 
 bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
@@ -431,6 +465,7 @@ bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
   pl->v = (size_t)NX * T * Cin;
   pl->d = (size_t)NX * T * Cout;
   pl->p = (size_t)nks * NX * Cout * Cin;
+  pl->bp = T % 256 == 0 ? (size_t)Cout * (T / 256) : 0;
   return true;
 }
 
@@ -442,20 +477,27 @@ size_t wgrad_wino_ws_floats(int Cin, int Cout, int B, int H, int ks, int mode) {
   if (!wgw_env() || ks != 3 || (mode != MODE_S1 && mode != MODE_UP)) return 0;
   if (mode == MODE_UP && wgw_env() == 2) return 0;   // ERTD_WGRAD_WINO=2: stride-1 only (A/B)
   if (!wgw_plan(Cin, Cout, B, mode == MODE_UP ? 2 * H : H, &pl)) return 0;
-  return pl.v + pl.d + pl.p;
+  return pl.v + pl.d + pl.p + pl.bp;
+}
+
+bool wgrad_wino_bias_ok(int Cin, int Cout, int B, int H, int ks, int mode) {
+  WgwPlan pl;
+  return wgrad_wino_ws_floats(Cin, Cout, B, H, ks, mode) > 0 &&
+         wgw_plan(Cin, Cout, B, mode == MODE_UP ? 2 * H : H, &pl) && pl.bp > 0;
 }
 
 hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B,
                              int H, int Cout, int mode, const float* gn, int act, float* dw,
-                             int accumulate, float* ws, hipStream_t s) {
+                             int accumulate, float* ws, hipStream_t s, float* db, float* db2) {
   const bool up = mode == MODE_UP;
   if ((mode != MODE_S1 && !up) || (up && act != ACT_NONE)) return hipErrorInvalidValue;
   const int Ho = up ? 2 * H : H;
   WgwPlan pl;
   if (!wgw_plan(Ca + Cb, Cout, B, Ho, &pl)) return hipErrorInvalidValue;
+  if ((db || db2) && (!db || !pl.bp)) return hipErrorInvalidValue;
   const int Cin = Ca + Cb;
   WgwArgs a{dy, x, x2, Ca, Cb, Cout, Ho, B, (const float2*)gn, ws, ws + pl.v, ws + pl.v + pl.d,
-            pl.T, pl.nks, pl.kr};
+            pl.T, pl.nks, pl.kr, db ? ws + pl.v + pl.d + pl.p : nullptr};
   const size_t nv = (size_t)pl.T * Cin, nd = (size_t)pl.T * Cout;
   const unsigned gv = (unsigned)((nv + 255) / 256);
   if (up) wgw_v_kernel<ACT_NONE, true><<<gv, 256, 0, s>>>(a);
@@ -482,7 +524,7 @@ hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const floa
     wgw_sum_kernel<<<(unsigned)((nw * NX + 255) / 256), 256, 0, s>>>(a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  wgw_final_kernel<<<(unsigned)((nw + 255) / 256), 256, 0, s>>>(a, dw, accumulate);
+  wgw_final_kernel<<<(unsigned)((nw + 255) / 256), 256, 0, s>>>(a, dw, accumulate, db, db2);
   return hipGetLastError();
 }
 

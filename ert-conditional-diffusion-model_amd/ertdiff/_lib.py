@@ -114,6 +114,8 @@ SIGNATURES = {
     "ertd_gn_act_apply": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _I, _VP, _VP]),
     "ertd_gn_act_backward": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _I, _VP, _VP, _VP,
                                   _I, _VP, _VP]),
+    "ertd_gn_act_backward_csum": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _I, _VP, _VP, _VP,
+                                       _I, _VP, _VP, ctypes.c_longlong, _VP]),
     "ertd_im2col": (_I, [_VP, _I, _I, _I, _I, _I, _VP, _VP]),
     "ertd_wgrad_ws_bytes": (_SZ, [_I, _I, _I, _I]),
     "ertd_wgrad_gemm": (_I, [_VP, _VP, _I, _I, _I, _I, _LL, _LL, _VP, _I, _VP, _SZ, _VP]),
@@ -147,6 +149,9 @@ SIGNATURES = {
     "ertd_conv_pack_batch": (_I, [_VP, _I, _I, _VP]),
     "ertd_conv_wgrad": (_I, [_VP, _VP, _I, _VP, _I, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _VP,
                              ctypes.c_size_t, _VP]),
+    "ertd_conv_wgrad_bias_ok": (_I, [_I, _I, _I, _I, _I, _I]),
+    "ertd_conv_wgrad_bias": (_I, [_VP, _VP, _I, _VP, _I, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP,
+                                  _VP, ctypes.c_size_t, _VP]),
     "ertd_encoder_train_ws_bytes": (_SZ, [_I, _I]),
     "ertd_encoder_train_fwd": (_I, [_VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _SZ, _VP]),
     "ertd_encoder_train_bwd": (_I, [_VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),

@@ -208,16 +208,28 @@ class _K:
                                               act, out.data_ptr(), self.s), "gn_act_apply")
         return out
 
-    def gn_backward(self, xa, xb, groups, gamma, beta, mr, act, dy, dxa, dxb, accumulate):
-        """dxa / dxb (+)= d act(GroupNorm(cat(xa, xb))); returns (dgamma, dbeta)."""
+    def gn_backward(self, xa, xb, groups, gamma, beta, mr, act, dy, dxa, dxb, accumulate,
+                    csum=None):
+        """dxa / dxb (+)= d act(GroupNorm(cat(xa, xb))); returns (dgamma, dbeta).
+        csum: an optional (B, C) row-strided view that receives the per-sample
+        pixel sums of the gradient added (fused; the ResBlock emb gradient)."""
         B, Ca, H, W = xa.shape
         Cb = 0 if xb is None else xb.shape[1]
         C = Ca + Cb
         part = self.empty(B, 2, C)
-        _lib.check(self.lib.ertd_gn_act_backward(
-            xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups, gamma.data_ptr(), beta.data_ptr(),
-            mr.data_ptr(), act, dy.data_ptr(), dxa.data_ptr(), _p(dxb), int(accumulate),
-            part.data_ptr(), self.s), "gn_act_backward")
+        if csum is not None and C // groups <= 64:
+            assert csum.shape == (B, C) and csum.stride(1) == 1
+            _lib.check(self.lib.ertd_gn_act_backward_csum(
+                xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups, gamma.data_ptr(), beta.data_ptr(),
+                mr.data_ptr(), act, dy.data_ptr(), dxa.data_ptr(), _p(dxb), int(accumulate),
+                part.data_ptr(), csum.data_ptr(), csum.stride(0), self.s), "gn_act_backward_csum")
+        else:
+            _lib.check(self.lib.ertd_gn_act_backward(
+                xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups, gamma.data_ptr(), beta.data_ptr(),
+                mr.data_ptr(), act, dy.data_ptr(), dxa.data_ptr(), _p(dxb), int(accumulate),
+                part.data_ptr(), self.s), "gn_act_backward")
+            if csum is not None:
+                self.chan_sums(dxa, out_bc=csum)
         dgb = self.empty(2, C)
         if self.deferred is None:
             self.reduce_rows(part, B, 2 * C, dgb)
@@ -243,20 +255,27 @@ class _K:
         self.deferred = []
 
     # ---- conv gradients
-    def conv_wgrad(self, dy, xa, xb, ks, mode, out, gn=None, act=0):
+    def conv_wgrad(self, dy, xa, xb, ks, mode, out, gn=None, act=0, db=None, db2=None):
         """out (Cout, Cin, ks, ks) = dL/dW of conv(act(cat(xa, xb))) (implicit GEMM; the
-        activation applied while staging)."""
+        activation applied while staging).  db / db2: the bias gradient (sum of dy)
+        fused into the Winograd path where it can be (returns whether it was)."""
         B, Ca, H, _ = xa.shape
         Cb = 0 if xb is None else xb.shape[1]
         Cout = dy.shape[1]
         n = self.lib.ertd_conv_wgrad_ws_bytes(Ca + Cb, Cout, B, H, ks, mode)
         if n == 0:
-            return False
+            return False, False
         ws = self.ws(n)
+        if db is not None and self.lib.ertd_conv_wgrad_bias_ok(Ca + Cb, Cout, B, H, ks, mode):
+            _lib.check(self.lib.ertd_conv_wgrad_bias(dy.data_ptr(), xa.data_ptr(), Ca, _p(xb), Cb, B, H,
+                                                     Cout, ks, mode, _p(gn), act, out.data_ptr(), 0,
+                                                     db.data_ptr(), _p(db2), ws.data_ptr(), ws.numel(),
+                                                     self.s), "conv_wgrad_bias")
+            return True, True
         _lib.check(self.lib.ertd_conv_wgrad(dy.data_ptr(), xa.data_ptr(), Ca, _p(xb), Cb, B, H, Cout,
                                             ks, mode, _p(gn), act, out.data_ptr(), 0, ws.data_ptr(),
                                             ws.numel(), self.s), "conv_wgrad")
-        return True
+        return True, False
 
     def wgrad_im2col(self, dy, xa, xb, ks, mode, out, gn=None, act=0):
         """Fallback outside the implicit-GEMM geometry: patch matrix + GEMM."""
@@ -445,19 +464,28 @@ class _Grads:
 
 
 def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, gn=None, act=0,
-                   bias_grad=True):
+                   bias_grad=True, also_bias=None):
     """Gradients of y = conv(act(cat(xa, xb))) + bias: weight and bias grads into
     grads[name.weight / .bias] (bias_grad=False: the caller supplies the bias
-    gradient); returns dL/d act(cat(xa, xb)) (or None)."""
+    gradient; also_bias: a second conv fed the same dy whose bias gradient is the
+    same sum, grads[also_bias] gets its own copy); returns dL/d act(cat(xa, xb))
+    (or None)."""
     Cout, Cin, ks, _ = w.shape
     dW = k.empty(Cout, Cin, ks, ks)
-    if not k.conv_wgrad(dy, xa, xb, ks, mode, dW, gn, act):
+    db = k.empty(Cout) if bias_grad else None
+    db2 = k.empty(Cout) if (bias_grad and also_bias) else None
+    ok, fused = k.conv_wgrad(dy, xa, xb, ks, mode, dW, gn, act, db=db, db2=db2)
+    if not ok:
         k.wgrad_im2col(dy, xa, xb, ks, mode, dW, gn, act)
     grads[name + ".weight"] = dW
     if bias_grad:
-        db = k.empty(Cout)
-        k.chan_sums(dy, out_c=db)
+        if not fused:
+            k.chan_sums(dy, out_c=db)
+            if db2 is not None:
+                db2.copy_(db)
         grads[name + ".bias"] = db
+        if db2 is not None:
+            grads[also_bias] = db2
     if not x_needs_grad:
         return None
     # input gradient: a conv of dY with the flipped, transposed weights
@@ -668,22 +696,25 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
             elif kind == "res":
                 xa, xb = d["xa"], d["xb"]
                 # y = conv2(a2) + b2 + skip(cat(xa, xb))
+                # conv2's fused bias gradient (sum of dy) is also the skip's
+                da2 = _conv_backward(k, grads, n + ".conv2", W[n + ".conv2.weight"], d["h"], None,
+                                     dy, MODE_S1, gn=d["ss2"], act=ACT_GN_SILU,
+                                     also_bias=n + ".skip.bias" if d["skip"] else None)
                 if d["skip"]:
                     dxs = _conv_backward(k, grads, n + ".skip", W[n + ".skip.weight"], xa, xb, dy,
-                                         MODE_S1)
+                                         MODE_S1, bias_grad=False)
                     G.add_cat(dxs, xa, xb)
                 else:
                     G.add(xa, dy)
-                da2 = _conv_backward(k, grads, n + ".conv2", W[n + ".conv2.weight"], d["h"], None,
-                                     dy, MODE_S1, gn=d["ss2"], act=ACT_GN_SILU)
                 h = d["h"]
                 dh = k.empty(*h.shape)
-                dg, db = k.gn_backward(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"],
-                                       d["mr2"], ACT_GN_SILU, da2, dh, None, False)
-                grads[n + ".norm2.weight"], grads[n + ".norm2.bias"] = dg, db
-                # h = conv1(a1) + b1 + emb(ea): the emb grad is dh summed over pixels
+                # h = conv1(a1) + b1 + emb(ea): the emb grad is dh summed over pixels,
+                # taken by the GroupNorm backward that writes dh
                 cout = h.shape[1]
-                k.chan_sums(dh, out_bc=deb_all[:, eoff[n]:eoff[n] + cout])
+                dg, db = k.gn_backward(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"],
+                                       d["mr2"], ACT_GN_SILU, da2, dh, None, False,
+                                       csum=deb_all[:, eoff[n]:eoff[n] + cout])
+                grads[n + ".norm2.weight"], grads[n + ".norm2.bias"] = dg, db
                 # conv1's bias gradient sum_{b,p} dh equals the emb bias gradient
                 # sum_b deb[b] (the same per-sample sums, reduced by the same
                 # fixed-order kernel): taken from the emb backward below

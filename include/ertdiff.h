@@ -398,6 +398,9 @@ int ertd_unet_plan_destroy(ertd_unet_plan* plan);
  * ertd_gn_act_backward: dx / dx2 of act(GroupNorm(cat(x, x2))) given dy (B, C, HW);
  *   dgb_part (B, 2, C): per-sample sum dxn*xhat ([b][0]) and sum dxn ([b][1]) ->
  *   (dgamma | dbeta) by one ertd_reduce_rows (rows B, cols 2C).
+ * ertd_gn_act_backward_csum: the same, plus csum[b * ldc + c] = sum over the HW pixels
+ *   of the gradient this call adds to channel c of sample b (a ResBlock's emb-projection
+ *   gradient when dx is the conv1 output's gradient; channels per group <= 64).
  * ertd_im2col: out (B, C*ks*ks, Ho*Ho) patches of x (B, C, H, H), mode 0 s1 / 1 s2 / 2 upsample.
  * ertd_wgrad_gemm: dW (M, N) = sum_b dY_b (M, P) . X_b (N, P)^T (batch strides bsA, bsB),
  *   fp32 MFMA, split per sample + fixed-order reduction; ws >= ertd_wgrad_ws_bytes.
@@ -428,6 +431,10 @@ int ertd_gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B,
                          const float* gamma, const float* beta, const float* mr, int act,
                          const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
                          void* stream);
+int ertd_gn_act_backward_csum(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                              const float* gamma, const float* beta, const float* mr, int act,
+                              const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
+                              float* csum, long long ldc, void* stream);
 int ertd_im2col(const float* x, int C, int B, int H, int ks, int mode, float* out, void* stream);
 size_t ertd_wgrad_ws_bytes(int M, int N, int P, int B);
 int ertd_wgrad_gemm(const float* dY, const float* X, int M, int N, int P, int B, long long bsA,
@@ -483,6 +490,15 @@ int ertd_conv_input_grad_run(const float* dy, int B, int H, int Cout, int Cin, i
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
                     int Cout, int ks, int mode, const float* gn, int act, float* dw, int accumulate,
                     void* ws, size_t ws_bytes, void* stream);
+/* ertd_conv_wgrad_bias: ertd_conv_wgrad plus the conv's bias gradient db (Cout) = sum of dy
+ *   over samples and pixels (written, not accumulated; also into db2 when non-null, e.g.
+ *   a 1x1 skip conv fed the same dy), fused into the Winograd path's dy transform.  Only
+ *   where ertd_conv_wgrad_bias_ok (3x3 stride 1 / upsample on the Winograd path, B * tiles
+ *   a multiple of 256); ws as ertd_conv_wgrad_ws_bytes.                                  */
+int ertd_conv_wgrad_bias_ok(int Cin, int Cout, int B, int H, int ks, int mode);
+int ertd_conv_wgrad_bias(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
+                         int Cout, int ks, int mode, const float* gn, int act, float* dw, int accumulate,
+                         float* db, float* db2, void* ws, size_t ws_bytes, void* stream);
 
 /* Batched fp32 weight packing (the train step packs every conv once per
  * optimizer step, in one launch).  A descriptor names one packing: the source

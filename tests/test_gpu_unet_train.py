@@ -217,6 +217,45 @@ def test_conv_wgrad_vs_autograd(Ca, Cb, Cout, H, ks, mode, B, cuda_dev):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("Ca,Cb,Cout,H,mode,B", [
+    (64, 0, 64, 64, 0, 32),        # 64x64 ResBlock conv2 at the train batch
+    (128, 64, 128, 32, 0, 8),      # concat input
+    (128, 0, 128, 32, 2, 8),       # Upsample conv
+])
+def test_conv_wgrad_fused_bias(Ca, Cb, Cout, H, mode, B, cuda_dev):
+    """ertd_conv_wgrad_bias: the same dW bits as ertd_conv_wgrad, plus the bias
+    gradient sum(dy) (into two outputs) from the Winograd path's dy transform."""
+    from ertdiff import _lib
+    g = torch.Generator().manual_seed(Ca + 3 * Cout + H)
+    Cin = Ca + Cb
+    Ho = 2 * H if mode == 2 else H
+    x = torch.randn(B, Cin, H, H, generator=g)
+    dy = torch.randn(B, Cout, Ho, Ho, generator=g)
+    lib = _lib.lib()
+    assert lib.ertd_conv_wgrad_bias_ok(Cin, Cout, B, H, 3, mode) == 1
+    n = lib.ertd_conv_wgrad_ws_bytes(Cin, Cout, B, H, 3, mode)
+    ws = torch.empty(n, dtype=torch.uint8, device=cuda_dev)
+    xa = x[:, :Ca].contiguous().to(cuda_dev)
+    xb = x[:, Ca:].contiguous().to(cuda_dev) if Cb else None
+    dyd = dy.to(cuda_dev)
+    s = _lib.stream_of(cuda_dev)
+    dw0, dw1 = (torch.empty(Cout, Cin, 3, 3, device=cuda_dev) for _ in range(2))
+    db, db2 = torch.full((Cout,), 7.0, device=cuda_dev), torch.full((Cout,), 7.0, device=cuda_dev)
+    assert lib.ertd_conv_wgrad(dyd.data_ptr(), xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(),
+                               Cb, B, H, Cout, 3, mode, None, 0, dw0.data_ptr(), 0, ws.data_ptr(), n, s) == 0
+    assert lib.ertd_conv_wgrad_bias(dyd.data_ptr(), xa.data_ptr(), Ca,
+                                    None if xb is None else xb.data_ptr(), Cb, B, H, Cout, 3, mode, None,
+                                    0, dw1.data_ptr(), 0, db.data_ptr(), db2.data_ptr(), ws.data_ptr(), n,
+                                    s) == 0
+    assert torch.equal(dw0, dw1)
+    assert torch.equal(db, db2)
+    err = _rel(db, dy.double().sum((0, 2, 3)))
+    record_error(f"conv_wgrad_fused_bias_{Cin}_{Cout}_{H}_m{mode}", err)
+    assert err < 1e-5, err
+    # outside the fused geometry (B * tiles not a multiple of 256) the query says so
+    assert lib.ertd_conv_wgrad_bias_ok(64, 64, 1, 16, 3, 0) == 0
+
+
 @pytest.mark.parametrize("Ca,Cb,Cout,H,ks,act,B", [
     (64, 0, 64, 64, 3, 1, 2),      # conv1 / conv2 / conv_out: GroupNorm + SiLU staged
     (96, 32, 64, 32, 3, 1, 2),     # decoder conv1 on a concat
@@ -301,6 +340,8 @@ def test_unet_autograd_matches_fused_step(cuda_dev):
 
 @pytest.mark.parametrize("Ca,Cb,HW,groups,act,acc", [
     (64, 0, 4096, 32, 1, 0),
+    (128, 64, 4096, 32, 1, 1),     # concat input at 64x64, accumulate into dx
+    (256, 0, 256, 32, 1, 0),       # 16x16: one wave per channel, 4 channels at once
     (128, 64, 1024, 32, 1, 1),     # concat input, accumulate into dx
     (128, 0, 256, 1, 1, 0),        # one group of 128 channels (> 64 per LDS batch)
     (96, 32, 64, 2, 2, 1),         # GN without SiLU (attention norm)
@@ -346,6 +387,25 @@ def test_gn_act_backward_vs_autograd(Ca, Cb, HW, groups, act, acc, cuda_dev):
     e = [_rel(dx, want), _rel(dgb[0], gr.grad), _rel(dgb[1], br.grad)]
     record_error(f"gn_act_backward_{C}_{HW}_g{groups}_a{act}", max(e))
     assert max(e) < 1e-5, e
+    if C // groups <= 64:
+        # the fused per-sample pixel sums of the added gradient (into a column
+        # block of a wider matrix), and the same dx bits as the plain entry
+        dxa2 = prev[:, :Ca].contiguous().to(dev)
+        dxb2 = prev[:, Ca:].contiguous().to(dev) if Cb else None
+        wide = torch.full((B, C + 7), 5.0, device=dev)
+        part2 = torch.empty(B, 2, C, device=dev)
+        assert lib.ertd_gn_act_backward_csum(
+            xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(), Cb, B, HW, groups, gam.data_ptr(),
+            bet.data_ptr(), mr.data_ptr(), act, dyd.data_ptr(), dxa2.data_ptr(),
+            None if dxb2 is None else dxb2.data_ptr(), acc, part2.data_ptr(), wide[:, 3:].data_ptr(),
+            C + 7, s) == 0
+        assert torch.equal(dxa2, dxa) and torch.equal(part2, part)
+        if dxb2 is not None:
+            assert torch.equal(dxb2, dxb)
+        assert torch.all(wide[:, :3] == 5.0) and torch.all(wide[:, 3 + C:] == 5.0)
+        ec = _rel(wide[:, 3:3 + C], xr.grad.sum(2))
+        record_error(f"gn_act_backward_csum_{C}_{HW}_g{groups}", ec)
+        assert ec < 1e-4, ec    # fp32 sums of HW terms (the gradient tests' tolerance)
 
 
 @pytest.mark.gpu
