@@ -72,6 +72,12 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 #ifndef CHAIN_SPI
 #define CHAIN_SPI 2
 #endif
+// members per chain block: a member's step body is ~1.5 us of a ~15 us step,
+// so one block runs the steps of CHAIN_MPB members in turn and the slots the
+// other chain blocks would hold go to strip workers
+#ifndef CHAIN_MPB
+#define CHAIN_MPB 2
+#endif
 constexpr uint64_t SPIN_TIMEOUT_TICKS = 50000000ull;  // 0.5 s of s_memrealtime (100 MHz)
 
 // A zero the compiler cannot see through: loads addressed with it stay inside
@@ -202,7 +208,7 @@ __device__ unsigned long long g_item[4096][4];  // member 0 items: start, polled
 struct ChainStepSmem {
   float w[H];
   alignas(16) float h[H];
-  float x[PMAX];
+  float x[CHAIN_MPB][PMAX];
 };
 struct ChainSmem {
   union {
@@ -228,10 +234,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   const int P = w.param_dim, B = a.B, S = a.S, R = a.R;
   const size_t ring_part = (size_t)B * S * C2;  // floats per ring slot
 
-  if ((int)blockIdx.x < B) {
-    // ======================= chain block: member b =======================
-    const int b = blockIdx.x;
-    const uint32_t member = member_id(a.member_offset, b, a.ncond, a.id_period);
+  const int NCH = (B + CHAIN_MPB - 1) / CHAIN_MPB;   // chain blocks
+  if ((int)blockIdx.x < NCH) {
+    // ============ chain block: members b0 .. b0 + nm - 1, one step each in turn ============
+    const int b0 = blockIdx.x * CHAIN_MPB;
+    const int nm = B - b0 < CHAIN_MPB ? B - b0 : CHAIN_MPB;
     const int xj = tid >> 1, xc = tid & 1;                             // mlp.0 x-part
     const int eo = tid >> 3, ehf = (tid >> 2) & 1, ei = tid & 3;       // mlp.2 chains
     const bool updater = ehf == 0 && ei == 0 && eo < P;
@@ -241,114 +248,127 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     const float4* wx_src = reinterpret_cast<const float4*>(packed + PACK_W0XR + xj * W0XR_PITCH + 16 * xc);
     const float4* w2_src = reinterpret_cast<const float4*>(packed + PACK_W2L + (2 * eo + ehf) * W2L_PITCH + 16 * ei);
     const float bo = eo < P ? w.mlp2_b[eo] : 0.f;
-    float xv = updater ? a.x[(size_t)b * P + eo] : 0.f;
+    float xv[CHAIN_MPB];
+#pragma unroll
+    for (int m = 0; m < CHAIN_MPB; ++m) {
+      xv[m] = updater && m < nm ? a.x[(size_t)(b0 + m) * P + eo] : 0.f;
+      if (tid < P && m < nm) sm.step.x[m][tid] = a.x[(size_t)(b0 + m) * P + tid];
+    }
     unsigned vseen = 0;  // lane 0: time rows known to be published
-    if (tid < P) sm.step.x[tid] = a.x[(size_t)b * P + tid];
     __syncthreads();
     for (int i = 0; i < a.n_run; ++i) {
       const int t = a.t_first - i;
       const int slot = i % R;
-      // inputs that do not depend on this step's u (noise first: its Philox
-      // and Box-Muller temporaries are dead before the x-part operands load)
-      float z = 0.f, c1 = 0.f, c2 = 0.f, sig = 0.f;
+      float c1 = 0.f, c2 = 0.f, sig = 0.f;
       if (updater) {
-        z = step_noise(a.noise, a.num_steps, t, B, b, P, eo, a.seed, member);
         c1 = a.c1[t];
         c2 = a.c2[t];
         sig = a.sigma[t];
       }
-      float wx[16];
-      {
-        const float4* src = wx_src + opaque0();
+#pragma unroll
+      for (int m = 0; m < CHAIN_MPB; ++m) {
+        if (m >= nm) break;
+        const int b = b0 + m;
+        // inputs that do not depend on this step's u (noise first: its Philox
+        // and Box-Muller temporaries are dead before the x-part operands load)
+        const float z = updater ? step_noise(a.noise, a.num_steps, t, B, b, P, eo, a.seed,
+                                             member_id(a.member_offset, b, a.ncond, a.id_period))
+                                : 0.f;
+        float wx[16];
+        {
+          const float4* src = wx_src + opaque0();
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 v4 = src[q4];
+            wx[4 * q4] = v4.x;
+            wx[4 * q4 + 1] = v4.y;
+            wx[4 * q4 + 2] = v4.z;
+            wx[4 * q4 + 3] = v4.w;
+          }
+        }
+        float xs[16];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) xs[kk] = (16 * xc + kk < P) ? sm.step.x[m][16 * xc + kk] : 0.f;
+        float bsum = 0.f;  // second x-part chain (k >= 16), from zero
+        if (xc == 1) {
+#pragma unroll
+          for (int kk = 0; kk < 16; ++kk)
+            if (16 + kk < P) bsum = fmaf(wx[kk], xs[kk], bsum);
+        }
+        // this step's condition row and time row: lane 0 polls the two flags
+        CST(0);
+        if (tid == 0) {
+          bool ok = true;
+          if (vseen < (unsigned)(i + 1)) ok = wait_ge(a.vready, (unsigned)(i + 1), a.status, 1u, vseen, 1);
+          unsigned useen = 0;
+          if (ok) ok = wait_ge(a.uflag + ((size_t)slot * B + b) * SYNC_PAD, (unsigned)(i + 1), a.status, 1u, useen, 1);
+          sm.flag = ok ? 0 : 1;
+        }
+        __syncthreads();
+        if (sm.flag) return;  // aborted: every waiter gives up
+        if (tid < H) {
+          const float u = Sc1Load()(a.uring + ((size_t)slot * B + b) * H + tid);
+          const float v = Sc1Load()(a.V + (size_t)i * H + tid);
+          sm.step.w[tid] = u + v;
+        }
+        __syncthreads();
+        CST(1);
+        if (tid == 0) st_relaxed(a.progress + (size_t)b * SYNC_PAD, (unsigned)(i + 1));  // slot i%R consumed
+        // mlp.0: h_j = relu((w_j + W0x[j][0:16].x) + W0x[j][16:P].x)
+        float av = bsum;
+        if (xc == 0) {
+          av = sm.step.w[xj];
+#pragma unroll
+          for (int kk = 0; kk < 16; ++kk)
+            if (kk < P) av = fmaf(wx[kk], xs[kk], av);
+        }
+        const float other = __shfl_xor(av, 1);
+        if (xc == 0) sm.step.h[xj] = fmaxf(av + other, 0.f);
+        float w2[16];
+        {
+          const float4* src = w2_src + opaque0();
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 v4 = src[q4];
+            w2[4 * q4] = v4.x;
+            w2[4 * q4 + 1] = v4.y;
+            w2[4 * q4 + 2] = v4.z;
+            w2[4 * q4 + 3] = v4.w;
+          }
+        }
+        __syncthreads();
+        // mlp.2: four 16-term chains per k-half, joined (c0+c1)+(c2+c3), halves added
+        const float4* h4 = reinterpret_cast<const float4*>(sm.step.h + 64 * ehf + 16 * ei);
+        float hv[16];
 #pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
-          const float4 v4 = src[q4];
-          wx[4 * q4] = v4.x;
-          wx[4 * q4 + 1] = v4.y;
-          wx[4 * q4 + 2] = v4.z;
-          wx[4 * q4 + 3] = v4.w;
+          const float4 v4 = h4[q4];
+          hv[4 * q4] = v4.x;
+          hv[4 * q4 + 1] = v4.y;
+          hv[4 * q4 + 2] = v4.z;
+          hv[4 * q4 + 3] = v4.w;
         }
-      }
-      float xs[16];
+        float c = 0.f;
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) xs[kk] = (16 * xc + kk < P) ? sm.step.x[16 * xc + kk] : 0.f;
-      float bsum = 0.f;  // second x-part chain (k >= 16), from zero
-      if (xc == 1) {
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk)
-          if (16 + kk < P) bsum = fmaf(wx[kk], xs[kk], bsum);
-      }
-      // this step's condition row and time row: lane 0 polls the two flags
-      CST(0);
-      if (tid == 0) {
-        bool ok = true;
-        if (vseen < (unsigned)(i + 1)) ok = wait_ge(a.vready, (unsigned)(i + 1), a.status, 1u, vseen, 1);
-        unsigned useen = 0;
-        if (ok) ok = wait_ge(a.uflag + ((size_t)slot * B + b) * SYNC_PAD, (unsigned)(i + 1), a.status, 1u, useen, 1);
-        sm.flag = ok ? 0 : 1;
-      }
-      __syncthreads();
-      if (sm.flag) return;  // aborted: every waiter gives up
-      if (tid < H) {
-        const float u = Sc1Load()(a.uring + ((size_t)slot * B + b) * H + tid);
-        const float v = Sc1Load()(a.V + (size_t)i * H + tid);
-        sm.step.w[tid] = u + v;
-      }
-      __syncthreads();
-      CST(1);
-      if (tid == 0) st_relaxed(a.progress + (size_t)b * SYNC_PAD, (unsigned)(i + 1));  // slot i%R consumed
-      // mlp.0: h_j = relu((w_j + W0x[j][0:16].x) + W0x[j][16:P].x)
-      float av = bsum;
-      if (xc == 0) {
-        av = sm.step.w[xj];
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk)
-          if (kk < P) av = fmaf(wx[kk], xs[kk], av);
-      }
-      const float other = __shfl_xor(av, 1);
-      if (xc == 0) sm.step.h[xj] = fmaxf(av + other, 0.f);
-      float w2[16];
-      {
-        const float4* src = w2_src + opaque0();
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const float4 v4 = src[q4];
-          w2[4 * q4] = v4.x;
-          w2[4 * q4 + 1] = v4.y;
-          w2[4 * q4 + 2] = v4.z;
-          w2[4 * q4 + 3] = v4.w;
+        for (int kk = 0; kk < 16; ++kk) c = fmaf(w2[kk], hv[kk], c);
+        const float s1 = c + __shfl_xor(c, 1);
+        const float s2 = s1 + __shfl_xor(s1, 2);
+        const float e = s2 + __shfl_xor(s2, 4);
+        if (updater) {
+          xv[m] = ddpm_update(xv[m], e + bo, c1, c2, sig, z, t > 0);
+          sm.step.x[m][eo] = xv[m];
         }
+        __syncthreads();
+        CST(2);
       }
-      __syncthreads();
-      // mlp.2: four 16-term chains per k-half, joined (c0+c1)+(c2+c3), halves added
-      const float4* h4 = reinterpret_cast<const float4*>(sm.step.h + 64 * ehf + 16 * ei);
-      float hv[16];
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const float4 v4 = h4[q4];
-        hv[4 * q4] = v4.x;
-        hv[4 * q4 + 1] = v4.y;
-        hv[4 * q4 + 2] = v4.z;
-        hv[4 * q4 + 3] = v4.w;
-      }
-      float c = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) c = fmaf(w2[kk], hv[kk], c);
-      const float s1 = c + __shfl_xor(c, 1);
-      const float s2 = s1 + __shfl_xor(s1, 2);
-      const float e = s2 + __shfl_xor(s2, 4);
-      if (updater) {
-        xv = ddpm_update(xv, e + bo, c1, c2, sig, z, t > 0);
-        sm.step.x[eo] = xv;
-      }
-      __syncthreads();
-      CST(2);
     }
-    if (updater) a.x[(size_t)b * P + eo] = xv;
+#pragma unroll
+    for (int m = 0; m < CHAIN_MPB; ++m)
+      if (updater && m < nm) a.x[(size_t)(b0 + m) * P + eo] = xv[m];
     return;
   }
 
-  if ((int)blockIdx.x == B) {
+  if ((int)blockIdx.x == NCH) {
     // ======================= time-row block =======================
     for (int i = 0; i < a.n_run; ++i) {
       float* f = sm.trow;
@@ -369,7 +389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   }
   unsigned seen_reg = 0;  // lane 0's copy
   __syncthreads();
-  const int wid = blockIdx.x - B - 1;
+  const int wid = blockIdx.x - NCH - 1;
   const int b = wid % B;
   const int NPS = (S + CHAIN_SPI - 1) / CHAIN_SPI;   // work items per step
   const unsigned n_items = (unsigned)a.n_run * (unsigned)NPS;
@@ -510,10 +530,11 @@ int faithful_chain_grid(int B, int S) {
     const int use = per_cu < CHAIN_MAX_BPC ? per_cu : CHAIN_MAX_BPC;
     cached[dev] = use > 0 ? use * cus : -1;
   }
-  // B chains + the time-row block + workers; every block must be resident.
-  // At most 2S workers per member: more only poll (and slow the chip).
-  const long long want = (long long)B + 1 + (long long)B * 2 * S;
-  if (cached[dev] < 2 * B + 1) return 0;
+  // the chain blocks + the time-row block + workers; every block must be
+  // resident.  At most 2S workers per member: more only poll (and slow the chip).
+  const int nch = (B + CHAIN_MPB - 1) / CHAIN_MPB;
+  const long long want = (long long)nch + 1 + (long long)B * 2 * S;
+  if (cached[dev] < nch + 1 + B) return 0;
   return (int)(want < cached[dev] ? want : cached[dev]);
 }
 

@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
   fa.claim = fa.progress + B * SYNC_PAD; fa.vready = fa.claim + B * SYNC_PAD; fa.status = fa.vready + SYNC_PAD;
   fa.uring = uring; fa.V = Vc;
   const int grid = faithful_chain_grid(B, S);
-  printf("B=%d T=%d S=%d R=%d grid=%d (workers %d)\n", B, T, S, R, grid, grid - B - 1);
+  printf("B=%d T=%d S=%d R=%d grid=%d (workers %d)\n", B, T, S, R, grid, grid - (B + CHAIN_MPB - 1) / CHAIN_MPB - 1);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   for (int rep = 0; rep < 3; ++rep) {
     CK(launch_zero_words((unsigned*)zero, zb / 4, 0));
@@ -85,7 +85,7 @@ int main(int argc, char** argv) {
     printf("  %5d %4d %2d | %9.1f %9.1f %9.1f %9.1f | %9.1f %9.1f %9.1f\n", k, i, (k % NPS) * CHAIN_SPI, rl(it[k][0]), rl(it[k][1]), rl(it[k][2]), rl(it[k][3]),
            rl(cst[0][i][0]), rl(cst[0][i][1]), rl(cst[0][i][2]));
   }
-  double tot[8] = {}; int nw = grid - B - 1;
+  double tot[8] = {}; int nw = grid - (B + CHAIN_MPB - 1) / CHAIN_MPB - 1;
   for (int k = 0; k < nw && k < 2048; ++k) for (int j = 0; j < 8; ++j) tot[j] += wacc[k][j];
   const double items = tot[5];
   printf("workers: items %.0f (%.1f/worker), last-arrivals %.0f, progress polls %.0f\n", items, items / nw, tot[6], tot[0]);
