@@ -371,15 +371,15 @@ __global__ __launch_bounds__(256) void wgw_sum_kernel(WgwArgs a) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   float s = a.P[i];
-  // batches of 16 independent loads (one memory round trip for the usual
-  // nks <= 17), then the adds in k order (a serial load-add chain was
-  // latency-bound: 15.7 us for 15 partials of 147 K floats)
-  for (int k = 1; k < a.nks; k += 16) {
-    float v[16];
+  // batches of 8 independent loads, then the adds in k order (a serial
+  // load-add chain was latency-bound: 11.0 us average per train-step launch;
+  // batches of 8: 8.3 us; of 16: 11.7 us)
+  for (int k = 1; k < a.nks; k += 8) {
+    float v[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = k + u < a.nks ? a.P[(size_t)(k + u) * n + i] : 0.f;
+    for (int u = 0; u < 8; ++u) v[u] = k + u < a.nks ? a.P[(size_t)(k + u) * n + i] : 0.f;
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
+    for (int u = 0; u < 8; ++u)
       if (k + u < a.nks) s += v[u];
   }
   a.P[i] = s;
