@@ -10,7 +10,7 @@ bash tools/layer_trace.sh > gpurun_out/lt_U2.txt 2>&1; echo "[trace] rc=$?"
 rm -rf gpurun_out/bprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/bprof -o run \
   -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-u3 --no-u5 --no-ensemble --no-hbm-kernels \
-  --no-kde --no-reference --no-unet-train > gpurun_out/bprof.log 2>&1
+  --no-kde --no-reference --no-unet-train --no-evaluation > gpurun_out/bprof.log 2>&1
 echo "[bench prof] rc=$?"
 bash tools/gpu_train_prof.sh
 [ "${PMC:-0}" = 1 ] && { CFG=U2 B=64 PREC=fp32 bash tools/unet_traffic.sh; echo "[u2 pmc] rc=$?"; }
