@@ -386,8 +386,11 @@ __global__ __launch_bounds__(256) void wgw_sum_kernel(WgwArgs a) {
 }
 
 // dW[co][ci] = G^T dU G in float64 (one thread per (co, ci))
+#ifndef WGW_FUSED_SUM
+#define WGW_FUSED_SUM 4  // K ranges at most this many: summed by wgw_final_kernel (0: never)
+#endif
 __global__ __launch_bounds__(256) void wgw_final_kernel(WgwArgs a, float* dw, int accumulate, float* db,
-                                                        float* db2) {
+                                                        float* db2, int nsum) {
   const int Cin = a.Ca + a.Cb;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t cc = (size_t)a.Cout * Cin;
@@ -400,9 +403,26 @@ __global__ __launch_bounds__(256) void wgw_final_kernel(WgwArgs a, float* dw, in
     db[co] = (float)s;
     if (db2) db2[co] = (float)s;
   }
+  // nsum > 1: the K-range partials are added here (the same k-ordered float
+  // sum as wgw_sum_kernel, so the same bits) -- for small nks, saving a launch
   double u[NX];
+  if (nsum > 1) {
+    const size_t ks_stride = (size_t)NX * cc;
 #pragma unroll
-  for (int x = 0; x < NX; ++x) u[x] = (double)a.P[(size_t)x * cc + i];
+    for (int x = 0; x < NX; ++x) {
+      float v[WGW_FUSED_SUM > 0 ? WGW_FUSED_SUM : 1];
+#pragma unroll
+      for (int k = 0; k < WGW_FUSED_SUM; ++k) v[k] = k < nsum ? a.P[(size_t)k * ks_stride + (size_t)x * cc + i] : 0.f;
+      float s = v[0];
+#pragma unroll
+      for (int k = 1; k < WGW_FUSED_SUM; ++k)
+        if (k < nsum) s += v[k];
+      u[x] = (double)s;
+    }
+  } else {
+#pragma unroll
+    for (int x = 0; x < NX; ++x) u[x] = (double)a.P[(size_t)x * cc + i];
+  }
   float* o = dw + i * 9;
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
@@ -521,11 +541,13 @@ hipError_t launch_wgrad_wino(const float* dy, const float* x, int Ca, const floa
 #endif
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const size_t nw = (size_t)Cout * Cin;
-  if (pl.nks > 1) {
+  const bool fuse = pl.nks > 1 && pl.nks <= WGW_FUSED_SUM;
+  if (pl.nks > 1 && !fuse) {
     wgw_sum_kernel<<<(unsigned)((nw * NX + 255) / 256), 256, 0, s>>>(a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  wgw_final_kernel<<<(unsigned)((nw + 255) / 256), 256, 0, s>>>(a, dw, accumulate, db, db2);
+  wgw_final_kernel<<<(unsigned)((nw + 255) / 256), 256, 0, s>>>(a, dw, accumulate, db, db2,
+                                                                  fuse ? pl.nks : 1);
   return hipGetLastError();
 }
 
