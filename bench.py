@@ -1032,8 +1032,9 @@ def main():
         dom = ck["d0r0.conv1 64->64 @64x64, GN+SiLU, +emb"]
         roof["dominant"] = {"kernel": "conv_wino4s_kernel (Winograd F(4x4,3x3), register-resident weights: "
                                       "36 of the 51 convs -- every ResBlock 3x3 and both Upsample convs -- "
-                                      "3.4 of 4.2 ms of serialized conv time per step, "
-                                      "profiles/r03_unet_layers.txt)",
+                                      "3.36 of 4.08 ms of serialized conv time per step and 46.6-46.9 % of "
+                                      "the fp32 peak over those 36 launches, profiles/r04_unet_layers.txt; "
+                                      "this layer is its weakest shape)",
                             "layer": "d0r0.conv1 64->64 @64x64, B=64, GN+SiLU prologue, +emb epilogue",
                             "achieved": dom["executed_tflops"], "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                             "frac": dom["mfma_frac"], "avg_us": dom["avg_us"],
