@@ -551,25 +551,57 @@ struct AdamMulti {
   const float* g[ADAM_T];
   float* m[ADAM_T];
   float* v[ADAM_T];
-  long long off[ADAM_T + 1];
+  long long n[ADAM_T];   // elements of tensor k
+  int boff[ADAM_T + 1];  // first workgroup of tensor k (each tensor starts a workgroup)
   int nt;
   float one_minus_b1, b2, one_minus_b2, step_size_neg, bc2_sqrt, eps;
 };
-__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.off[a.nt]) return;
-  int k = 0;
-  while (k + 1 < a.nt && i >= a.off[k + 1]) ++k;
-  const long long e = i - a.off[k];
-  const float g = a.g[k][e];
-  float m = a.m[k][e];
+// one element, torch.optim.Adam's op order (the same bits as before)
+__device__ __forceinline__ void adam_elem(const AdamMulti& a, float g, float& p, float& m, float& v) {
   m = m + a.one_minus_b1 * (g - m);                 // exp_avg.lerp_(grad, 1 - beta1)
-  float v = a.v[k][e] * a.b2;                       // exp_avg_sq.mul_(beta2)
+  v = v * a.b2;                                     // exp_avg_sq.mul_(beta2)
   v = v + a.one_minus_b2 * g * g;                   //   .addcmul_(grad, grad, 1 - beta2)
   const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
-  a.p[k][e] = a.p[k][e] + a.step_size_neg * (m / denom);
-  a.m[k][e] = m;
-  a.v[k][e] = v;
+  p = p + a.step_size_neg * (m / denom);
+}
+// A workgroup belongs to one tensor (found by a workgroup-uniform scan of
+// boff: the per-element search over the tensor list cost more than the
+// element's memory traffic) and a thread updates 4 consecutive elements with
+// float4 accesses where they are whole and 16-B aligned.
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
+  const int blk = blockIdx.x;
+  int k = 0;
+  while (k + 1 < a.nt && blk >= a.boff[k + 1]) ++k;
+  const long long e0 = ((long long)(blk - a.boff[k]) * 256 + threadIdx.x) * 4;
+  const long long n = a.n[k];
+  if (e0 >= n) return;
+  float* P = a.p[k];
+  const float* Gp = a.g[k];
+  float* M = a.m[k];
+  float* V = a.v[k];
+  const bool vec = e0 + 4 <= n && ((reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(Gp) |
+                                    reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(V)) & 15) == 0;
+  if (vec) {
+    const float4 g4 = *reinterpret_cast<const float4*>(Gp + e0);
+    float4 p4 = *reinterpret_cast<const float4*>(P + e0);
+    float4 m4 = *reinterpret_cast<const float4*>(M + e0);
+    float4 v4 = *reinterpret_cast<const float4*>(V + e0);
+    adam_elem(a, g4.x, p4.x, m4.x, v4.x);
+    adam_elem(a, g4.y, p4.y, m4.y, v4.y);
+    adam_elem(a, g4.z, p4.z, m4.z, v4.z);
+    adam_elem(a, g4.w, p4.w, m4.w, v4.w);
+    *reinterpret_cast<float4*>(P + e0) = p4;
+    *reinterpret_cast<float4*>(M + e0) = m4;
+    *reinterpret_cast<float4*>(V + e0) = v4;
+  } else {
+    for (long long e = e0; e < e0 + 4 && e < n; ++e) {
+      float p = P[e], m = M[e], v = V[e];
+      adam_elem(a, Gp[e], p, m, v);
+      P[e] = p;
+      M[e] = m;
+      V[e] = v;
+    }
+  }
 }
 
 // dst = cat(src[0], src[1], ...) over up to 64 contiguous tensors per launch
@@ -949,16 +981,19 @@ int ertd_adam_multi(float* const* params, const float* const* grads, float* cons
   for (int t0 = 0; t0 < ntensors; t0 += ADAM_T) {
     AdamMulti a{};
     a.nt = ntensors - t0 < ADAM_T ? ntensors - t0 : ADAM_T;
-    long long off = 0;
+    long long blocks = 0;
     for (int k = 0; k < a.nt; ++k) {
+      if (sizes[t0 + k] < 0) return ERTD_EINVAL;
       a.p[k] = params[t0 + k];
       a.g[k] = grads[t0 + k];
       a.m[k] = exp_avg[t0 + k];
       a.v[k] = exp_avg_sq[t0 + k];
-      a.off[k] = off;
-      off += sizes[t0 + k];
+      a.n[k] = sizes[t0 + k];
+      a.boff[k] = (int)blocks;
+      blocks += (sizes[t0 + k] + 1023) / 1024;   // 256 threads x 4 elements
     }
-    a.off[a.nt] = off;
+    a.boff[a.nt] = (int)blocks;
+    if (blocks == 0) continue;
     // scalars formed as torch does: Python floats (double), rounded when applied to fp32
     a.one_minus_b1 = (float)(1.0 - (double)beta1);
     a.b2 = beta2;
@@ -966,7 +1001,7 @@ int ertd_adam_multi(float* const* params, const float* const* grads, float* cons
     a.step_size_neg = (float)(-((double)lr / bc1));
     a.bc2_sqrt = (float)std::sqrt(bc2);
     a.eps = eps;
-    adam_multi_kernel<<<nblk((size_t)off), 256, 0, s>>>(a);
+    adam_multi_kernel<<<(unsigned)blocks, 256, 0, s>>>(a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
   }
