@@ -271,6 +271,10 @@ __global__ __launch_bounds__(256) void wgrad_conv_kernel(WgArgs a) {
     }
 }
 
+#ifndef WG_REDUCE4
+#define WG_REDUCE4 1  // 1: K-range partial sums on wgrad_reduce4_kernel where cols % 4 == 0 (A/B)
+#endif
+
 // dW[j] (+)= sum over ranges of part[r][j] (as reduce_rows_kernel in unet_train.hip)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rows,
                                                            size_t cols, float* __restrict__ out,
@@ -293,6 +297,228 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     const float s = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
     out[j] = accumulate ? out[j] + s : s;
   }
+}
+
+// the same sum for cols % 4 == 0: a workgroup owns 64 columns as 16 float4
+// column quads x 16 row groups (rows r = g mod 16, two interleaved chains),
+// the 16 group totals added in order -- 4x the loads in flight per lane of
+// wgrad_reduce_kernel, whose 4 row groups left a 256-range sum latency-bound
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restrict__ part, int rows,
+                                                            size_t cols, float* __restrict__ out,
+                                                            int accumulate) {
+  __shared__ f32x4 red[16][16];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const size_t c4 = cols / 4, j = (size_t)blockIdx.x * 16 + tx;
+  const f32x4* p = reinterpret_cast<const f32x4*>(part);
+  f32x4 s0{}, s1{};
+  if (j < c4) {
+    int r = ty;
+    for (; r + 16 < rows; r += 32) {
+      s0 += p[(size_t)r * c4 + j];
+      s1 += p[(size_t)(r + 16) * c4 + j];
+    }
+    if (r < rows) s0 += p[(size_t)r * c4 + j];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && j < c4) {
+    f32x4 s = red[0][tx];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) s += red[g][tx];
+    f32x4* o = reinterpret_cast<f32x4*>(out) + j;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
+// dW (+)= the fixed-order sum of the rows x cols partials
+hipError_t reduce_parts(const float* part, int rows, size_t cols, float* dw, int accumulate, hipStream_t s) {
+  if (WG_REDUCE4 && cols % 4 == 0 && ((uintptr_t)dw & 15) == 0)
+    wgrad_reduce4_kernel<<<(unsigned)((cols / 4 + 15) / 16), 256, 0, s>>>(part, rows, cols, dw, accumulate);
+  else
+    wgrad_reduce_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>(part, rows, cols, dw, accumulate);
+  return hipGetLastError();
+}
+
+#ifndef WG1_LDS
+#define WG1_LDS 1  // 1: 1x1 weight gradients on wg1_lds_kernel; 0: wgrad_conv_kernel<S1, 1> (A/B)
+#endif
+#ifndef WG1_PD
+#define WG1_PD 1   // wg1_lds_kernel global-load prefetch distance in 32-k blocks (1 or 2; A/B: 2 no faster)
+#endif
+
+// The 1x1 convs (the res-block skips) are a plain GEMM dW = dY Xᵀ over K =
+// B * H * W with both operands already K-contiguous in NCHW: one workgroup
+// per (co block 64 MB, ci block 64 NB, K range) stages the 16-k block's dY
+// rows and X rows in LDS once (one float4 per lane per 256 row-quads, rows
+// padded to 20 floats: conflict-free fragment reads) and the 2 x 2 waves
+// multiply their 32 MB x 32 NB sub-tiles out of it -- the LDS-tiled GEMM of
+// the Winograd weight gradient (unet_wgrad_wino.hip) with the NCHW sample
+// stride folded into the K index (H W % 16 == 0: a 16-k block never spans
+// two samples).  Partials per K range, summed in a fixed order by
+// wgrad_reduce_kernel.
+struct W1Args {
+  const float* dy;
+  const float* xa;
+  const float* xb;
+  int Ca, Cb, Cout, HW, nq, qpr;   // nq 32-k blocks, qpr per K range
+  float* P;   // (nks, Cout, Cin)
+};
+
+// per stage a 32-k block: 8 row-quads per row (each row's 128 bytes one
+// whole cache line, 8 lanes), two 16-k MFMA sub-blocks per barrier; the next
+// block's loads are in flight during the current block's MFMAs (WG1_PD = 2:
+// two blocks ahead).  Measured and not kept: an XCD-aware workgroup order
+// putting a K range's tiles on one L2 (same time: the MALL absorbs the
+// re-reads).
+template <int MB, int NB>
+__global__ __launch_bounds__(256) void wg1_lds_kernel(W1Args a) {
+  constexpr int RA = 64 * MB, RB = 64 * NB, PITCH = 36, NU = 2 * (MB + NB);
+  constexpr int WI = 2 * MB, WJ = 2 * NB;
+  __shared__ __attribute__((aligned(16))) float lds[2][(RA + RB) * PITCH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int Cin = a.Ca + a.Cb;
+  const int ncb = Cin / RB, nmb = a.Cout / RA;
+  int r = blockIdx.x;
+  const int nb = r % ncb; r /= ncb;
+  const int mb = r % nmb;
+  const int ks = r / nmb;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int q0 = ks * a.qpr, q1 = min(q0 + a.qpr, a.nq);
+  // staging: thread tid moves row-quad f = tid + 256 u: row f >> 3, k-quad f & 7;
+  // each row's sample-0 pointer is fixed for the workgroup
+  const float* src[NU];
+  long long bstride[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int f = tid + 256 * u;
+    if (u < 2 * MB) {
+      const int co = RA * mb + (f >> 3);
+      src[u] = a.dy + (size_t)co * a.HW + 4 * (f & 7);
+      bstride[u] = (long long)a.Cout * a.HW;
+    } else {
+      const int ci = RB * nb + ((f - 512 * MB) >> 3);
+      const bool lo = ci < a.Ca;
+      src[u] = (lo ? a.xa + (size_t)ci * a.HW : a.xb + (size_t)(ci - a.Ca) * a.HW) + 4 * (f & 7);
+      bstride[u] = (long long)(lo ? a.Ca : a.Cb) * a.HW;
+    }
+  }
+  auto gload = [&](int Q, f32x4 (&stg)[NU]) {
+    const int t0 = 32 * Q, b = t0 / a.HW, p = t0 - b * a.HW;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) stg[u] = *reinterpret_cast<const f32x4*>(src[u] + b * bstride[u] + p);
+  };
+  auto lstore = [&](int buf, const f32x4 (&stg)[NU]) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int f = tid + 256 * u;
+      const int row = u < 2 * MB ? f >> 3 : RA + ((f - 512 * MB) >> 3);
+      *reinterpret_cast<f32x4*>(&lds[buf][row * PITCH + 4 * (f & 7)]) = stg[u];
+    }
+  };
+  f32x4 acc[WI][WJ];
+#pragma unroll
+  for (int i = 0; i < WI; ++i)
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) acc[i][j] = f32x4{};
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      f32x4 av[WI], bv[WJ];
+#pragma unroll
+      for (int i = 0; i < WI; ++i)
+        av[i] = *reinterpret_cast<const f32x4*>(
+            &lds[buf][(32 * MB * wm + 16 * i + c16) * PITCH + 16 * sb + 4 * g]);
+#pragma unroll
+      for (int j = 0; j < WJ; ++j)
+        bv[j] = *reinterpret_cast<const f32x4*>(
+            &lds[buf][(RA + 32 * NB * wn + 16 * j + c16) * PITCH + 16 * sb + 4 * g]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < WI; ++i)
+#pragma unroll
+          for (int j = 0; j < WJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][k], bv[j][k], acc[i][j], 0, 0, 0);
+    }
+  };
+  if (q0 < q1) {
+    // two register stage sets: block Q + 2 is in flight while Q computes and
+    // Q + 1 moves to LDS (2 blocks of compute hide each load)
+    f32x4 s0[NU], s1[NU];
+    gload(q0, s0);
+    lstore(0, s0);
+    if (WG1_PD > 1 && q0 + 1 < q1) gload(q0 + 1, s1);
+    __syncthreads();
+    auto step = [&](int Q, f32x4 (&mine)[NU], f32x4 (&next)[NU]) {
+      const int buf = (Q - q0) & 1;
+      if (WG1_PD > 1) {
+        if (Q + 2 < q1) gload(Q + 2, mine);
+      } else if (Q + 1 < q1) {
+        gload(Q + 1, next);
+      }
+      compute(buf);
+      if (Q + 1 < q1) lstore(buf ^ 1, next);
+      __syncthreads();
+    };
+    for (int Q = q0; Q < q1; Q += 2) {
+      step(Q, s0, s1);
+      if (Q + 1 < q1) step(Q + 1, s1, s0);
+    }
+  }
+  // lane holds rows co = RA mb + 32 MB wm + 16 i + 4 g + e, column ci = RB nb + 32 NB wn + 16 j + c16
+  float* P = a.P + (size_t)ks * a.Cout * Cin;
+  const int co0 = RA * mb + 32 * MB * wm, ci0 = RB * nb + 32 * NB * wn;
+#pragma unroll
+  for (int i = 0; i < WI; ++i)
+#pragma unroll
+    for (int j = 0; j < WJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        P[(size_t)(co0 + 16 * i + 4 * g + e) * Cin + ci0 + 16 * j + c16] = acc[i][j][e];
+}
+
+struct W1Plan {
+  int mb, nb, nq, qpr, nks;   // tile 64 mb x 64 nb
+  size_t part_floats;
+};
+
+// Tile and K split, as measured over forced plans at the U2 B = 32 skip
+// shapes (tools/wgrad_probe.py --skip --sweep): 64 x 64 tiles (the most
+// workgroups in flight) with 8 32-k blocks per K range, or 16 once that still
+// leaves >= 512 workgroups -- 256 .. 768 workgroups, 256 .. 512 k per range,
+// the best measured plan at every shape but one (within 4 %).  A pure
+// function of the shape (bitwise reproducible); ERTD_WG1_MB / _NB / _QPR
+// (diag build) force a plan.
+bool wg1_plan(int Cin, int Cout, int B, int H, int ks, int mode, int act, W1Plan* p) {
+  if (!WG1_LDS || ks != 1 || mode != MODE_S1 || act != ACT_NONE || Cin % 64 || Cout % 64 || B < 1 ||
+      H < 4 || (H * H) % 32)
+    return false;
+  const long long K = (long long)B * H * H;
+  if (K / 32 > (1 << 30)) return false;
+  p->nq = (int)(K / 32);
+  p->mb = ERTD_KNOB("WG1_MB", 1);
+  p->nb = ERTD_KNOB("WG1_NB", 1);
+  if (p->mb < 1 || p->mb > 2 || p->nb < 1 || p->nb > 2 || Cout % (64 * p->mb) || Cin % (64 * p->nb))
+    return false;
+  const long long tiles = (long long)(Cout / (64 * p->mb)) * (Cin / (64 * p->nb));
+  int qpr = tiles * (p->nq / 16) >= 512 ? 16 : 8;
+  qpr = ERTD_KNOB("WG1_QPR", qpr);
+  p->qpr = std::max(1, std::min(qpr, p->nq));
+  p->nks = (p->nq + p->qpr - 1) / p->qpr;
+  p->part_floats = (size_t)p->nks * Cout * Cin;
+  return true;
+}
+
+hipError_t launch_wg1(const W1Plan& pl, const float* dy, const float* x, int Ca, const float* x2, int Cb,
+                      int HW, int Cout, float* part, hipStream_t s) {
+  W1Args a{dy, x, x2, Ca, Cb, Cout, HW, pl.nq, pl.qpr, part};
+  const unsigned nwg = (unsigned)((Cout / (64 * pl.mb)) * ((Ca + Cb) / (64 * pl.nb)) * pl.nks);
+  if (pl.mb == 1 && pl.nb == 1) wg1_lds_kernel<1, 1><<<nwg, 256, 0, s>>>(a);
+  else if (pl.mb == 1) wg1_lds_kernel<1, 2><<<nwg, 256, 0, s>>>(a);
+  else if (pl.nb == 1) wg1_lds_kernel<2, 1><<<nwg, 256, 0, s>>>(a);
+  else wg1_lds_kernel<2, 2><<<nwg, 256, 0, s>>>(a);
+  return hipGetLastError();
 }
 
 int n_cu() {
@@ -378,8 +604,10 @@ extern "C" {
 size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mode) {
   Plan p;
   if (!plan_of(Cin, Cout, B, H, ks, mode, &p)) return 0;
-  // the Winograd path (3x3 stride 1, unet_wgrad_wino.hip) where eligible
-  return std::max(p.part_floats, wgrad_wino_ws_floats(Cin, Cout, B, H, ks, mode)) * sizeof(float);
+  // the Winograd path (3x3 stride 1, unet_wgrad_wino.hip) and the 1x1 GEMM where eligible
+  W1Plan w1;
+  const size_t f1 = wg1_plan(Cin, Cout, B, H, ks, mode, ACT_NONE, &w1) ? w1.part_floats : 0;
+  return std::max({p.part_floats, f1, wgrad_wino_ws_floats(Cin, Cout, B, H, ks, mode)}) * sizeof(float);
 }
 
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
@@ -397,20 +625,25 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
                                            (float*)ws, (hipStream_t)stream);
     return e == hipSuccess ? ERTD_OK : (int)e;
   }
+  hipStream_t s = (hipStream_t)stream;
+  W1Plan w1;
+  if (wg1_plan(Ca + Cb, Cout, B, H, ks, mode, act, &w1)) {
+    if (w1.part_floats * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+    hipError_t e = launch_wg1(w1, dy, x, Ca, x2, Cb, H * H, Cout, (float*)ws, s);
+    if (e != hipSuccess) return (int)e;
+    e = reduce_parts((const float*)ws, w1.nks, (size_t)Cout * (Ca + Cb), dw, accumulate, s);
+    return e == hipSuccess ? ERTD_OK : (int)e;
+  }
   if (p.part_floats * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
   WgArgs a{dy, x, x2, Ca, Cb, Cout, H, p.Ho, p.R, (const float2*)gn, p.ntiles, p.nco, p.nsplit,
            p.cps, p.nchunks, (float*)ws};
-  hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   if (ks == 1) e = launch_a<MODE_S1, 1>(a, act, p.lds, s);
   else if (mode == MODE_S2) e = launch_a<MODE_S2, 3>(a, act, p.lds, s);
   else if (mode == MODE_UP) e = launch_a<MODE_UP, 3>(a, act, p.lds, s);
   else e = launch_a<MODE_S1, 3>(a, act, p.lds, s);
   if (e != hipSuccess) return (int)e;
-  const size_t cols = (size_t)Cout * (Ca + Cb) * ks * ks;
-  wgrad_reduce_kernel<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>((const float*)ws, p.nsplit, cols,
-                                                                    dw, accumulate);
-  e = hipGetLastError();
+  e = reduce_parts((const float*)ws, p.nsplit, (size_t)Cout * (Ca + Cb) * ks * ks, dw, accumulate, s);
   return e == hipSuccess ? ERTD_OK : (int)e;
 }
 

@@ -185,8 +185,13 @@ def test_unet_train_rejects_bf16(cuda_dev):
     (64, 0, 64, 64, 3, 2, 1),      # Upsample 64 -> 128
     (128, 0, 128, 32, 3, 2, 8),    # u1.up 32 -> 64 (Winograd wgrad over the upsampled input)
     (256, 0, 256, 16, 3, 2, 8),    # u2.up 16 -> 32
-    (96, 32, 64, 32, 1, 0, 2),     # 1x1 skip on a concat
+    (96, 32, 64, 32, 1, 0, 2),     # 1x1 skip on a concat (LDS GEMM; concat split inside a ci tile)
     (256, 0, 768, 16, 1, 0, 2),    # attention qkv
+    (128, 64, 64, 64, 1, 0, 32),   # u0 skip 192 -> 64 at the train batch (64 co x 64 ci tiles)
+    (384, 128, 256, 16, 1, 0, 32), # u2 skip 512 -> 256 (128 x 128 tiles)
+    (64, 0, 128, 32, 1, 0, 3),     # d1 skip 64 -> 128 (128 co x 64 ci tiles)
+    (48, 0, 40, 32, 1, 0, 2),      # ragged channels: the implicit-GEMM 1x1 path
+    (64, 0, 64, 16, 1, 0, 1),      # K = 256: a single K range
 ])
 def test_conv_wgrad_vs_autograd(Ca, Cb, Cout, H, ks, mode, B, cuda_dev):
     from ertdiff import _lib
