@@ -101,7 +101,8 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
     const float* __restrict__ xa, int Ca, const float* __restrict__ xb, int Cb, int HW, int groups,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float2* __restrict__ mr,
     int act, const float* __restrict__ dy, float* __restrict__ dxa, float* __restrict__ dxb,
-    int accumulate, float* __restrict__ dgb, float* __restrict__ csum, long long ldc) {
+    int accumulate, float* __restrict__ dgb, float* __restrict__ csum, long long ldc,
+    const float* __restrict__ addc) {
   __shared__ double part[2][GNB_CB][4];
   __shared__ float cred[GNB_CB][4];
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -174,11 +175,16 @@ __global__ __launch_bounds__(256) void gn_act_bwd_kernel(
     const float4* x = (const float4*)xptr(c);
     float4* dx = (float4*)(c < Ca ? dxa + ((size_t)b * Ca + c) * HW : dxb + ((size_t)b * Cb + c - Ca) * HW);
     const float4* d = (const float4*)(dy + ((size_t)b * C + c) * HW);
+    const float4* ad = addc ? (const float4*)(addc + ((size_t)b * C + c) * HW) : nullptr;
     const float ga = gamma[c], be = beta[c];
     float cs = 0.f;
     for (int p = p0; p < HW4; p += pst) {
       const float4 xv = x[p], dv = d[p];
       float4 o = accumulate ? dx[p] : float4{0.f, 0.f, 0.f, 0.f};
+      if (ad) {   // (dx + addc) + the GroupNorm term: the order of a separate add before
+        const float4 av = ad[p];
+        o = accumulate ? float4{o.x + av.x, o.y + av.y, o.z + av.z, o.w + av.w} : av;
+      }
       float xh, dn, q0, q1, q2, q3;
       dn = dxn_of(xv.x, dv.x, ga, be, xh); q0 = rstd * ((ga * dn - mA) - xh * mB); o.x += q0;
       dn = dxn_of(xv.y, dv.y, ga, be, xh); q1 = rstd * ((ga * dn - mA) - xh * mB); o.y += q1;
@@ -681,7 +687,7 @@ int ertd_gn_act_apply(const float* x, int Ca, const float* x2, int Cb, int B, in
 static int gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
                            const float* gamma, const float* beta, const float* mr, int act,
                            const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
-                           float* csum, long long ldc, void* stream) {
+                           float* csum, long long ldc, const float* addc, void* stream) {
   const int C = Ca + Cb;
   if (!x || !gamma || !beta || !mr || !dy || !dx || !dgb_part || B < 1 || Ca < 1 || Cb < 0 ||
       (Cb > 0 && (!x2 || !dx2)) || groups < 1 || C % groups || HW < 4 || HW % 4 ||
@@ -690,7 +696,7 @@ static int gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int 
   const dim3 grid(groups, B);
   hipStream_t s = (hipStream_t)stream;
   gn_act_bwd_kernel<<<grid, 256, 0, s>>>(x, Ca, x2, Cb, HW, groups, gamma, beta, (const float2*)mr, act,
-                                         dy, dx, dx2, accumulate, dgb_part, csum, ldc);
+                                         dy, dx, dx2, accumulate, dgb_part, csum, ldc, addc);
   return rcode(hipGetLastError());
 }
 
@@ -699,7 +705,7 @@ int ertd_gn_act_backward(const float* x, int Ca, const float* x2, int Cb, int B,
                          const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
                          void* stream) {
   return gn_act_backward(x, Ca, x2, Cb, B, HW, groups, gamma, beta, mr, act, dy, dx, dx2, accumulate,
-                         dgb_part, nullptr, 0, stream);
+                         dgb_part, nullptr, 0, nullptr, stream);
 }
 
 int ertd_gn_act_backward_csum(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
@@ -708,7 +714,16 @@ int ertd_gn_act_backward_csum(const float* x, int Ca, const float* x2, int Cb, i
                               float* csum, long long ldc, void* stream) {
   if (!csum) return ERTD_EINVAL;
   return gn_act_backward(x, Ca, x2, Cb, B, HW, groups, gamma, beta, mr, act, dy, dx, dx2, accumulate,
-                         dgb_part, csum, ldc, stream);
+                         dgb_part, csum, ldc, nullptr, stream);
+}
+
+int ertd_gn_act_backward_add(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                             const float* gamma, const float* beta, const float* mr, int act,
+                             const float* dy, const float* addc, float* dx, float* dx2, int accumulate,
+                             float* dgb_part, float* csum, long long ldc, void* stream) {
+  if (!addc) return ERTD_EINVAL;
+  return gn_act_backward(x, Ca, x2, Cb, B, HW, groups, gamma, beta, mr, act, dy, dx, dx2, accumulate,
+                         dgb_part, csum, ldc, addc, stream);
 }
 
 int ertd_im2col(const float* x, int C, int B, int H, int ks, int mode, float* out, void* stream) {

@@ -116,6 +116,8 @@ SIGNATURES = {
                                   _I, _VP, _VP]),
     "ertd_gn_act_backward_csum": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _I, _VP, _VP, _VP,
                                        _I, _VP, _VP, ctypes.c_longlong, _VP]),
+    "ertd_gn_act_backward_add": (_I, [_VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _I, _VP, _VP, _VP,
+                                      _VP, _I, _VP, _VP, ctypes.c_longlong, _VP]),
     "ertd_im2col": (_I, [_VP, _I, _I, _I, _I, _I, _VP, _VP]),
     "ertd_wgrad_ws_bytes": (_SZ, [_I, _I, _I, _I]),
     "ertd_wgrad_gemm": (_I, [_VP, _VP, _I, _I, _I, _I, _LL, _LL, _VP, _I, _VP, _SZ, _VP]),

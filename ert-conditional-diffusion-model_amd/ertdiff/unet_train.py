@@ -209,15 +209,26 @@ class _K:
         return out
 
     def gn_backward(self, xa, xb, groups, gamma, beta, mr, act, dy, dxa, dxb, accumulate,
-                    csum=None):
+                    csum=None, add=None):
         """dxa / dxb (+)= d act(GroupNorm(cat(xa, xb))); returns (dgamma, dbeta).
         csum: an optional (B, C) row-strided view that receives the per-sample
-        pixel sums of the gradient added (fused; the ResBlock emb gradient)."""
+        pixel sums of the gradient added (fused; the ResBlock emb gradient).
+        add: an optional (B, Ca + Cb, H, W) gradient of the same input added
+        first (the ResBlock skip / identity path), fused into the same pass."""
         B, Ca, H, W = xa.shape
         Cb = 0 if xb is None else xb.shape[1]
         C = Ca + Cb
         part = self.empty(B, 2, C)
-        if csum is not None and C // groups <= 64:
+        if add is not None:
+            assert add.shape == (B, C, H, W) and add.is_contiguous()
+            if csum is not None:
+                assert C // groups <= 64 and csum.shape == (B, C) and csum.stride(1) == 1
+            _lib.check(self.lib.ertd_gn_act_backward_add(
+                xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups, gamma.data_ptr(), beta.data_ptr(),
+                mr.data_ptr(), act, dy.data_ptr(), add.data_ptr(), dxa.data_ptr(), _p(dxb),
+                int(accumulate), part.data_ptr(), _p(csum), 0 if csum is None else csum.stride(0),
+                self.s), "gn_act_backward_add")
+        elif csum is not None and C // groups <= 64:
             assert csum.shape == (B, C) and csum.stride(1) == 1
             _lib.check(self.lib.ertd_gn_act_backward_csum(
                 xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups, gamma.data_ptr(), beta.data_ptr(),
@@ -452,16 +463,6 @@ class _Grads:
         buf, acc = self.target(t)
         self.k.elt(ELT_SCALE, v, out=buf, alpha=1.0, accumulate=acc)
 
-    def add_cat(self, dx, xa, xb):
-        """Split dL/d cat(xa, xb) into the two inputs' gradients."""
-        if xb is None:
-            self.add(xa, dx, owned=True)
-            return
-        Ca = xa.shape[1]
-        for t, c0, cd in ((xa, 0, Ca), (xb, Ca, xb.shape[1])):
-            buf, acc = self.target(t)
-            self.k.chan_copy(dx, c0, cd, buf, 0, accumulate=acc)
-
 
 def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, gn=None, act=0,
                    bias_grad=True, also_bias=None):
@@ -664,8 +665,7 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                 if need_x:
                     grads["__x__"] = dx.view(B, -1)
             elif kind == "attn":
-                x = d["x"]
-                G.add(x, dy)                          # y = x + proj(O)
+                x = d["x"]                            # y = x + proj(O): dy joins the norm's backward
                 dO = _conv_backward(k, grads, n + ".proj", W[n + ".proj.weight"], d["O"], None,
                                     dy, MODE_S1)
                 C = x.shape[1]
@@ -691,7 +691,7 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                                      gn=d["ss"], act=ACT_GN)
                 buf, acc = G.target(x)
                 dg, db = k.gn_backward(x, None, g, W[n + ".norm.weight"], W[n + ".norm.bias"],
-                                       d["mr"], ACT_GN, dan, buf, None, acc)
+                                       d["mr"], ACT_GN, dan, buf, None, acc, add=dy)
                 grads[n + ".norm.weight"], grads[n + ".norm.bias"] = dg, db
             elif kind == "res":
                 xa, xb = d["xa"], d["xb"]
@@ -700,12 +700,13 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                 da2 = _conv_backward(k, grads, n + ".conv2", W[n + ".conv2.weight"], d["h"], None,
                                      dy, MODE_S1, gn=d["ss2"], act=ACT_GN_SILU,
                                      also_bias=n + ".skip.bias" if d["skip"] else None)
+                # the skip path's input gradient (dy itself for an identity skip) is
+                # added by norm1's GroupNorm backward below, in the same pass
                 if d["skip"]:
                     dxs = _conv_backward(k, grads, n + ".skip", W[n + ".skip.weight"], xa, xb, dy,
                                          MODE_S1, bias_grad=False)
-                    G.add_cat(dxs, xa, xb)
                 else:
-                    G.add(xa, dy)
+                    dxs = dy
                 h = d["h"]
                 dh = k.empty(*h.shape)
                 # h = conv1(a1) + b1 + emb(ea): the emb grad is dh summed over pixels,
@@ -725,7 +726,7 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                 if acc_a != acc_b:     # one accumulate flag per launch: pre-zero the new one
                     (dxb if acc_a else dxa).zero_()
                 dg, db = k.gn_backward(xa, xb, g, W[n + ".norm1.weight"], W[n + ".norm1.bias"],
-                                       d["mr1"], ACT_GN_SILU, da1, dxa, dxb, acc_a or acc_b)
+                                       d["mr1"], ACT_GN_SILU, da1, dxa, dxb, acc_a or acc_b, add=dxs)
                 grads[n + ".norm1.weight"], grads[n + ".norm1.bias"] = dg, db
         # ---- every ResBlock's emb projection at once: ea (B, temb) -> (B, sum C)
         ea, w_all = tape["ea"], tape["w_all"]

@@ -401,6 +401,10 @@ int ertd_unet_plan_destroy(ertd_unet_plan* plan);
  * ertd_gn_act_backward_csum: the same, plus csum[b * ldc + c] = sum over the HW pixels
  *   of the gradient this call adds to channel c of sample b (a ResBlock's emb-projection
  *   gradient when dx is the conv1 output's gradient; channels per group <= 64).
+ * ertd_gn_act_backward_add: the same with an addend: dx / dx2 (+)= addc + the GroupNorm
+ *   gradient, addc (B, C, HW) in the concatenated channel order (a ResBlock's skip / identity
+ *   gradient of the same input), added first (as a separate add before the call would); csum
+ *   optional (null: none), and when given it sums the GroupNorm term only.
  * ertd_im2col: out (B, C*ks*ks, Ho*Ho) patches of x (B, C, H, H), mode 0 s1 / 1 s2 / 2 upsample.
  * ertd_wgrad_gemm: dW (M, N) = sum_b dY_b (M, P) . X_b (N, P)^T (batch strides bsA, bsB),
  *   fp32 MFMA, split per sample + fixed-order reduction; ws >= ertd_wgrad_ws_bytes.
@@ -435,6 +439,10 @@ int ertd_gn_act_backward_csum(const float* x, int Ca, const float* x2, int Cb, i
                               const float* gamma, const float* beta, const float* mr, int act,
                               const float* dy, float* dx, float* dx2, int accumulate, float* dgb_part,
                               float* csum, long long ldc, void* stream);
+int ertd_gn_act_backward_add(const float* x, int Ca, const float* x2, int Cb, int B, int HW, int groups,
+                             const float* gamma, const float* beta, const float* mr, int act,
+                             const float* dy, const float* addc, float* dx, float* dx2, int accumulate,
+                             float* dgb_part, float* csum, long long ldc, void* stream);
 int ertd_im2col(const float* x, int C, int B, int H, int ks, int mode, float* out, void* stream);
 size_t ertd_wgrad_ws_bytes(int M, int N, int P, int B);
 int ertd_wgrad_gemm(const float* dY, const float* X, int M, int N, int P, int B, long long bsA,

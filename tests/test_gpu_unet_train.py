@@ -411,6 +411,37 @@ def test_gn_act_backward_vs_autograd(Ca, Cb, HW, groups, act, acc, cuda_dev):
         ec = _rel(wide[:, 3:3 + C], xr.grad.sum(2))
         record_error(f"gn_act_backward_csum_{C}_{HW}_g{groups}", ec)
         assert ec < 1e-4, ec    # fp32 sums of HW terms (the gradient tests' tolerance)
+    # the fused addend (a ResBlock's skip / identity gradient, concatenated
+    # channel order): bitwise the separate add (prev + addc, or addc) followed
+    # by the plain entry; csum (when given) sums the GroupNorm term only
+    addc = torch.randn(B, C, HW, generator=g).to(dev)
+    sep = (prev.to(dev) + addc) if acc else addc.clone()
+    sa, sb = sep[:, :Ca].contiguous(), (sep[:, Ca:].contiguous() if Cb else None)
+    part_s = torch.empty(B, 2, C, device=dev)
+    assert lib.ertd_gn_act_backward(xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(), Cb, B, HW,
+                                    groups, gam.data_ptr(), bet.data_ptr(), mr.data_ptr(), act,
+                                    dyd.data_ptr(), sa.data_ptr(), None if sb is None else sb.data_ptr(),
+                                    1, part_s.data_ptr(), s) == 0
+    fa = prev[:, :Ca].contiguous().to(dev) if acc else torch.full((B, Ca, HW), float("nan"), device=dev)
+    fb = None
+    if Cb:
+        fb = prev[:, Ca:].contiguous().to(dev) if acc else torch.full((B, Cb, HW), float("nan"), device=dev)
+    part_f = torch.empty(B, 2, C, device=dev)
+    cs = torch.empty(B, C, device=dev) if C // groups <= 64 else None
+    assert lib.ertd_gn_act_backward_add(
+        xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(), Cb, B, HW, groups, gam.data_ptr(),
+        bet.data_ptr(), mr.data_ptr(), act, dyd.data_ptr(), addc.data_ptr(), fa.data_ptr(),
+        None if fb is None else fb.data_ptr(), acc, part_f.data_ptr(),
+        None if cs is None else cs.data_ptr(), C, s) == 0
+    assert torch.equal(fa, sa) and torch.equal(part_f, part)
+    if Cb:
+        assert torch.equal(fb, sb)
+    if cs is not None:
+        assert _rel(cs, xr.grad.sum(2)) < 1e-4
+    assert lib.ertd_gn_act_backward_add(
+        xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(), Cb, B, HW, groups, gam.data_ptr(),
+        bet.data_ptr(), mr.data_ptr(), act, dyd.data_ptr(), None, fa.data_ptr(),
+        None if fb is None else fb.data_ptr(), acc, part_f.data_ptr(), None, 0, s) != 0
 
 
 @pytest.mark.gpu

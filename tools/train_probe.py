@@ -8,7 +8,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "ert-conditional-diffusion-model_amd"))
+# ERTD_PKG_PATH: an alternative copy of the package (A/B of host-side changes)
+sys.path.insert(0, os.environ.get("ERTD_PKG_PATH") or os.path.join(ROOT, "ert-conditional-diffusion-model_amd"))
 
 import torch  # noqa: E402
 
