@@ -746,12 +746,25 @@ size_t ertd_conv2d_workspace_bytes(int cin, int cout, int ks, int precision, int
 }
 
 namespace {
+// which Winograd layout ertd_conv2d dispatches (geometry only)
+void conv2d_wino_flags(int Cin, int Ca, int Cout, int ks, int mode, int act, int precision, int B, int Ho,
+                       bool* wino, bool* wino4) {
+  const bool bf = bf_prec(precision);
+  *wino4 = !bf && ks == 3 && Cout > 1 && conv_packed_floats_wino4(Cin, Cout) > 0 &&
+           ((mode == MODE_S1 && wino4_ok(Cin, Ca, Cout, Ho, B)) ||
+            (mode == MODE_UP && act == ACT_NONE && wino4s_up_ok(Cin, Ca, Cout, Ho, B)));
+  *wino = *wino4 || (!bf && ks == 3 && mode == MODE_S1 && Cout > 1 &&
+                     conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho));
+}
+
 // ertd_conv2d: pack (unless `pack` is false: ws already holds this shape's
-// packing from an earlier call) and launch
+// packing from an earlier call) and launch; gnp (B, Cout, gn_np) float2: the
+// GroupNorm partials of the output from the epilogue (gn_np must be what
+// ertd_conv2d_gn_parts returns for the call, > 0)
 int conv2d_impl(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
                 const float* bias, int Cout, int ks, int mode, const float* gn, int act,
                 const float* ebias, int eb_stride, const float* res, float* out, int precision,
-                void* ws, size_t ws_bytes, void* stream, bool pack) {
+                void* ws, size_t ws_bytes, void* stream, bool pack, float* gnp = nullptr, int gn_np = 0) {
   const int Cin = Ca + Cb;
   if (!x || (pack && !w) || !bias || !out || !ws || B < 1 || Ca < 1 || Cb < 0 || (Cb > 0 && !x2) ||
       !conv2d_geom_ok(Cin, Cout, ks, precision, B, H, mode) || act < ACT_NONE || act > ACT_GN ||
@@ -767,11 +780,9 @@ int conv2d_impl(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   // the Winograd path reads only its own packing: skip the direct one then
   const int Ho_ = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   const bool bf = bf_prec(precision), split = precision == ERTD_PREC_BF16X3;
-  const bool wino4 = !bf && ks == 3 && Cout > 1 && conv_packed_floats_wino4(Cin, Cout) > 0 &&
-                     ((mode == MODE_S1 && wino4_ok(Cin, Ca, Cout, Ho_, B)) ||
-                      (mode == MODE_UP && act == ACT_NONE && wino4s_up_ok(Cin, Ca, Cout, Ho_, B)));
-  const bool wino = wino4 || (!bf && ks == 3 && mode == MODE_S1 && Cout > 1 &&
-                              conv_packed_floats_wino(Cin, Cout) > 0 && conv_wino_ok(Cin, Ca, Cout, Ho_));
+  bool wino, wino4;
+  conv2d_wino_flags(Cin, Ca, Cout, ks, mode, act, precision, B, Ho_, &wino, &wino4);
+  if (gnp && (bf || gn_np < 1)) return ERTD_EINVAL;
   hipError_t e = hipSuccess;
   if (!wino && pack)
     e = bf ? launch_pack_conv_bf16(w, Cin, Cout, ks, pk, s, split)
@@ -795,6 +806,10 @@ int conv2d_impl(const float* x, int Ca, const float* x2, int Cb, int B, int H, c
   }
   a.bimg = bimg;
   a.split = split ? 1 : 0;
+  if (gnp) {
+    if (conv_gn_parts(ks, mode, act, a, B) != gn_np) return ERTD_EINVAL;
+    a.gnp = (float2*)gnp;
+  }
   e = bf ? launch_conv_bf16(ks, mode, act, a, B, s) : launch_conv(ks, mode, act, a, B, s);
   return e == hipErrorInvalidValue ? ERTD_EINVAL : rcode(e);
 }
@@ -814,6 +829,44 @@ int ertd_conv2d_run(const float* x, int Ca, const float* x2, int Cb, int B, int 
                     size_t ws_bytes, void* stream) {
   return conv2d_impl(x, Ca, x2, Cb, B, H, nullptr, bias, Cout, ks, mode, gn, act, ebias, eb_stride, res,
                      out, precision, ws, ws_bytes, stream, false);
+}
+
+int ertd_conv2d_gn_parts(int Ca, int Cb, int Cout, int ks, int mode, int act, int precision, int B, int H) {
+  const int Cin = Ca + Cb;
+  if (Ca < 1 || Cb < 0 || !conv2d_geom_ok(Cin, Cout, ks, precision, B, H, mode) || bf_prec(precision) ||
+      act < ACT_NONE || act > ACT_GN)
+    return 0;
+  const int Ho = mode == MODE_S2 ? H / 2 : (mode == MODE_UP ? 2 * H : H);
+  bool wino, wino4;
+  conv2d_wino_flags(Cin, Ca, Cout, ks, mode, act, precision, B, Ho, &wino, &wino4);
+  const Conv2dWs need = conv2d_ws(Cin, Ca, Cout, ks, precision, B, H, mode, act);
+  // the dispatch reads only which pointers are set: sentinels, as the walk's dry run
+  const float* sent = reinterpret_cast<const float*>(16);
+  ConvArgs q{};
+  q.Ca = Ca; q.Cb = Cb; q.Cin = Cin; q.Cout = Cout;
+  q.Hs = H; q.Ws = H; q.Ho = Ho; q.Wo = Ho;
+  q.wpk_wino4 = wino4 ? sent : nullptr;
+  q.wpk_wino = wino && !wino4 ? sent : nullptr;
+  q.ksplit_buf = wino && need.kbuf_floats ? const_cast<float*>(sent) : nullptr;
+  return conv_gn_parts(ks, mode, act, q, B);
+}
+
+int ertd_conv2d_gn(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
+                   const float* bias, int Cout, int ks, int mode, const float* gn, int act,
+                   const float* ebias, int eb_stride, const float* res, float* out, int precision,
+                   void* ws, size_t ws_bytes, float* gn_parts, int gn_np, void* stream) {
+  if (!gn_parts) return ERTD_EINVAL;
+  return conv2d_impl(x, Ca, x2, Cb, B, H, w, bias, Cout, ks, mode, gn, act, ebias, eb_stride, res, out,
+                     precision, ws, ws_bytes, stream, true, gn_parts, gn_np);
+}
+
+int ertd_conv2d_run_gn(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* bias,
+                       int Cout, int ks, int mode, const float* gn, int act, const float* ebias,
+                       int eb_stride, const float* res, float* out, int precision, void* ws,
+                       size_t ws_bytes, float* gn_parts, int gn_np, void* stream) {
+  if (!gn_parts) return ERTD_EINVAL;
+  return conv2d_impl(x, Ca, x2, Cb, B, H, nullptr, bias, Cout, ks, mode, gn, act, ebias, eb_stride, res,
+                     out, precision, ws, ws_bytes, stream, false, gn_parts, gn_np);
 }
 
 // dX (B, Cin, H, H) (+)= the input gradient of y = conv(x) (Cout, Cin, ks, ks; mode as

@@ -90,6 +90,11 @@ SIGNATURES = {
                               _VP, _VP, _VP, _VP, _VP]),
     "ertd_conv2d_run": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP, _I,
                              _VP, _SZ, _VP]),
+    "ertd_conv2d_gn_parts": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I]),
+    "ertd_conv2d_gn": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP,
+                            _I, _VP, _SZ, _VP, _I, _VP]),
+    "ertd_conv2d_run_gn": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP, _I,
+                                _VP, _SZ, _VP, _I, _VP]),
     "ertd_group_norm_partials": (_I, [_VP, _I, _I, _I, _I, _VP, _VP]),
     "ertd_group_norm_finalize": (_I, [_VP, _I, _I, _VP, _I, _I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP]),
     "ertd_conv2d_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),

@@ -46,6 +46,10 @@ ACT_GN_SILU, ACT_GN = 1, 2
 MODE_S1, MODE_S2, MODE_UP = 0, 1, 2
 ELT_SILU, ELT_SILU_BWD, ELT_RELU, ELT_RELU_BWD, ELT_ADD, ELT_SCALE = range(6)
 PREC_FP32 = 0
+# the forward's GroupNorm statistics from the partials the producing conv's
+# epilogue writes (ertd_conv2d_gn), finalized per group; False: a separate
+# statistics pass over every normalized tensor (ertd_gn_stats_mr)
+GN_FROM_EPILOGUE = True
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -138,6 +142,9 @@ class _K:
         # flush_reductions() at the end of the backward walk (nothing reads them
         # before the optimizer); defer=False launches each one in place
         self.deferred = [] if defer else None
+        # GroupNorm partials of conv outputs: id(tensor) -> (tensor, parts, np)
+        self.gparts: Dict[int, tuple] = {}
+        self._gnp_np: Dict[tuple, int] = {}
 
     def empty(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)
@@ -158,11 +165,14 @@ class _K:
         return self._ws
 
     # ---- convolution forward / input gradient (ertd_conv2d)
-    def conv(self, x, w, b, xb=None, mode=MODE_S1, ebias=None, res=None, gn=None, act=0, name=None):
+    def conv(self, x, w, b, xb=None, mode=MODE_S1, ebias=None, res=None, gn=None, act=0, name=None,
+             gn_out=True):
         """conv(act(cat(x, xb))) + b (+ ebias[:, :, None, None]) (+ res); act(v) =
         v * gn.scale + gn.shift (+ SiLU) applied while staging; ebias may be a
         column block of a wider (B, n) matrix (its row stride is passed).
-        name: the call site (its packing lives in the pack registry)."""
+        name: the call site (its packing lives in the pack registry).
+        gn_out: the output will be GroupNorm'd -- keep the epilogue's partials
+        when the dispatched kernel writes them (gn_stats finalizes from them)."""
         B, Ca, H, _ = x.shape
         Cb = 0 if xb is None else xb.shape[1]
         Cout, Cin, ks, _ = w.shape
@@ -178,7 +188,27 @@ class _K:
         else:
             ws = self.ws(n)
         eb_ld = 0 if ebias is None else ebias.stride(0)
-        if packed:
+        np_ = 0
+        if gn_out and GN_FROM_EPILOGUE:
+            key = (Ca, Cb, Cout, ks, mode, act, B, H)
+            np_ = self._gnp_np.get(key)
+            if np_ is None:
+                np_ = self._gnp_np[key] = self.lib.ertd_conv2d_gn_parts(Ca, Cb, Cout, ks, mode, act,
+                                                                         PREC_FP32, B, H)
+        if np_ > 0:
+            parts = self.empty(B, Cout, np_, 2)
+            self.gparts[id(out)] = (out, parts, np_)
+            if packed:
+                _lib.check(self.lib.ertd_conv2d_run_gn(
+                    x.data_ptr(), Ca, _p(xb), Cb, B, H, b.data_ptr(), Cout, ks, mode, _p(gn), act, _p(ebias),
+                    eb_ld, _p(res), out.data_ptr(), PREC_FP32, ws.data_ptr(), ws.numel(), parts.data_ptr(),
+                    np_, self.s), "conv2d_run_gn")
+            else:
+                _lib.check(self.lib.ertd_conv2d_gn(
+                    x.data_ptr(), Ca, _p(xb), Cb, B, H, w.data_ptr(), b.data_ptr(), Cout, ks, mode, _p(gn),
+                    act, _p(ebias), eb_ld, _p(res), out.data_ptr(), PREC_FP32, ws.data_ptr(), ws.numel(),
+                    parts.data_ptr(), np_, self.s), "conv2d_gn")
+        elif packed:
             _lib.check(self.lib.ertd_conv2d_run(
                 x.data_ptr(), Ca, _p(xb), Cb, B, H, b.data_ptr(), Cout, ks, mode, _p(gn), act, _p(ebias), eb_ld,
                 _p(res), out.data_ptr(), PREC_FP32, ws.data_ptr(), ws.numel(), self.s), "conv2d_run")
@@ -190,11 +220,35 @@ class _K:
         return out
 
     # ---- GroupNorm
+    def _gn_parts(self, t):
+        """(parts, np) of t: its conv's epilogue partials, else a partials pass."""
+        rec = self.gparts.get(id(t))
+        if rec is not None and rec[0] is t:
+            return rec[1], rec[2]
+        B, C, H, W = t.shape
+        np_ = H * W // 256
+        parts = self.empty(B, C, np_, 2)
+        _lib.check(self.lib.ertd_group_norm_partials(t.data_ptr(), C, B, H * W, np_, parts.data_ptr(),
+                                                     self.s), "group_norm_partials")
+        self.gparts[id(t)] = (t, parts, np_)
+        return parts, np_
+
     def gn_stats(self, xa, xb, groups, gamma, beta):
+        """GroupNorm {scale, shift} (B, C, 2) and {mean, rstd} (B, groups, 2) of
+        cat(xa, xb): from the producing convs' epilogue partials where they
+        exist (GN_FROM_EPILOGUE), else one statistics pass."""
         B, Ca, H, W = xa.shape
         Cb = 0 if xb is None else xb.shape[1]
         ss = self.empty(B, Ca + Cb, 2)
         mr = self.empty(B, groups, 2)
+        if GN_FROM_EPILOGUE and (H * W) % 256 == 0 and (
+                id(xa) in self.gparts or (xb is not None and id(xb) in self.gparts)):
+            pa, npa = self._gn_parts(xa)
+            pb, npb = self._gn_parts(xb) if xb is not None else (None, 0)
+            _lib.check(self.lib.ertd_group_norm_finalize(
+                pa.data_ptr(), npa, Ca, _p(pb), npb, Cb, B, H * W, groups, gamma.data_ptr(),
+                beta.data_ptr(), ss.data_ptr(), mr.data_ptr(), self.s), "group_norm_finalize")
+            return ss, mr
         _lib.check(self.lib.ertd_gn_stats_mr(xa.data_ptr(), Ca, _p(xb), Cb, B, H * W, groups,
                                              gamma.data_ptr(), beta.data_ptr(), ss.data_ptr(),
                                              mr.data_ptr(), self.s), "gn_stats_mr")
@@ -568,7 +622,8 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
                        act=ACT_GN_SILU, name=n + ".conv1")
             ss2, mr2 = k.gn_stats(h, None, g, W[n + ".norm2.weight"], W[n + ".norm2.bias"])
             if Cin != cout:
-                sk = k.conv(xa, W[n + ".skip.weight"], W[n + ".skip.bias"], xb=xb, name=n + ".skip")
+                sk = k.conv(xa, W[n + ".skip.weight"], W[n + ".skip.bias"], xb=xb, name=n + ".skip",
+                            gn_out=False)
             else:
                 sk = xa
             y = k.conv(h, W[n + ".conv2.weight"], W[n + ".conv2.bias"], res=sk, gn=ss2, act=ACT_GN_SILU,
@@ -599,7 +654,7 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
             N = h.shape[2] * h.shape[3]
             ssn, mrn = k.gn_stats(h, None, g, W[n + ".norm.weight"], W[n + ".norm.bias"])
             qkv = k.conv(h, W[n + ".qkv.weight"], W[n + ".qkv.bias"], gn=ssn, act=ACT_GN,
-                         name=n + ".qkv").view(B, 3, C, N)
+                         name=n + ".qkv", gn_out=False).view(B, 3, C, N)
             q, kk, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
             S = k.empty(B, N, N)    # S[i][j] = sum_c q[c][i] k[c][j]
             k.gemm(q, (1, N, 3 * C * N), kk, (N, 1, 3 * C * N), S, (N, 1, N * N), N, N, C, batch=B)
@@ -621,7 +676,8 @@ def unet_train_forward(model: ConditionalUNet, x, t, cond):
                 nodes.append(("up", f"up.{i}.upsample", dict(x=h, y=y)))
                 h = y
         sso, mro = k.gn_stats(h, None, g, W["norm_out.weight"], W["norm_out.bias"])
-        eps = k.conv(h, W["conv_out.weight"], W["conv_out.bias"], gn=sso, act=ACT_GN_SILU, name="conv_out")
+        eps = k.conv(h, W["conv_out.weight"], W["conv_out.bias"], gn=sso, act=ACT_GN_SILU, name="conv_out",
+                     gn_out=False)
         nodes.append(("out", "conv_out", dict(x=h, ss=sso, mr=mro, y=eps)))
     return eps.reshape(B, -1), tape
 

@@ -310,6 +310,21 @@ int ertd_conv2d_run(const float* x, int Ca, const float* x2, int Cb, int B, int 
                     int Cout, int ks, int mode, const float* gn, int act, const float* ebias,
                     int eb_stride, const float* res, float* out, int precision, void* ws,
                     size_t ws_bytes, void* stream);
+/* ertd_conv2d_gn_parts: np > 0 when the fp32 conv ertd_conv2d dispatches for this geometry
+ *   emits the GroupNorm partials of its output from the epilogue ((B, Cout, np) float2
+ *   {sum, M2} over HW / np pixels each, the ertd_group_norm_partials format), else 0.
+ * ertd_conv2d_gn / ertd_conv2d_run_gn: ertd_conv2d / ertd_conv2d_run that also write those
+ *   partials (gn_np = that np), for ertd_group_norm_finalize without re-reading the output
+ *   (the train walk).  */
+int ertd_conv2d_gn_parts(int Ca, int Cb, int Cout, int ks, int mode, int act, int precision, int B, int H);
+int ertd_conv2d_gn(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* w,
+                   const float* bias, int Cout, int ks, int mode, const float* gn, int act,
+                   const float* ebias, int eb_stride, const float* res, float* out, int precision,
+                   void* ws, size_t ws_bytes, float* gn_parts, int gn_np, void* stream);
+int ertd_conv2d_run_gn(const float* x, int Ca, const float* x2, int Cb, int B, int H, const float* bias,
+                       int Cout, int ks, int mode, const float* gn, int act, const float* ebias,
+                       int eb_stride, const float* res, float* out, int precision, void* ws,
+                       size_t ws_bytes, float* gn_parts, int gn_np, void* stream);
 int ertd_group_norm_stats(const float* x, int Ca, const float* x2, int Cb, int B, int HW,
                           int groups, const float* gamma, const float* beta, float* out,
                           void* stream);

@@ -602,3 +602,59 @@ def test_unet_train_step_u5_runs(cuda_dev):
     assert all(bool(torch.isfinite(p.grad).all()) for p in m.parameters())
     l1 = unet_train_step(m, opt, x0, cond, T, ab, t=t, noise=noise)
     assert l1 < l0, (l0, l1)
+
+
+@pytest.mark.parametrize("Ca,Cb,Cout,H,mode,act,B", [
+    (64, 0, 64, 64, 0, 1, 4),      # ResBlock conv at 64x64 (register-weight F(4x4))
+    (128, 64, 128, 32, 0, 1, 4),   # concat input
+    (128, 0, 128, 16, 2, 0, 4),    # Upsample conv 16 -> 32
+    (64, 0, 64, 64, 0, 1, 32),     # the train batch
+])
+def test_conv2d_gn_parts_finalize(Ca, Cb, Cout, H, mode, act, B, cuda_dev):
+    """ertd_conv2d_gn / _run_gn (the train walk's forward convs): the same output
+    bits as ertd_conv2d, and the epilogue's GroupNorm partials finalized give
+    the statistics of a separate pass (ertd_gn_stats_mr) to fp32 rounding."""
+    from ertdiff import _lib
+    lib = _lib.lib()
+    dev, s = cuda_dev, _lib.stream_of(cuda_dev)
+    g = torch.Generator(device=dev).manual_seed(Ca + Cout + H + mode)
+    Cin = Ca + Cb
+    Ho = 2 * H if mode == 2 else H
+    xa = torch.randn(B, Ca, H, H, device=dev, generator=g)
+    xb = torch.randn(B, Cb, H, H, device=dev, generator=g) if Cb else None
+    w = torch.randn(Cout, Cin, 3, 3, device=dev, generator=g) * 0.05
+    bias = torch.randn(Cout, device=dev, generator=g)
+    gn = torch.randn(B, Cin, 2, device=dev, generator=g) * 0.5 if act else None
+    np_ = lib.ertd_conv2d_gn_parts(Ca, Cb, Cout, 3, mode, act, 0, B, H)
+    assert np_ > 0
+    assert lib.ertd_conv2d_gn_parts(Ca, Cb, 1, 3, 0, act, 0, B, H) == 0     # conv_out: none
+    n = lib.ertd_conv2d_workspace_bytes(Cin, Cout, 3, 0, B, H, mode)
+    ws = torch.empty(n, dtype=torch.uint8, device=dev)
+    ref = torch.empty(B, Cout, Ho, Ho, device=dev)
+    args = (xa.data_ptr(), Ca, None if xb is None else xb.data_ptr(), Cb, B, H)
+    tail = (Cout, 3, mode, None if gn is None else gn.data_ptr(), act, None, 0, None)
+    assert lib.ertd_conv2d(*args, w.data_ptr(), bias.data_ptr(), *tail, ref.data_ptr(), 0, ws.data_ptr(), n,
+                           s) == 0
+    out = torch.empty_like(ref)
+    parts = torch.empty(B, Cout, np_, 2, device=dev)
+    assert lib.ertd_conv2d_gn(*args, w.data_ptr(), bias.data_ptr(), *tail, out.data_ptr(), 0, ws.data_ptr(),
+                              n, parts.data_ptr(), np_, s) == 0
+    assert torch.equal(out, ref)
+    out2, parts2 = torch.empty_like(ref), torch.empty_like(parts)
+    assert lib.ertd_conv2d_run_gn(*args, bias.data_ptr(), *tail, out2.data_ptr(), 0, ws.data_ptr(), n,
+                                  parts2.data_ptr(), np_, s) == 0
+    assert torch.equal(out2, ref) and torch.equal(parts2, parts)
+    assert lib.ertd_conv2d_run_gn(*args, bias.data_ptr(), *tail, out2.data_ptr(), 0, ws.data_ptr(), n,
+                                  parts2.data_ptr(), np_ + 1, s) != 0           # wrong part count
+    groups = 32
+    gam = 1 + 0.1 * torch.randn(Cout, device=dev, generator=g)
+    bet = 0.1 * torch.randn(Cout, device=dev, generator=g)
+    ss, mr = torch.empty(B, Cout, 2, device=dev), torch.empty(B, groups, 2, device=dev)
+    assert lib.ertd_group_norm_finalize(parts.data_ptr(), np_, Cout, None, 0, 0, B, Ho * Ho, groups,
+                                        gam.data_ptr(), bet.data_ptr(), ss.data_ptr(), mr.data_ptr(), s) == 0
+    ss_r, mr_r = torch.empty_like(ss), torch.empty_like(mr)
+    assert lib.ertd_gn_stats_mr(ref.data_ptr(), Cout, None, 0, B, Ho * Ho, groups, gam.data_ptr(),
+                                bet.data_ptr(), ss_r.data_ptr(), mr_r.data_ptr(), s) == 0
+    e = max(_rel(ss, ss_r), _rel(mr, mr_r))
+    record_error(f"conv2d_gn_parts_{Cin}_{Cout}_{Ho}_m{mode}", e)
+    assert e < 1e-6, e
