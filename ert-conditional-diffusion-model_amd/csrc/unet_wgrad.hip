@@ -521,6 +521,159 @@ hipError_t launch_wg1(const W1Plan& pl, const float* dy, const float* x, int Ca,
   return hipGetLastError();
 }
 
+#ifndef WGT_ON
+#define WGT_ON 1  // 1: 3x3 weight gradients with a single-channel side on wgt_kernel (0: implicit GEMM; A/B)
+#endif
+
+// The convs with one input or one output channel (conv_in: Cin = 1, conv_out:
+// Cout = 1) leave 63 of 64 rows of the implicit GEMM's MFMA tile idle.  Their
+// weight gradient dW[c][ky][kx] = sum_{b,y,x} P[y][x] Q[y + ky - 1][x + kx - 1]
+// (conv_out: P = dy, Q = act(x[c]); conv_in: P = dy[c], Q = x) is C x 9 sums
+// over B H W terms: one workgroup per (sample, band of R rows) stages P's R rows
+// and Q's R + 2 rows (zero halo, the activation applied) in LDS, thread (c, ky)
+// walks the band's pixels in order keeping the three kx sums (a sliding window:
+// one Q read per pixel), and the per-band partials are summed in a fixed order.
+struct WtArgs {
+  const float* dy;
+  const float* x;
+  const float2* gn;   // (B, Cin) {scale, shift} of the activation on x, or null
+  int C, H, R, cin1;  // C: the multi-channel side; cin1: conv_in (Cin = 1), else conv_out
+  float* P;           // (B H / R, C * 9)
+};
+
+template <int ACT>
+__global__ __launch_bounds__(256) void wgt_kernel(WtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = a.H, W = a.H, R = a.R, C = a.C, QW = W + 2, W4 = W / 4;
+  // odd per-channel strides: the lanes of a wave (21 channels x 3 ky) read
+  // distinct banks (an even multiple of 32 put every channel on one bank)
+  const int PS = R * W + 1, QS = (R + 2) * QW + 1;
+  const int nband = H / R;
+  const int b = blockIdx.x / nband, y0 = (blockIdx.x - b * nband) * R;
+  const int CP = a.cin1 ? C : 1, CQ = a.cin1 ? 1 : C;
+  float* Ps = sm;                     // [CP][PS]: R rows of W
+  float* Qs = sm + CP * PS;           // [CQ][QS]: R + 2 rows of W + 2
+  const int tid = threadIdx.x;
+  constexpr int NB = 8;   // float4 loads in flight per lane while staging
+  const int np4 = CP * R * W4;
+  for (int i0 = tid; i0 < np4; i0 += 256 * NB) {
+    f32x4 v[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = i0 + 256 * u, c = i / (R * W4), rem = i - c * (R * W4);
+      v[u] = i < np4 ? *reinterpret_cast<const f32x4*>(a.dy + ((size_t)b * CP + c) * H * W + (size_t)y0 * W +
+                                                      4 * rem)
+                     : f32x4{};
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = i0 + 256 * u, c = i / (R * W4), rem = i - c * (R * W4);
+      if (i < np4) {
+        float* p = Ps + c * PS + 4 * rem;
+        p[0] = v[u][0]; p[1] = v[u][1]; p[2] = v[u][2]; p[3] = v[u][3];
+      }
+    }
+  }
+  // Q: halo columns zero, rows outside the image zero
+  for (int i = tid; i < CQ * (R + 2); i += 256) {
+    const int c = i / (R + 2), r = i - c * (R + 2);
+    Qs[c * QS + r * QW] = 0.f;
+    Qs[c * QS + r * QW + W + 1] = 0.f;
+  }
+  const int nq4 = CQ * (R + 2) * W4;
+  for (int i0 = tid; i0 < nq4; i0 += 256 * NB) {
+    f32x4 v[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = i0 + 256 * u, c = i / ((R + 2) * W4), rem = i - c * ((R + 2) * W4);
+      const int r = rem / W4, x4 = rem - r * W4, y = y0 - 1 + r;
+      v[u] = i < nq4 && y >= 0 && y < H
+                 ? *reinterpret_cast<const f32x4*>(a.x + ((size_t)b * CQ + c) * H * W + (size_t)y * W + 4 * x4)
+                 : f32x4{};
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = i0 + 256 * u, c = i / ((R + 2) * W4), rem = i - c * ((R + 2) * W4);
+      const int r = rem / W4, x4 = rem - r * W4, y = y0 - 1 + r;
+      if (i < nq4) {
+        f32x4 t = v[u];
+        if constexpr (ACT != ACT_NONE) {
+          if (y >= 0 && y < H) t = wg_act<ACT>(t, a.gn[(size_t)b * CQ + c]);   // padding stays zero
+        }
+        float* q = Qs + c * QS + r * QW + 1 + 4 * x4;
+        q[0] = t[0]; q[1] = t[1]; q[2] = t[2]; q[3] = t[3];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 3 * C) {
+    const int c = tid / 3, ky = tid - 3 * c;
+    const float* pr = Ps + (a.cin1 ? c : 0) * PS;
+    const float* qr = Qs + (a.cin1 ? 0 : c) * QS + ky * QW;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const float* pp = pr + r * W;
+      const float* qq = qr + r * QW;
+      float q0 = qq[0], q1 = qq[1];
+#pragma unroll 8
+      for (int x = 0; x < W; ++x) {
+        const float q2 = qq[x + 2], p = pp[x];
+        s0 = fmaf(p, q0, s0);
+        s1 = fmaf(p, q1, s1);
+        s2 = fmaf(p, q2, s2);
+        q0 = q1;
+        q1 = q2;
+      }
+    }
+    float* o = a.P + (size_t)blockIdx.x * C * 9 + c * 9 + 3 * ky;
+    o[0] = s0;
+    o[1] = s1;
+    o[2] = s2;
+  }
+}
+
+// rows per band (0: not this path): the largest of 8 / 4 / 2 dividing H whose
+// staging fits 100 KB of LDS (two workgroups per CU; ERTD_WGT_LDSKB in the diag
+// build: conv_out at 64x64 29.1 us with 4-row bands in 102 KB, 24.7 with 2-row)
+int wgt_rows(int Cin, int Cout, int Cb, int H, int ks, int mode) {
+  if (!WGT_ON || ks != 3 || mode != MODE_S1 || Cb != 0 || H < 4 || H % 4 || H > 128) return 0;
+  const bool cin1 = Cin == 1 && Cout >= 1 && Cout <= 64, cout1 = Cout == 1 && Cin >= 2 && Cin <= 64;
+  if (!cin1 && !cout1) return 0;
+  const int C = cin1 ? Cout : Cin, CP = cin1 ? C : 1, CQ = cin1 ? 1 : C;
+  const size_t cap = (size_t)ERTD_KNOB("WGT_LDSKB", 100) * 1024;
+  for (int R = 8; R >= 2; R /= 2)
+    if (H % R == 0 && (size_t)(CP * (R * H + 1) + CQ * ((R + 2) * (H + 2) + 1)) * sizeof(float) <= cap)
+      return R;
+  return 0;
+}
+
+size_t wgt_part_floats(int Cin, int Cout, int B, int H, int R) {
+  return (size_t)B * (H / R) * std::max(Cin, Cout) * 9;
+}
+
+hipError_t launch_wgt(const float* dy, const float* x, int Cin, int Cout, int B, int H, int R, const float* gn,
+                      int act, float* part, hipStream_t s) {
+  const bool cin1 = Cin == 1;
+  WtArgs a{dy, x, (const float2*)gn, cin1 ? Cout : Cin, H, R, cin1 ? 1 : 0, part};
+  const int C = a.C, CP = cin1 ? C : 1, CQ = cin1 ? 1 : C;
+  const size_t lds = (size_t)(CP * (R * H + 1) + CQ * ((R + 2) * (H + 2) + 1)) * sizeof(float);
+  const unsigned nwg = (unsigned)(B * (H / R));
+  if (act == ACT_GN_SILU) {
+    static std::atomic<unsigned long long> at{0};
+    set_max_lds_once((const void*)wgt_kernel<ACT_GN_SILU>, 160 * 1024, at);
+    wgt_kernel<ACT_GN_SILU><<<nwg, 256, lds, s>>>(a);
+  } else if (act == ACT_GN) {
+    static std::atomic<unsigned long long> at{0};
+    set_max_lds_once((const void*)wgt_kernel<ACT_GN>, 160 * 1024, at);
+    wgt_kernel<ACT_GN><<<nwg, 256, lds, s>>>(a);
+  } else {
+    static std::atomic<unsigned long long> at{0};
+    set_max_lds_once((const void*)wgt_kernel<ACT_NONE>, 160 * 1024, at);
+    wgt_kernel<ACT_NONE><<<nwg, 256, lds, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
 int n_cu() {
   static int v = [] {
     int dev = 0, n = 0;
@@ -607,7 +760,9 @@ size_t ertd_conv_wgrad_ws_bytes(int Cin, int Cout, int B, int H, int ks, int mod
   // the Winograd path (3x3 stride 1, unet_wgrad_wino.hip) and the 1x1 GEMM where eligible
   W1Plan w1;
   const size_t f1 = wg1_plan(Cin, Cout, B, H, ks, mode, ACT_NONE, &w1) ? w1.part_floats : 0;
-  return std::max({p.part_floats, f1, wgrad_wino_ws_floats(Cin, Cout, B, H, ks, mode)}) * sizeof(float);
+  const int rt = wgt_rows(Cin, Cout, 0, H, ks, mode);
+  const size_t ft = rt ? wgt_part_floats(Cin, Cout, B, H, rt) : 0;
+  return std::max({p.part_floats, f1, ft, wgrad_wino_ws_floats(Cin, Cout, B, H, ks, mode)}) * sizeof(float);
 }
 
 int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, int Cb, int B, int H,
@@ -626,6 +781,14 @@ int ertd_conv_wgrad(const float* dy, const float* x, int Ca, const float* x2, in
     return e == hipSuccess ? ERTD_OK : (int)e;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (const int rt = wgt_rows(Ca + Cb, Cout, Cb, H, ks, mode)) {
+    const size_t nf = wgt_part_floats(Ca + Cb, Cout, B, H, rt);
+    if (nf * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+    hipError_t e = launch_wgt(dy, x, Ca + Cb, Cout, B, H, rt, gn, act, (float*)ws, s);
+    if (e != hipSuccess) return (int)e;
+    e = reduce_parts((const float*)ws, B * (H / rt), (size_t)Cout * (Ca + Cb) * 9, dw, accumulate, s);
+    return e == hipSuccess ? ERTD_OK : (int)e;
+  }
   W1Plan w1;
   if (wg1_plan(Ca + Cb, Cout, B, H, ks, mode, act, &w1)) {
     if (w1.part_floats * sizeof(float) > ws_bytes) return ERTD_ENOSPC;

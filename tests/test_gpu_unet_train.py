@@ -176,8 +176,11 @@ def test_unet_train_rejects_bf16(cuda_dev):
     (128, 64, 128, 32, 3, 0, 2),   # Winograd wgrad tile 128 co x 64 ci (Cin % 128 != 0)
     (64, 64, 64, 32, 3, 0, 2),     # ... 64 co x 128 ci
     (256, 0, 256, 16, 3, 0, 2),
-    (1, 0, 32, 32, 3, 0, 2),       # conv_in: Cin = 1 (masked ci tile)
-    (32, 0, 1, 32, 3, 0, 2),       # conv_out: Cout = 1 (masked co tile)
+    (1, 0, 32, 32, 3, 0, 2),       # conv_in: Cin = 1 (single-channel-side kernel)
+    (32, 0, 1, 32, 3, 0, 2),       # conv_out: Cout = 1
+    (1, 0, 64, 64, 3, 0, 32),      # conv_in at the train batch
+    (1, 0, 64, 16, 3, 0, 3),       # 16x16: 8-row bands
+    (1, 0, 80, 32, 3, 0, 2),       # Cout > 64: the implicit GEMM's masked tile
     (48, 0, 40, 128, 3, 0, 1),     # ragged channel tiles, 128x128 rows
     (64, 0, 64, 64, 3, 1, 2),      # Downsample (stride 2): 64 -> 32
     (128, 0, 128, 32, 3, 1, 2),    # 32 -> 16
@@ -265,6 +268,8 @@ def test_conv_wgrad_fused_bias(Ca, Cb, Cout, H, mode, B, cuda_dev):
     (64, 0, 64, 64, 3, 1, 2),      # conv1 / conv2 / conv_out: GroupNorm + SiLU staged
     (96, 32, 64, 32, 3, 1, 2),     # decoder conv1 on a concat
     (256, 0, 768, 16, 1, 2, 2),    # attention qkv: GroupNorm only
+    (64, 0, 1, 64, 3, 1, 32),      # conv_out at the train batch (single-output-channel kernel)
+    (32, 0, 1, 128, 3, 1, 2),      # ... 128x128 rows (2-row bands)
 ])
 def test_conv_wgrad_fused_activation(Ca, Cb, Cout, H, ks, act, B, cuda_dev):
     """dL/dW of conv(act(x)) with act(v) = v * scale + shift (+ SiLU) applied by the
