@@ -409,14 +409,26 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(SmallGemm g) {
   const float* A = g.A + bt * g.a_b;
   const float* Bm = g.Bm + bt * g.b_b;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < g.K; k0 += 32) {
+  // the next 32-k tile is loaded into registers during this one's FMAs (the
+  // small grids here leave a dependent load per tile latency-bound)
+  float ra[4], rb[4];
+  auto gload = [&](int k0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ii = ty + 8 * r;
-      As[ii][tx] = (i0 + ii < g.I && k0 + tx < g.K) ? A[(i0 + ii) * g.a_i + (k0 + tx) * g.a_k] : 0.f;
-      Bs[ii][tx] = (k0 + ii < g.K && j0 + tx < g.J) ? Bm[(k0 + ii) * g.b_k + (j0 + tx) * g.b_j] : 0.f;
+      ra[r] = (i0 + ii < g.I && k0 + tx < g.K) ? A[(i0 + ii) * g.a_i + (k0 + tx) * g.a_k] : 0.f;
+      rb[r] = (k0 + ii < g.K && j0 + tx < g.J) ? Bm[(k0 + ii) * g.b_k + (j0 + tx) * g.b_j] : 0.f;
+    }
+  };
+  gload(0);
+  for (int k0 = 0; k0 < g.K; k0 += 32) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      As[ty + 8 * r][tx] = ra[r];
+      Bs[ty + 8 * r][tx] = rb[r];
     }
     __syncthreads();
+    if (k0 + 32 < g.K) gload(k0 + 32);
 #pragma unroll 8
     for (int k = 0; k < 32; ++k) {
       const float bv = Bs[k][tx];
