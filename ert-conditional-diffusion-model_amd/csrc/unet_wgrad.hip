@@ -707,9 +707,11 @@ bool plan_of(int Cin, int Cout, int B, int H, int ks, int mode, Plan* p) {
   p->ntiles = p->nco * p->nci;
   p->nchunks = B * (Ho / p->R);
   if (ks == 1 && Ho * Ho < PXC) return false;
-  // about 4 workgroups per CU, >= 4 chunks per range (measured optimum at
-  // U2 B=32 of the partial write + reduce traffic vs occupancy: tools/wgrad_sweep.sh)
-  static const int wpc = ERTD_KNOB("WGRAD_WPC", 4), min_cps = ERTD_KNOB("WGRAD_CPS", 4);
+  // about 4 workgroups per CU, >= 2 chunks per range (the partial write +
+  // reduce traffic vs occupancy; measured at U2 B=32 once the 3x3 stride-1 and
+  // 1x1 convs had left this kernel: >= 4 chunks gave the stride-2 convs 128
+  // workgroups, train step 10.19 -> 10.11 ms, tools/gpu_cps.sh)
+  static const int wpc = ERTD_KNOB("WGRAD_WPC", 4), min_cps = ERTD_KNOB("WGRAD_CPS", 2);
   const int want = (wpc * n_cu() + p->ntiles - 1) / p->ntiles;
   int cps = (p->nchunks + want - 1) / want;
   if (cps < min_cps) cps = min_cps;
