@@ -464,9 +464,11 @@ bool wgw_plan(int Cin, int Cout, int B, int H, WgwPlan* pl) {
   const int nq = T / 16;                         // 16-k blocks
 #if WGW_LDS
   const int base = NX * (Cout / (64 * pl->mb)) * (Cin / (64 * pl->nb));
-  static const int target = [] {                 // ERTD_WGW_TASKS: workgroup target (A/B)
-    const int v = ERTD_KNOB("WGW_TASKS", 512);
-    return v > 0 ? v : 512;
+  // ERTD_WGW_TASKS: workgroup target (A/B; U2 B=32 train step, tools/gpu_knobs.sh:
+  // 256 10.39, 320 10.21, 384 10.02-10.05, 448 10.05, 512 10.10-10.14 ms)
+  static const int target = [] {
+    const int v = ERTD_KNOB("WGW_TASKS", 384);
+    return v > 0 ? v : 384;
   }();
 #else
   const int base = NX * (Cout / 64) * (Cin / 64);
