@@ -366,10 +366,10 @@ class _K:
         _lib.check(self.lib.ertd_wgrad_gemm(dy.data_ptr(), col.data_ptr(), M, N, P, B, M * P, N * P,
                                             out.data_ptr(), 0, ws.data_ptr(), n, self.s), "wgrad_gemm")
 
-    def conv_input_grad(self, dy, w, mode, H, name=None):
+    def conv_input_grad(self, dy, w, mode, H, name=None, out=None, accumulate=False):
         """dL/dx (B, Cin, H, H) of y = conv(x) with weight w given dy: a conv of dy with
         w transposed and flipped (ertd_conv_input_grad; with a registry, the packing
-        of the step's batched pack)."""
+        of the step's batched pack); into `out` (+= with accumulate) when given."""
         Cout, Cin, ks, _ = w.shape
         B = dy.shape[0]
         n = self.lib.ertd_conv_input_grad_ws_bytes(Cin, Cout, B, H, ks, mode)
@@ -382,13 +382,15 @@ class _K:
             ws, packed = self.packs.get(("dgrad", name, B, H), n, describe, w)
         else:
             ws = self.ws(n)
-        dx = self.empty(B, Cin, H, H)
+        dx = self.empty(B, Cin, H, H) if out is None else out
+        acc = int(bool(accumulate) and out is not None)
         if packed:
-            _lib.check(self.lib.ertd_conv_input_grad_run(dy.data_ptr(), B, H, Cout, Cin, ks, mode, dx.data_ptr(), 0,
-                                                         ws.data_ptr(), ws.numel(), self.s), "conv_input_grad_run")
+            _lib.check(self.lib.ertd_conv_input_grad_run(dy.data_ptr(), B, H, Cout, Cin, ks, mode, dx.data_ptr(),
+                                                         acc, ws.data_ptr(), ws.numel(), self.s),
+                       "conv_input_grad_run")
         else:
             _lib.check(self.lib.ertd_conv_input_grad(dy.data_ptr(), B, H, w.data_ptr(), Cout, Cin, ks, mode,
-                                                     dx.data_ptr(), 0, ws.data_ptr(), ws.numel(), self.s),
+                                                     dx.data_ptr(), acc, ws.data_ptr(), ws.numel(), self.s),
                        "conv_input_grad")
         return dx
 
@@ -508,18 +510,9 @@ class _Grads:
             return buf, False
         return buf, True
 
-    def add(self, t, v, owned=False):
-        """dL/dt += v (v adopted as the buffer when it is the first and owned)."""
-        buf = self.g.get(id(t))
-        if buf is None and owned:
-            self.g[id(t)] = v
-            return
-        buf, acc = self.target(t)
-        self.k.elt(ELT_SCALE, v, out=buf, alpha=1.0, accumulate=acc)
-
 
 def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, gn=None, act=0,
-                   bias_grad=True, also_bias=None):
+                   bias_grad=True, also_bias=None, dx_into=None):
     """Gradients of y = conv(act(cat(xa, xb))) + bias: weight and bias grads into
     grads[name.weight / .bias] (bias_grad=False: the caller supplies the bias
     gradient; also_bias: a second conv fed the same dy whose bias gradient is the
@@ -544,7 +537,10 @@ def _conv_backward(k: _K, grads, name, w, xa, xb, dy, mode, x_needs_grad=True, g
     if not x_needs_grad:
         return None
     # input gradient: a conv of dY with the flipped, transposed weights
-    return k.conv_input_grad(dy, w, mode, xa.shape[2], name=name)
+    # (dx_into: a (buffer, accumulate) target, e.g. a gradient already holding
+    # the skip connection's contribution)
+    out, acc = dx_into if dx_into is not None else (None, False)
+    return k.conv_input_grad(dy, w, mode, xa.shape[2], name=name, out=out, accumulate=acc)
 
 
 def _encoder_pack(model: ConditionalUNet, k: _K, W):
@@ -713,8 +709,9 @@ def unet_train_backward(model: ConditionalUNet, tape, deps, need_x: bool = False
                 grads["norm_out.weight"], grads["norm_out.bias"] = dg, db
             elif kind in ("up", "down"):
                 mode = MODE_UP if kind == "up" else MODE_S2
-                dx = _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, mode)
-                G.add(d["x"], dx, owned=True)
+                # written (or accumulated, x is also a skip input) by the conv itself
+                _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, mode,
+                               dx_into=G.target(d["x"]))
             elif kind == "conv_in":
                 dx = _conv_backward(k, grads, n, W[n + ".weight"], d["x"], None, dy, MODE_S1,
                                     x_needs_grad=need_x)
