@@ -399,7 +399,15 @@ __global__ __launch_bounds__(256) void wgw_final_kernel(WgwArgs a, float* dw, in
     const size_t co = i / Cin;
     const int nb = a.T / 256;
     double s = 0.0;
-    for (int k = 0; k < nb; ++k) s += (double)a.BP[co * nb + k];
+    int k = 0;
+    for (; k + 8 <= nb; k += 8) {   // 8 loads in flight, added in order
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = a.BP[co * nb + k + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (double)t[j];
+    }
+    for (; k < nb; ++k) s += (double)a.BP[co * nb + k];
     db[co] = (float)s;
     if (db2) db2[co] = (float)s;
   }
