@@ -99,7 +99,7 @@ def parse():
     ap.add_argument("--no-unet-train", action="store_true", help="skip the U-Net train-step timing")
     ap.add_argument("--no-hbm-kernels", action="store_true",
                     help="skip the per-kernel GB/s of the HBM-bound U-Net kernels")
-    ap.add_argument("--unet-train-steps", type=int, default=5)
+    ap.add_argument("--unet-train-steps", type=int, default=30)
     ap.add_argument("--no-conv-kernels", action="store_true",
                     help="skip the per-conv-kernel timing (GB/s and TF/s vs roofline)")
     ap.add_argument("--no-strip-roofline", action="store_true")
@@ -432,7 +432,7 @@ def bench_conv_kernels(dev, B=64, reps=20):
     return out
 
 
-def bench_unet_train(dev, name="U2", B=32, steps=5, warmup=2, T=1000, rank=0, world=1):
+def bench_unet_train(dev, name="U2", B=32, steps=30, warmup=5, T=1000, rank=0, world=1):
     """The reference train step (:309-320) on the U-Net denoiser: q_sample, the
     HIP forward with saved activations, the hand-written HIP backward, MSE and
     the multi-tensor Adam kernel, fp32, batch B per GPU -- through
