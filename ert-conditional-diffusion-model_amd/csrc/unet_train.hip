@@ -409,33 +409,42 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(SmallGemm g) {
   const float* A = g.A + bt * g.a_b;
   const float* Bm = g.Bm + bt * g.b_b;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  // the next 32-k tile is loaded into registers during this one's FMAs (the
-  // small grids here leave a dependent load per tile latency-bound)
-  float ra[4], rb[4];
-  auto gload = [&](int k0) {
+  // 32-k tiles are loaded into a ring of 4 register slots, 3 tiles ahead of
+  // the FMAs (the small grids here -- 8 .. 86 workgroups -- leave each tile's
+  // first-touch HBM load latency-bound: one tile ahead still waited per tile)
+  constexpr int NS = 4;
+  float ra[NS][4], rb[NS][4];
+  auto gload = [&](float (&la)[4], float (&lb)[4], int k0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ii = ty + 8 * r;
-      ra[r] = (i0 + ii < g.I && k0 + tx < g.K) ? A[(i0 + ii) * g.a_i + (k0 + tx) * g.a_k] : 0.f;
-      rb[r] = (k0 + ii < g.K && j0 + tx < g.J) ? Bm[(k0 + ii) * g.b_k + (j0 + tx) * g.b_j] : 0.f;
+      la[r] = (i0 + ii < g.I && k0 + tx < g.K) ? A[(i0 + ii) * g.a_i + (k0 + tx) * g.a_k] : 0.f;
+      lb[r] = (k0 + ii < g.K && j0 + tx < g.J) ? Bm[(k0 + ii) * g.b_k + (j0 + tx) * g.b_j] : 0.f;
     }
   };
-  gload(0);
-  for (int k0 = 0; k0 < g.K; k0 += 32) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      As[ty + 8 * r][tx] = ra[r];
-      Bs[ty + 8 * r][tx] = rb[r];
-    }
-    __syncthreads();
-    if (k0 + 32 < g.K) gload(k0 + 32);
+  for (int sl = 0; sl < NS; ++sl)
+    if (32 * sl < g.K) gload(ra[sl], rb[sl], 32 * sl);
+  for (int k00 = 0; k00 < g.K; k00 += 32 * NS) {
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+      const int k0 = k00 + 32 * sl;
+      if (k0 >= g.K) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        As[ty + 8 * r][tx] = ra[sl][r];
+        Bs[ty + 8 * r][tx] = rb[sl][r];
+      }
+      __syncthreads();
+      if (k0 + 32 * NS < g.K) gload(ra[sl], rb[sl], k0 + 32 * NS);
 #pragma unroll 8
-    for (int k = 0; k < 32; ++k) {
-      const float bv = Bs[k][tx];
+      for (int k = 0; k < 32; ++k) {
+        const float bv = Bs[k][tx];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = fmaf(As[ty + 8 * r][k], bv, acc[r]);
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(As[ty + 8 * r][k], bv, acc[r]);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   float* C = g.C + bt * g.c_b;
 #pragma unroll
