@@ -1,3 +1,8 @@
+#!/bin/bash
+# Host-package A/B (diagnostic): the train tests, then tools/train_probe.py
+# alternating this tree's ertdiff package and a copy under variants/oldpy
+# (e.g. the package at an older commit: git show HEAD~1:... per file), both on
+# this tree's library (ERTD_PKG_PATH / ERTD_LIB_PATH).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_unet_train.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tr_tests.log 2>&1
