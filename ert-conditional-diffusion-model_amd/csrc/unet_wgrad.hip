@@ -521,6 +521,9 @@ hipError_t launch_wg1(const W1Plan& pl, const float* dy, const float* x, int Ca,
   return hipGetLastError();
 }
 
+#ifndef WGT_T
+#define WGT_T 512  // wgt_kernel threads: 512 splits each row between two threads (256: one; A/B)
+#endif
 #ifndef WGT_ON
 #define WGT_ON 1  // 1: 3x3 weight gradients with a single-channel side on wgt_kernel (0: implicit GEMM; A/B)
 #endif
@@ -542,7 +545,7 @@ struct WtArgs {
 };
 
 template <int ACT>
-__global__ __launch_bounds__(256) void wgt_kernel(WtArgs a) {
+__global__ __launch_bounds__(WGT_T) void wgt_kernel(WtArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int H = a.H, W = a.H, R = a.R, C = a.C, QW = W + 2, W4 = W / 4;
   // odd per-channel strides: the lanes of a wave (21 channels x 3 ky) read
@@ -556,18 +559,18 @@ __global__ __launch_bounds__(256) void wgt_kernel(WtArgs a) {
   const int tid = threadIdx.x;
   constexpr int NB = 8;   // float4 loads in flight per lane while staging
   const int np4 = CP * R * W4;
-  for (int i0 = tid; i0 < np4; i0 += 256 * NB) {
+  for (int i0 = tid; i0 < np4; i0 += WGT_T * NB) {
     f32x4 v[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int i = i0 + 256 * u, c = i / (R * W4), rem = i - c * (R * W4);
+      const int i = i0 + WGT_T * u, c = i / (R * W4), rem = i - c * (R * W4);
       v[u] = i < np4 ? *reinterpret_cast<const f32x4*>(a.dy + ((size_t)b * CP + c) * H * W + (size_t)y0 * W +
                                                       4 * rem)
                      : f32x4{};
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int i = i0 + 256 * u, c = i / (R * W4), rem = i - c * (R * W4);
+      const int i = i0 + WGT_T * u, c = i / (R * W4), rem = i - c * (R * W4);
       if (i < np4) {
         float* p = Ps + c * PS + 4 * rem;
         p[0] = v[u][0]; p[1] = v[u][1]; p[2] = v[u][2]; p[3] = v[u][3];
@@ -575,17 +578,17 @@ __global__ __launch_bounds__(256) void wgt_kernel(WtArgs a) {
     }
   }
   // Q: halo columns zero, rows outside the image zero
-  for (int i = tid; i < CQ * (R + 2); i += 256) {
+  for (int i = tid; i < CQ * (R + 2); i += WGT_T) {
     const int c = i / (R + 2), r = i - c * (R + 2);
     Qs[c * QS + r * QW] = 0.f;
     Qs[c * QS + r * QW + W + 1] = 0.f;
   }
   const int nq4 = CQ * (R + 2) * W4;
-  for (int i0 = tid; i0 < nq4; i0 += 256 * NB) {
+  for (int i0 = tid; i0 < nq4; i0 += WGT_T * NB) {
     f32x4 v[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int i = i0 + 256 * u, c = i / ((R + 2) * W4), rem = i - c * ((R + 2) * W4);
+      const int i = i0 + WGT_T * u, c = i / ((R + 2) * W4), rem = i - c * ((R + 2) * W4);
       const int r = rem / W4, x4 = rem - r * W4, y = y0 - 1 + r;
       v[u] = i < nq4 && y >= 0 && y < H
                  ? *reinterpret_cast<const f32x4*>(a.x + ((size_t)b * CQ + c) * H * W + (size_t)y * W + 4 * x4)
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(256) void wgt_kernel(WtArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int i = i0 + 256 * u, c = i / ((R + 2) * W4), rem = i - c * ((R + 2) * W4);
+      const int i = i0 + WGT_T * u, c = i / ((R + 2) * W4), rem = i - c * ((R + 2) * W4);
       const int r = rem / W4, x4 = rem - r * W4, y = y0 - 1 + r;
       if (i < nq4) {
         f32x4 t = v[u];
@@ -606,17 +609,22 @@ __global__ __launch_bounds__(256) void wgt_kernel(WtArgs a) {
     }
   }
   __syncthreads();
-  if (tid < 3 * C) {
-    const int c = tid / 3, ky = tid - 3 * c;
+  // thread (xh, c, ky): the half xh of every row (WGT_T = 512: two halves,
+  // their sums added in order below; 256: one)
+  constexpr int NH = WGT_T / 256;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  const int xh = tid / (WGT_T / NH), tl = tid - xh * (WGT_T / NH);
+  const int c = tl / 3, ky = tl - 3 * c;
+  if (tl < 3 * C) {
     const float* pr = Ps + (a.cin1 ? c : 0) * PS;
     const float* qr = Qs + (a.cin1 ? 0 : c) * QS + ky * QW;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    const int xw = W / NH, x0 = xh * xw;
     for (int r = 0; r < R; ++r) {
-      const float* pp = pr + r * W;
-      const float* qq = qr + r * QW;
+      const float* pp = pr + r * W + x0;
+      const float* qq = qr + r * QW + x0;
       float q0 = qq[0], q1 = qq[1];
 #pragma unroll 8
-      for (int x = 0; x < W; ++x) {
+      for (int x = 0; x < xw; ++x) {
         const float q2 = qq[x + 2], p = pp[x];
         s0 = fmaf(p, q0, s0);
         s1 = fmaf(p, q1, s1);
@@ -625,6 +633,18 @@ __global__ __launch_bounds__(256) void wgt_kernel(WtArgs a) {
         q1 = q2;
       }
     }
+  }
+  if constexpr (NH > 1) {
+    __syncthreads();   // the staging is free: the upper half's sums go through it
+    if (xh == 1 && tl < 3 * C) {
+      Ps[3 * tl] = s0; Ps[3 * tl + 1] = s1; Ps[3 * tl + 2] = s2;
+    }
+    __syncthreads();
+    if (xh == 0 && tl < 3 * C) {
+      s0 += Ps[3 * tl]; s1 += Ps[3 * tl + 1]; s2 += Ps[3 * tl + 2];
+    }
+  }
+  if (xh == 0 && tl < 3 * C) {
     float* o = a.P + (size_t)blockIdx.x * C * 9 + c * 9 + 3 * ky;
     o[0] = s0;
     o[1] = s1;
@@ -661,15 +681,15 @@ hipError_t launch_wgt(const float* dy, const float* x, int Cin, int Cout, int B,
   if (act == ACT_GN_SILU) {
     static std::atomic<unsigned long long> at{0};
     set_max_lds_once((const void*)wgt_kernel<ACT_GN_SILU>, 160 * 1024, at);
-    wgt_kernel<ACT_GN_SILU><<<nwg, 256, lds, s>>>(a);
+    wgt_kernel<ACT_GN_SILU><<<nwg, WGT_T, lds, s>>>(a);
   } else if (act == ACT_GN) {
     static std::atomic<unsigned long long> at{0};
     set_max_lds_once((const void*)wgt_kernel<ACT_GN>, 160 * 1024, at);
-    wgt_kernel<ACT_GN><<<nwg, 256, lds, s>>>(a);
+    wgt_kernel<ACT_GN><<<nwg, WGT_T, lds, s>>>(a);
   } else {
     static std::atomic<unsigned long long> at{0};
     set_max_lds_once((const void*)wgt_kernel<ACT_NONE>, 160 * 1024, at);
-    wgt_kernel<ACT_NONE><<<nwg, 256, lds, s>>>(a);
+    wgt_kernel<ACT_NONE><<<nwg, WGT_T, lds, s>>>(a);
   }
   return hipGetLastError();
 }
