@@ -228,10 +228,7 @@ int ertd_device_ok(void) {
 size_t ertd_workspace_bytes(int B, int L, int P, int T, int op) {
   (void)P;
   if (B < 1 || L < 1) return 0;
-  if (op == ERTD_OP_TRAIN) {
-    int offs[5];
-    return train_ws_floats(B, L, offs) * sizeof(float);
-  }
+  if (op == ERTD_OP_TRAIN) return train_ws_floats(B, L) * sizeof(float);
   return ws_layout(B, L, T, op, nullptr, nullptr);
 }
 
@@ -464,26 +461,23 @@ int ertd_train_forward(const ertd_weights* w, float* packed, const float* x, con
                        const float* noise, const float* alpha_bar, const int64_t* t,
                        const float* cond, int B, int L, const float* freq, float* eps_out,
                        void* ws, size_t ws_bytes, void* stream) {
-  if (!weights_ok(w) || !packed || !t || !cond || !freq || !ws || B < 1 || L < 1) return ERTD_EINVAL;
+  (void)packed;  // the train kernels read the parameters in place
+  if (!weights_ok(w) || !t || !cond || !freq || !ws || B < 1 || L < 1) return ERTD_EINVAL;
   if (!x && (!x0 || !noise || !alpha_bar)) return ERTD_EINVAL;
-  int offs[5];
-  if (train_ws_floats(B, L, offs) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
-  hipStream_t s = (hipStream_t)stream;
-  ERTD_TRY(launch_pack(*w, packed, s));
-  return rc(launch_train_forward(*w, packed, x, x0, noise, alpha_bar, t, cond, B, L, freq, eps_out,
-                                 (float*)ws, s));
+  if (train_ws_floats(B, L) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+  return rc(launch_train_forward(*w, x, x0, noise, alpha_bar, t, cond, B, L, freq, eps_out,
+                                 (float*)ws, (hipStream_t)stream));
 }
 
 int ertd_train_backward(const ertd_weights* w, const float* packed, const float* dout,
                         const float* noise, const float* cond, int B, int L, float* const* grads,
                         float* loss_out, float* dx_out, void* ws, size_t ws_bytes, void* stream) {
-  if (!weights_ok(w) || !packed || !cond || !grads_ok(grads) || !ws || B < 1 || L < 1)
-    return ERTD_EINVAL;
+  (void)packed;
+  if (!weights_ok(w) || !cond || !grads_ok(grads) || !ws || B < 1 || L < 1) return ERTD_EINVAL;
   if (!dout && (!noise || !loss_out)) return ERTD_EINVAL;
-  int offs[5];
-  if (train_ws_floats(B, L, offs) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
-  return rc(launch_train_backward(*w, packed, dout, noise, cond, B, L, grads, loss_out, dx_out,
-                                  (float*)ws, (hipStream_t)stream));
+  if (train_ws_floats(B, L) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+  return rc(launch_train_backward(*w, dout, noise, cond, B, L, grads, loss_out, dx_out, (float*)ws,
+                                  (hipStream_t)stream));
 }
 
 int ertd_adam(const ertd_weights* w, float* const* grads, float* const* exp_avg,
@@ -495,20 +489,55 @@ int ertd_adam(const ertd_weights* w, float* const* grads, float* const* exp_avg,
                         (hipStream_t)stream));
 }
 
+static int train_step_args_ok(const ertd_weights* w, const float* x0, const int64_t* t,
+                              const float* noise, const float* cond, const float* alpha_bar, int B,
+                              int L, const float* freq, float* const* grads, float* const* exp_avg,
+                              float* const* exp_avg_sq, float* loss_out, void* ws, size_t ws_bytes) {
+  if (!weights_ok(w) || !x0 || !t || !noise || !cond || !alpha_bar || !freq || !loss_out || !ws ||
+      B < 1 || L < 1)
+    return ERTD_EINVAL;
+  if (!grads_ok(grads) || !grads_ok(exp_avg) || !grads_ok(exp_avg_sq)) return ERTD_EINVAL;
+  if (train_ws_floats(B, L) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+  return ERTD_OK;
+}
+
 int ertd_train_step(const ertd_weights* w, float* packed, const float* x0, const int64_t* t,
                     const float* noise, const float* cond, const float* alpha_bar, int B, int L,
                     const float* freq, float* const* grads, float* const* exp_avg,
                     float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
                     float eps, float* loss_out, void* ws, size_t ws_bytes, void* stream) {
-  if (!x0 || !noise || !alpha_bar || !loss_out) return ERTD_EINVAL;
-  if (!grads_ok(exp_avg) || !grads_ok(exp_avg_sq) || step < 1) return ERTD_EINVAL;
-  int r = ertd_train_forward(w, packed, nullptr, x0, noise, alpha_bar, t, cond, B, L, freq,
-                             nullptr, ws, ws_bytes, stream);
+  (void)packed;
+  const int r = train_step_args_ok(w, x0, t, noise, cond, alpha_bar, B, L, freq, grads, exp_avg,
+                                   exp_avg_sq, loss_out, ws, ws_bytes);
   if (r != ERTD_OK) return r;
-  r = ertd_train_backward(w, packed, nullptr, noise, cond, B, L, grads, loss_out, nullptr, ws,
-                          ws_bytes, stream);
+  if (step < 1) return ERTD_EINVAL;
+  const TrainAdam adam{step, lr, beta1, beta2, eps, nullptr, nullptr, 0, 0, 0, 0, 0};
+  return rc(launch_train_step(*w, x0, t, noise, cond, alpha_bar, B, L, freq, grads, exp_avg,
+                              exp_avg_sq, adam, loss_out, (float*)ws, (hipStream_t)stream));
+}
+
+int ertd_adam_table(int step_first, int n, float lr, float beta1, float beta2, float eps,
+                    float* out) {
+  if (!out || step_first < 1 || n < 1) return ERTD_EINVAL;
+  adam_table_host(step_first, n, lr, beta1, beta2, eps, out);
+  return ERTD_OK;
+}
+
+int ertd_train_step_dev(const ertd_weights* w, const float* x0, int64_t* t, float* noise,
+                        const float* cond, const float* alpha_bar, int B, int L, const float* freq,
+                        float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                        int* step_dev, const float* adam_table, int table_first, int table_len,
+                        int draw, int T, uint64_t seed, float* loss_out, void* ws, size_t ws_bytes,
+                        void* stream) {
+  const int r = train_step_args_ok(w, x0, t, noise, cond, alpha_bar, B, L, freq, grads, exp_avg,
+                                   exp_avg_sq, loss_out, ws, ws_bytes);
   if (r != ERTD_OK) return r;
-  return ertd_adam(w, grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, stream);
+  if (!step_dev || !adam_table || table_first < 1 || table_len < 1) return ERTD_EINVAL;
+  if (draw && T < 1) return ERTD_EINVAL;
+  const TrainAdam adam{0, 0.f, 0.f, 0.f, 0.f, adam_table, step_dev, table_first, table_len, seed,
+                       draw ? 1 : 0, T};
+  return rc(launch_train_step(*w, x0, t, noise, cond, alpha_bar, B, L, freq, grads, exp_avg,
+                              exp_avg_sq, adam, loss_out, (float*)ws, (hipStream_t)stream));
 }
 
 }  // extern "C"

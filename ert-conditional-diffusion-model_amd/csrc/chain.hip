@@ -440,8 +440,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
 #pragma unroll 1
     for (int u = 0; u < ns; ++u) {
       const int zu = opaque0(), tu = opaque_tid();
-      enc_strip_fp32<false>(sm.enc, packed + zu, w.enc0_b + zu, w.enc2_b + zu, a.cond, a.cstride, a.L, L1, L2, b,
-                            cond_row(b, a.ncond), s0 + u, nullptr, nullptr, tu);
+      enc_strip_fp32(sm.enc, packed + zu, w.enc0_b + zu, w.enc2_b + zu, a.cond, a.cstride, a.L, L1, L2, b,
+                     cond_row(b, a.ncond), s0 + u, tu);
       if (tid < C2) sm.keep[u][tid] = sm.enc.red[0][tid] + sm.enc.red[1][tid];
     }
     WACC(2, wt1_);

@@ -40,17 +40,15 @@ __device__ __forceinline__ void conv1_tile(f32x16& acc, const float (&a1)[STEPS1
 // One strip (member b, conv2 outputs [strip*J, strip*J + J)) by the calling
 // 256-thread workgroup: leaves the 64 channel sums in sm.red[0][c] + sm.red[1][c]
 // (after a closing barrier).  tid = threadIdx.x (a persistent caller passes an
-// opaque copy so the per-lane addresses are not hoisted out of its item loop).  TRAIN additionally stores what the backward needs
-// (train.hip): the conv1 activations a1 (B,32,L1) at the conv1 positions this
-// strip owns, i in [2*j0, 2*j0 + 2J), and the conv2 ReLU mask m2 (B,64,L2) as bytes.
-template <bool TRAIN>
+// opaque copy so the per-lane addresses are not hoisted out of its item loop).
+// The training forward (train.hip enc_train_kernel) runs the same body on the
+// raw weights and also stores the activations its backward reads.
 __device__ __forceinline__ void enc_strip_fp32(EncSmem& sm, const float* __restrict__ packed,
                                                const float* __restrict__ b1,
                                                const float* __restrict__ b2,
                                                const float* __restrict__ cond, long long cstride,
                                                int L, int L1, int L2, int b, int crow, int strip,
-                                               float* __restrict__ a1out,
-                                               unsigned char* __restrict__ m2out, int tid) {
+                                               int tid) {
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
   const int j0 = strip * J;
@@ -93,15 +91,6 @@ __device__ __forceinline__ void enc_strip_fp32(EncSmem& sm, const float* __restr
     }
   }
   __syncthreads();
-  if constexpr (TRAIN) {  // owned conv1 positions i = 2*j0 + r, r < 2J  (p = r + 1)
-    float* a1b = a1out + (size_t)b * C1 * L1;
-    for (int idx = tid; idx < C1 * 2 * J; idx += 256) {
-      const int c = idx / (2 * J), r = idx - c * (2 * J);
-      const int i = 2 * j0 + r;
-      if (i < L1) a1b[(size_t)c * L1 + i] = (r & 1) ? sm.E[c][(r + 1) >> 1] : sm.O[c][r >> 1];
-    }
-  }
-
   // ---- conv2 + bias + ReLU + masked column sum
   {
     const int qt = wave & 1, ot = wave >> 1;
@@ -132,9 +121,6 @@ __device__ __forceinline__ void enc_strip_fp32(EncSmem& sm, const float* __restr
       const float z = acc[r] + bias;
       const float v = fmaxf(z, 0.f);
       sum += valid ? v : 0.f;
-      if constexpr (TRAIN) {
-        if (valid) m2out[((size_t)b * C2 + o) * L2 + j0 + qq] = z > 0.f ? 1 : 0;
-      }
     }
     sum += __shfl_xor(sum, 32);
     if (h == 0) sm.red[qt][o] = sum;

@@ -109,14 +109,21 @@ __global__ __launch_bounds__(256) void pack_w2b_kernel(ertd_weights w, float* __
   packed[PACK_W2B + idx] = w.enc2_w[(o * C1 + c) * 3 + kk];
 }
 
-// only the encoder conv regions (fp32 + bf16 fragments, W2B): what the encoder's
-// train-mode forward / backward read (the U-Net train step's condition encoder)
+// The U-Net train step's condition encoder (unet_train.hip): its train-mode
+// forward / backward (train.hip) read the conv weights in their own layout, so
+// the "packing" is a copy of the two tensors, W1 (32,14,3) at packed[0] and
+// W2 (64,32,3) at packed[ENC_RAW_W2], taken once per tape: a second forward
+// before that tape's backward must not change what the backward reads.
+__global__ __launch_bounds__(256) void copy_encoder_convs_kernel(const float* __restrict__ w0,
+                                                                 const float* __restrict__ w2,
+                                                                 float* __restrict__ packed) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < C1 * K1) packed[i] = w0[i];
+  else if (i < C1 * K1 + C2 * K2) packed[i] = w2[i - C1 * K1];
+}
+
 hipError_t launch_pack_encoder_convs(const float* w0, const float* w2, float* packed, hipStream_t s) {
-  ertd_weights w{};
-  w.enc0_w = w0;
-  w.enc2_w = w2;
-  pack_kernel<<<(PACK_TOTAL + 255) / 256, 256, 0, s>>>(w, packed);
-  pack_w2b_kernel<<<W2B_FLOATS / 256, 256, 0, s>>>(w, packed);
+  copy_encoder_convs_kernel<<<(C1 * K1 + C2 * K2 + 255) / 256, 256, 0, s>>>(w0, w2, packed);
   return hipGetLastError();
 }
 
@@ -134,29 +141,25 @@ hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // Optionally (tr.V != null) block number nstrip computes the time row v(tr.t)
 // for the faithful sampler's next head launch (time_row_lean: few registers).
-template <bool TRAIN>
 __global__ __launch_bounds__(256) void enc_fp32_kernel(const float* __restrict__ packed,
                                                        const float* __restrict__ b1,
                                                        const float* __restrict__ b2,
                                                        const float* __restrict__ cond,
                                                        long long cstride, int L, int L1, int L2,
                                                        int S, float* __restrict__ partial,
-                                                       float* __restrict__ a1out,
-                                                       unsigned char* __restrict__ m2out,
                                                        int nstrip, TimeRowArgs tr, int ncond) {
   __shared__ EncSmem sm;
   const int tid = threadIdx.x;
-  if (!TRAIN && (int)blockIdx.x >= nstrip) {
+  if ((int)blockIdx.x >= nstrip) {
     float* f = &sm.X[0][0][0];  // e[128] | te[128] | part[2][128]
     time_row_lean(tr.w, packed, tr.freq, tr.t, tr.V + (size_t)tr.t * H, f, f + H,
                   reinterpret_cast<float(*)[H]>(f + 2 * H), tid);
     return;
   }
   const int b = blockIdx.x / S, strip = blockIdx.x - b * S;
-  enc_strip_fp32<TRAIN>(sm, packed, b1, b2, cond, cstride, L, L1, L2, b, cond_row(b, ncond), strip, a1out,
-                        m2out, tid);
+  enc_strip_fp32(sm, packed, b1, b2, cond, cstride, L, L1, L2, b, cond_row(b, ncond), strip, tid);
   if (tid < C2) partial[((size_t)b * S + strip) * C2 + tid] = sm.red[0][tid] + sm.red[1][tid];
-  if (!TRAIN && tr.V) {
+  if (tr.V) {
     // Warm this XCD's L2 with a slice of the weights the next head_step reads
     // (W3T, the cond columns of W0T, the two step images: ~134 KB).  Blocks
     // b, b+8, ... share an XCD under the observed round-robin placement (a
@@ -299,8 +302,8 @@ hipError_t launch_encoder_strips(const float* packed, const float* b1, const flo
   if (precision == ERTD_PREC_BF16)
     enc_bf16_kernel<<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S, partial, ncond);
   else
-    enc_fp32_kernel<false><<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S,
-                                                 partial, nullptr, nullptr, B * S, TimeRowArgs{}, ncond);
+    enc_fp32_kernel<<<grid, 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1, L2, S, partial, B * S,
+                                         TimeRowArgs{}, ncond);
   return hipGetLastError();
 }
 
@@ -314,18 +317,8 @@ hipError_t launch_encoder_strips_t(const float* packed, const float* b1, const f
     return launch_time_table(tr.w, packed, tr.freq, tr.t, 1, tr.V, s);
   }
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
-  enc_fp32_kernel<false><<<dim3((unsigned)(B * S + 1)), 256, 0, s>>>(
-      packed, b1, b2, cond, cstride, L, L1, L2, S, partial, nullptr, nullptr, B * S, tr, ncond);
-  return hipGetLastError();
-}
-
-hipError_t launch_encoder_train(const float* packed, const float* b1, const float* b2,
-                                const float* cond, int B, int L, float* partial, float* a1,
-                                unsigned char* m2, hipStream_t s) {
-  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
-  enc_fp32_kernel<true><<<dim3((unsigned)(B * S)), 256, 0, s>>>(
-      packed, b1, b2, cond, (long long)CIN * L, L, L1, L2, S, partial, a1, m2, B * S,
-      TimeRowArgs{}, 0);
+  enc_fp32_kernel<<<dim3((unsigned)(B * S + 1)), 256, 0, s>>>(packed, b1, b2, cond, cstride, L, L1,
+                                                               L2, S, partial, B * S, tr, ncond);
   return hipGetLastError();
 }
 

@@ -197,22 +197,14 @@ constexpr int W2L_FLOATS = 64 * W2L_PITCH;
 constexpr int PACKED_FLOATS_ALL = PACK_W2L + W2L_FLOATS;
 
 hipError_t launch_pack(const ertd_weights& w, float* packed, hipStream_t s);
+// the U-Net train step's encoder weights: W1 raw at packed[0], W2 raw at packed[ENC_RAW_W2]
+constexpr int ENC_RAW_W2 = C1 * K1;
 hipError_t launch_pack_encoder_convs(const float* w0, const float* w2, float* packed, hipStream_t s);
-hipError_t launch_encoder_train(const float* packed, const float* b1, const float* b2,
-                                const float* cond, int B, int L, float* partial, float* a1,
-                                unsigned char* m2, hipStream_t s);
 // ncond > 0: member b reads condition row b % ncond (a many-condition launch,
 // ertd_sample_conditions); 0: row b
 hipError_t launch_encoder_strips(const float* packed, const float* b1, const float* b2,
                                  const float* cond, long long cstride, int B, int L,
                                  int precision, float* partial, hipStream_t s, int ncond = 0);
-// conv part of the encoder backward given g = dL/d(pool mean) / L2 (B, 64)
-// (train.hip; the U-Net train step)
-size_t encoder_bwd_ws_floats(int B, int L);
-hipError_t launch_encoder_conv_backward(const float* packed, const float* cond, const float* a1,
-                                        const unsigned char* m2, const float* g, int B, int L,
-                                        float* ws, float* dw1, float* db1, float* dw2, float* db2,
-                                        hipStream_t s);
 // Same, plus one extra block computing the time row v(t) = W0t.relu(Wt.e(t)+bt)
 // into V[t] (faithful sampler: the row the next head_step launch consumes).
 // Member b of a many-condition launch (ertd_sample_conditions): realisation
@@ -300,18 +292,44 @@ int faithful_chain_grid(int B, int S);
 hipError_t launch_zero_words(unsigned* p, size_t n, hipStream_t s);
 hipError_t launch_faithful_chain(const ertd_weights& w, const float* packed,
                                  const FaithfulChainArgs& a, int grid, hipStream_t s);
-// train.hip
-size_t train_ws_floats(int B, int L, int* offs);
-hipError_t launch_train_forward(const ertd_weights& w, const float* packed, const float* x_in,
-                                const float* x0, const float* noise, const float* alpha_bar,
-                                const int64_t* t, const float* cond, int B, int L,
-                                const float* freq, float* eps_out, float* ws, hipStream_t s);
-hipError_t launch_train_backward(const ertd_weights& w, const float* packed, const float* dout,
-                                 const float* noise, const float* cond, int B, int L,
-                                 float* const* grads, float* loss_out, float* dx_out, float* ws,
-                                 hipStream_t s);
+// train.hip (every kernel reads the parameters of w in place: no packing)
+size_t train_ws_floats(int B, int L);
+// Adam hyper-parameters of a train step: host scalars (table == nullptr), or
+// the device step counter *step_dev (advanced by the step itself) indexing a
+// table of adam_table_host() entries for steps [table_first, table_first + table_len)
+// draw != 0 (with step_dev): the step draws t ~ U{0..T-1} and noise ~ N(0,1)
+// itself (Philox keyed (seed, member, step)) into the t / noise buffers
+struct TrainAdam {
+  int step; float lr, beta1, beta2, eps;
+  const float* table; int* step_dev; int table_first, table_len;
+  uint64_t seed; int draw; int T;
+};
+constexpr int ADAM_TABLE_FLOATS = 6;  // floats per step entry
+void adam_table_host(int step_first, int n, float lr, float beta1, float beta2, float eps, float* out);
+hipError_t launch_train_forward(const ertd_weights& w, const float* x_in, const float* x0,
+                                const float* noise, const float* alpha_bar, const int64_t* t,
+                                const float* cond, int B, int L, const float* freq, float* eps_out,
+                                float* ws, hipStream_t s);
+hipError_t launch_train_backward(const ertd_weights& w, const float* dout, const float* noise,
+                                 const float* cond, int B, int L, float* const* grads,
+                                 float* loss_out, float* dx_out, float* ws, hipStream_t s);
+hipError_t launch_train_step(const ertd_weights& w, const float* x0, const int64_t* t,
+                             const float* noise, const float* cond, const float* alpha_bar, int B,
+                             int L, const float* freq, float* const* grads, float* const* exp_avg,
+                             float* const* exp_avg_sq, const TrainAdam& adam, float* loss_out,
+                             float* ws, hipStream_t s);
 hipError_t launch_adam(const ertd_weights& w, float* const* grads, float* const* exp_avg,
                        float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
                        float eps, hipStream_t s);
+// the reference condition encoder alone (the U-Net's condition branch): forward
+// with saved activations (partial_out = the (B, S, 64) pool partials in ws) and
+// the conv-parameter backward from g = dL/dm / L2 (B, 64); raw weights w1 (32,14,3), w2 (64,32,3)
+size_t encoder_train_ws_floats(int B, int L);
+hipError_t launch_encoder_train(const float* w1, const float* b1, const float* w2, const float* b2,
+                                const float* cond, int B, int L, float* ws, float** partial_out,
+                                hipStream_t s);
+hipError_t launch_encoder_conv_backward(const float* w2, const float* cond, const float* g, int B,
+                                        int L, float* ws, float* dw1, float* db1, float* dw2,
+                                        float* db2, hipStream_t s);
 
 }  // namespace ertd

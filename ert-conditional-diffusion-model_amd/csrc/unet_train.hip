@@ -904,25 +904,12 @@ int ertd_mse_loss(const float* eps, const float* noise, long long n, float* loss
   return rcode(hipGetLastError());
 }
 
-// the reference condition encoder with saved activations: partial (B,S,64),
-// a1 (B,32,L1), relu mask m2 (B,64,L2) bytes, pool mean m (B,64); packed =
-// the reference-layout packing (ertd_pack_weights) of the current encoder weights
+// the reference condition encoder with saved activations (train.hip: pool
+// partials, conv1 strip images, conv2 ReLU mask bits) and the backward's strip
+// partial rows; packed = ertd_encoder_train_pack's copy of the conv weights
 size_t ertd_encoder_train_ws_bytes(int B, int L) {
   if (B < 1 || L < 1) return 0;
-  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
-  size_t f = (size_t)B * S * C2 + (size_t)B * C1 * L1 + ((size_t)B * C2 * L2 + 3) / 4 + 64 * 4 +
-             encoder_bwd_ws_floats(B, L);
-  return f * sizeof(float);
-}
-
-static void enc_layout(int B, int L, float* ws, float** partial, float** a1, unsigned char** m2,
-                       float** bw) {
-  const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
-  size_t o = 0;
-  *partial = ws + o; o += ((size_t)B * S * C2 + 63) / 64 * 64;
-  *a1 = ws + o; o += ((size_t)B * C1 * L1 + 63) / 64 * 64;
-  *m2 = (unsigned char*)(ws + o); o += (((size_t)B * C2 * L2 + 3) / 4 + 63) / 64 * 64;
-  *bw = ws + o;
+  return encoder_train_ws_floats(B, L) * sizeof(float);
 }
 
 int ertd_encoder_train_pack(const float* w0, const float* w2, float* packed, void* stream) {
@@ -934,11 +921,10 @@ int ertd_encoder_train_fwd(const float* packed, const float* b1, const float* b2
                            int B, int L, float* m_out, void* ws, size_t ws_bytes, void* stream) {
   if (!packed || !b1 || !b2 || !cond || !m_out || !ws || B < 1 || L < 1) return ERTD_EINVAL;
   if (ertd_encoder_train_ws_bytes(B, L) > ws_bytes) return ERTD_ENOSPC;
-  float *partial, *a1, *bw;
-  unsigned char* m2;
-  enc_layout(B, L, (float*)ws, &partial, &a1, &m2, &bw);
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = launch_encoder_train(packed, b1, b2, cond, B, L, partial, a1, m2, s);
+  float* partial = nullptr;
+  hipError_t e = launch_encoder_train(packed, b1, packed + ENC_RAW_W2, b2, cond, B, L, (float*)ws,
+                                      &partial, s);
   if (e != hipSuccess) return (int)e;
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
   pool_mean_kernel<<<nblk((size_t)B * C2), 256, 0, s>>>(partial, S, L2, B, m_out);
@@ -952,11 +938,8 @@ int ertd_encoder_train_bwd(const float* packed, const float* cond, const float* 
   if (!packed || !cond || !g || !dw1 || !db1 || !dw2 || !db2 || !ws || B < 1 || L < 1)
     return ERTD_EINVAL;
   if (ertd_encoder_train_ws_bytes(B, L) > ws_bytes) return ERTD_ENOSPC;
-  float *partial, *a1, *bw;
-  unsigned char* m2;
-  enc_layout(B, L, (float*)ws, &partial, &a1, &m2, &bw);
-  return rcode(launch_encoder_conv_backward(packed, cond, a1, m2, g, B, L, bw, dw1, db1, dw2, db2,
-                                            (hipStream_t)stream));
+  return rcode(launch_encoder_conv_backward(packed + ENC_RAW_W2, cond, g, B, L, (float*)ws, dw1, db1,
+                                            dw2, db2, (hipStream_t)stream));
 }
 
 int ertd_concat(const float* const* srcs, const long long* sizes, int n, float* dst, void* stream) {

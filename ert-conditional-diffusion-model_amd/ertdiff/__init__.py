@@ -12,7 +12,7 @@ from .model import STATE_KEYS, ConditionalDiffusionModel, get_timestep_embedding
 from .sampler import (SamplerPlan, as_ertdiff_model, draw_reference_noise, philox_normal,
                       sample_conditions, sample_model)
 from .schedule import get_diffusion_schedule, step_tables, timestep_frequencies
-from .train import DiffusionForwardFn, train_step, validation_loss
+from .train import DiffusionForwardFn, TrainPlan, train_step, validation_loss
 from .ensemble import member_range, sample_conditions_sharded, sample_ensemble
 from .postproc import compact, postprocess, sample_realisations
 from .unet import ConditionalUNet, UNetSamplerPlan, sample_unet
@@ -24,7 +24,7 @@ __all__ = [
     "sample_model", "SamplerPlan", "philox_normal", "draw_reference_noise", "as_ertdiff_model",
     "step_tables", "timestep_frequencies", "transform_to_unconstrained", "inverse_transform",
     "DiffusionDataset", "check_param_bounds", "bounds_mask", "load_best_model",
-    "save_checkpoint", "STATE_KEYS", "train_step", "validation_loss", "DiffusionForwardFn",
+    "save_checkpoint", "STATE_KEYS", "train_step", "TrainPlan", "validation_loss", "DiffusionForwardFn",
     "sample_ensemble", "member_range", "sample_conditions", "sample_conditions_sharded", "postprocess", "sample_realisations", "compact",
     "ConditionalUNet", "UNetSamplerPlan", "sample_unet", "kde_mode", "ensemble_mode",
     "mode_kde_calculation", "unet_train_step", "UNetTrainPlan", "unet_train_forward", "unet_train_backward",

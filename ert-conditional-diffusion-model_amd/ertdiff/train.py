@@ -10,6 +10,10 @@
                        library call: q_sample -> forward -> MSELoss -> backward
                        -> Adam, updating the torch.optim.Adam state in place so
                        optimizer.state_dict() stays valid (:348).
+  TrainPlan            the same step for a fixed (B, L) captured once as a graph
+                       (the draws of t and noise and the Adam step count on the
+                       device): the reference loop's 63,500 steps at one graph
+                       launch each.
   validation_loss      the no-grad validation pass body (:327-336).
 """
 from __future__ import annotations
@@ -37,17 +41,16 @@ class DiffusionForwardFn(torch.autograd.Function):
         tt = t.to(torch.int64).contiguous()
         B, L, P = x.shape[0], cond.shape[2], model.param_dim
         ws = _train_ws(dev, B, L, P)
-        packed = torch.empty(_lib.lib().ertd_packed_floats(), dtype=torch.float32, device=dev)
         eps = torch.empty(B, P, dtype=torch.float32, device=dev)
         freq = timestep_frequencies(_lib.HIDDEN, dev)
         w = model.weights_struct()
         with torch.cuda.device(dev):
             _lib.check(_lib.lib().ertd_train_forward(
-                ctypes.byref(w), packed.data_ptr(), x.data_ptr(), None, None, None, tt.data_ptr(),
+                ctypes.byref(w), None, x.data_ptr(), None, None, None, tt.data_ptr(),
                 cond.data_ptr(), B, L, freq.data_ptr(), eps.data_ptr(), ws.data_ptr(), ws.numel(),
                 _lib.stream_of(dev)), "train_forward")
         ctx.model = model
-        ctx.ws, ctx.packed, ctx.cond, ctx.B, ctx.L = ws, packed, cond, B, L
+        ctx.ws, ctx.cond, ctx.B, ctx.L = ws, cond, B, L
         ctx.save_for_backward(*params)
         return eps
 
@@ -62,7 +65,7 @@ class DiffusionForwardFn(torch.autograd.Function):
         w = ctx.model.weights_struct()
         with torch.cuda.device(dev):
             _lib.check(_lib.lib().ertd_train_backward(
-                ctypes.byref(w), ctx.packed.data_ptr(), dout.data_ptr(), None, ctx.cond.data_ptr(),
+                ctypes.byref(w), None, dout.data_ptr(), None, ctx.cond.data_ptr(),
                 ctx.B, ctx.L, _lib.ptr_array(grads), None, _lib.ptr(dx), ctx.ws.data_ptr(),
                 ctx.ws.numel(), _lib.stream_of(dev)), "train_backward")
         return (None, dx, None, None, *grads)
@@ -83,6 +86,21 @@ def _adam_hparams(optimizer, params):
     if isinstance(lr, torch.Tensor):
         lr = float(lr)
     return float(lr), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"])
+
+
+def _adam_state(optimizer, params):
+    """exp_avg / exp_avg_sq of every parameter, created as torch.optim.Adam
+    creates them on its first step (step = 0-dim float32 CPU tensor)."""
+    exp_avg, exp_avg_sq = [], []
+    for p in params:
+        st = optimizer.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0, dtype=torch.float32)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        exp_avg.append(st["exp_avg"])
+        exp_avg_sq.append(st["exp_avg_sq"])
+    return exp_avg, exp_avg_sq
 
 
 def train_step(model, optimizer, x0, cond, T, alpha_bar, *, t=None, noise=None,
@@ -110,34 +128,186 @@ def train_step(model, optimizer, x0, cond, T, alpha_bar, *, t=None, noise=None,
     tt = t.to(device=dev, dtype=torch.int64).contiguous()
     model._check_inputs(x0, tt, cond)
     lr, b1, b2, eps = _adam_hparams(optimizer, params)
-    exp_avg, exp_avg_sq = [], []
+    exp_avg, exp_avg_sq = _adam_state(optimizer, params)
     for p in params:
-        st = optimizer.state[p]
-        if len(st) == 0:
-            st["step"] = torch.tensor(0.0, dtype=torch.float32)
-            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-        st["step"] += 1
-        exp_avg.append(st["exp_avg"])
-        exp_avg_sq.append(st["exp_avg_sq"])
+        optimizer.state[p]["step"] += 1
         if p.grad is None:
             p.grad = torch.empty_like(p)
     step = int(optimizer.state[params[0]]["step"].item())
     grads = [p.grad for p in params]
     L = cond.shape[2]
     ws = model.workspace(dev, B, L, 0, _lib.OP_TRAIN)
-    packed = model.packed_weights(dev)
     loss = torch.empty((), dtype=torch.float32, device=dev)
     freq = timestep_frequencies(_lib.HIDDEN, dev)
     w = model.weights_struct()
     with torch.cuda.device(dev):
         _lib.check(_lib.lib().ertd_train_step(
-            ctypes.byref(w), packed.data_ptr(), x0.data_ptr(), tt.data_ptr(), noise.data_ptr(),
+            ctypes.byref(w), None, x0.data_ptr(), tt.data_ptr(), noise.data_ptr(),
             cond.data_ptr(), ab.data_ptr(), B, L, freq.data_ptr(), _lib.ptr_array(grads),
             _lib.ptr_array(exp_avg), _lib.ptr_array(exp_avg_sq), step, lr, b1, b2, eps,
             loss.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_of(dev)), "train_step")
     model._packed_key = None  # parameters changed in place behind autograd's back: re-pack
     return loss if return_tensor else loss.item()
+
+
+class TrainPlan:
+    """train_step for a fixed (B, L), captured ONCE as a graph
+    (torch.cuda.CUDAGraph = hipGraph) and replayed per step: the draws
+    t ~ U{0..T-1} and noise ~ N(0, 1) (:312-313), q_sample -> forward -> MSELoss
+    -> backward -> Adam (the four kernels of csrc/train.hip).
+
+    rng="philox" (default): the step draws t and noise itself inside its head
+      kernel (Philox4x32-10 keyed by (seed, member, Adam step): reproducible,
+      no extra launches); seed defaults to one drawn from torch's CPU generator.
+    rng="torch": torch.randint / torch.randn_like on torch's own generator are
+      captured too (graph-safe): the same numbers the reference's eager draws
+      give after the same manual_seed, at the cost of their extra launches.  The Adam step count lives on the
+    device (advanced inside the graph); the bias corrections come from a table
+    the host formed as torch does (ertd_adam_table), so a replay needs no host
+    scalars.  optimizer.state[p]["step"], exp_avg, exp_avg_sq and p.grad stay
+    the torch.optim.Adam state of the eager path (optimizer.state_dict() is
+    valid after every step, :348).
+
+        plan = TrainPlan(model, optimizer, B, L, T, alpha_bar)
+        loss = plan.step(x0, cond)                # == train_step(...), bit for bit
+        plan.x0.copy_(...); plan.cond.copy_(...)  # or fill the inputs in place
+        plan.run(n)                               # n steps, no per-step host sync
+
+    The graph addresses the parameters, their gradients and the Adam state:
+    keep them (optimizer.step() / load_state_dict on the model copy in place;
+    build a new plan after optimizer.load_state_dict(), which replaces the
+    state tensors)."""
+
+    TABLE = 65536  # Adam steps per table; a plan past its table re-captures
+
+    def __init__(self, model, optimizer, B: int, L: int, T: int, alpha_bar, warmup: int = 1,
+                 rng: str = "philox", seed=None):
+        if rng not in ("philox", "torch"):
+            raise ValueError("ertdiff: TrainPlan rng must be 'philox' or 'torch'")
+        self.rng = rng
+        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if seed is None else int(seed)
+        model._check_supported()
+        self.model, self.optimizer, self.T = model, optimizer, int(T)
+        self.params = model._params()
+        dev = _lib.require_device(alpha_bar, self.params[0])
+        self.dev, self.B, self.L = dev, int(B), int(L)
+        P = model.param_dim
+        self.lr, self.b1, self.b2, self.eps = _adam_hparams(optimizer, self.params)
+        self.alpha_bar = _lib.f32c(alpha_bar, "alpha_bar")
+        z = dict(dtype=torch.float32, device=dev)
+        self.x0 = torch.zeros(B, P, **z)
+        self.cond = torch.zeros(B, _lib.CIN, L, **z)
+        self.t = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.noise = torch.zeros(B, P, **z)
+        self.loss = torch.zeros((), **z)
+        self.exp_avg, self.exp_avg_sq = _adam_state(optimizer, self.params)
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.empty_like(p)
+        self.grads = [p.grad for p in self.params]
+        self._steps = [optimizer.state[p]["step"] for p in self.params]
+        self.ws = torch.empty(max(_lib.lib().ertd_workspace_bytes(B, L, P, 0, _lib.OP_TRAIN), 256),
+                              dtype=torch.uint8, device=dev)
+        self.freq = timestep_frequencies(_lib.HIDDEN, dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._graphs = {}
+        self._table_at(int(self._steps[0].item()))
+        # warm-up outside any capture (module load, lazily created state): the
+        # forward + backward on the zero inputs -- parameters, Adam state and the
+        # generator are untouched
+        w = model.weights_struct()
+        scratch = torch.empty((), **z)
+        with torch.cuda.device(dev):
+            for _ in range(max(1, int(warmup))):
+                _lib.check(_lib.lib().ertd_train_forward(
+                    ctypes.byref(w), None, None, self.x0.data_ptr(), self.noise.data_ptr(),
+                    self.alpha_bar.data_ptr(), self.t.data_ptr(), self.cond.data_ptr(), B, L,
+                    self.freq.data_ptr(), None, self.ws.data_ptr(), self.ws.numel(),
+                    _lib.stream_of(dev)), "train_forward")
+                _lib.check(_lib.lib().ertd_train_backward(
+                    ctypes.byref(w), None, None, self.noise.data_ptr(), self.cond.data_ptr(), B, L,
+                    _lib.ptr_array(self.grads), scratch.data_ptr(), None, self.ws.data_ptr(),
+                    self.ws.numel(), _lib.stream_of(dev)), "train_backward")
+            torch.cuda.synchronize(dev)
+
+    def _table_at(self, step0: int):
+        """Adam scalars of steps step0+1 ... step0+TABLE; drops captured graphs
+        (the table's first step is a kernel argument)."""
+        n = self.TABLE
+        host = torch.empty(n * 6, dtype=torch.float32)
+        _lib.check(_lib.lib().ertd_adam_table(step0 + 1, n, self.lr, self.b1, self.b2, self.eps,
+                                              host.data_ptr()), "adam_table")
+        torch.cuda.synchronize(self.dev)
+        self.table = host.to(self.dev)
+        self.table_first = step0 + 1
+        self.step_dev.fill_(step0)
+        self.host_step = step0
+        self._graphs = {}
+
+    def _body(self, draw: bool):
+        dev_draw = draw and self.rng == "philox"
+        if draw and not dev_draw:
+            self.t.random_(0, self.T)   # torch.randint(0, T, (B,)) (:312)
+            self.noise.normal_()        # torch.randn_like(x0) (:313)
+        w = self.model.weights_struct()
+        _lib.check(_lib.lib().ertd_train_step_dev(
+            ctypes.byref(w), self.x0.data_ptr(), self.t.data_ptr(), self.noise.data_ptr(),
+            self.cond.data_ptr(), self.alpha_bar.data_ptr(), self.B, self.L, self.freq.data_ptr(),
+            _lib.ptr_array(self.grads), _lib.ptr_array(self.exp_avg), _lib.ptr_array(self.exp_avg_sq),
+            self.step_dev.data_ptr(), self.table.data_ptr(), self.table_first, self.TABLE,
+            1 if dev_draw else 0, self.T, self.seed, self.loss.data_ptr(), self.ws.data_ptr(),
+            self.ws.numel(), _lib.stream_of(self.dev)), "train_step_dev")
+
+    def _graph(self, draw: bool):
+        g = self._graphs.get(draw)
+        if g is None:
+            with torch.cuda.device(self.dev):
+                torch.cuda.synchronize(self.dev)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    self._body(draw)
+            self._graphs[draw] = g
+        return g
+
+    @torch.no_grad()
+    def _replay(self, draw: bool):
+        if self.host_step + 1 >= self.table_first + self.TABLE:
+            self._table_at(self.host_step)
+        g = self._graph(draw)
+        with torch.cuda.device(self.dev):
+            g.replay()
+        self.host_step += 1
+        torch._foreach_add_(self._steps, 1.0)
+        for p, gr in zip(self.params, self.grads):
+            if p.grad is not gr:
+                p.grad = gr
+        self.model._packed_key = None  # parameters changed in place: re-pack for sampling
+
+    @torch.no_grad()
+    def step(self, x0=None, cond=None, *, t=None, noise=None, return_tensor: bool = False):
+        """One optimizer step (the contract of train_step).  x0 / cond default to
+        the plan's input buffers (fill them in place to skip the copies); t and
+        noise are drawn in the graph unless both are given."""
+        for src, dst, nm in ((x0, self.x0, "x0"), (cond, self.cond, "condition")):
+            if src is not None and src.data_ptr() != dst.data_ptr():
+                if src.shape != dst.shape:
+                    raise RuntimeError(f"ertdiff: this plan was captured for {nm} {tuple(dst.shape)}")
+                dst.copy_(src)
+        if (t is None) != (noise is None):
+            raise RuntimeError("ertdiff: TrainPlan.step takes both t and noise, or neither")
+        draw = t is None
+        if not draw:
+            self.t.copy_(t.to(torch.int64))
+            self.noise.copy_(noise)
+        self._replay(draw)
+        return self.loss.clone() if return_tensor else self.loss.item()
+
+    @torch.no_grad()
+    def run(self, n: int):
+        """n steps on the plan's inputs with fresh draws; no per-step host sync
+        (the loss of the last step stays in plan.loss)."""
+        for _ in range(int(n)):
+            self._replay(True)
 
 
 @torch.no_grad()

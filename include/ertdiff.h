@@ -224,7 +224,8 @@ int ertd_sample_conditions_plan_create(const ertd_weights* w, const float* packe
 
 /* Training forward: eps = model(x, t, cond) with activations saved in ws.
  * x (B,P), or x == NULL and x0/noise/alpha_bar given: x = q_sample(x0, t, noise)
- * (:314).  Re-packs the weights into `packed` first (they change every step). */
+ * (:314).  The train kernels read the parameters of `w` in place: `packed` is
+ * unused (kept for ABI compatibility; may be NULL), here and below.          */
 int ertd_train_forward(const ertd_weights* w, float* packed, const float* x, const float* x0,
                        const float* noise, const float* alpha_bar, const int64_t* t,
                        const float* cond, int B, int L, const float* freq, float* eps_out,
@@ -244,12 +245,33 @@ int ertd_adam(const ertd_weights* w, float* const* grads, float* const* exp_avg,
               void* stream);
 
 /* The reference train step (:309-319) in one call: q_sample -> forward ->
- * MSELoss -> backward -> Adam.  loss_out (1) float32 on device.            */
+ * MSELoss -> backward -> Adam.  loss_out (1) float32 on device; grads receive
+ * the gradients (the reference's p.grad after loss.backward()).            */
 int ertd_train_step(const ertd_weights* w, float* packed, const float* x0, const int64_t* t,
                     const float* noise, const float* cond, const float* alpha_bar, int B, int L,
                     const float* freq, float* const* grads, float* const* exp_avg,
                     float* const* exp_avg_sq, int step, float lr, float beta1, float beta2,
                     float eps, float* loss_out, void* ws, size_t ws_bytes, void* stream);
+
+/* ertd_train_step with no host scalars, for graph capture (ertdiff.TrainPlan):
+ * the step advances the device counter *step_dev (int32; the count of Adam
+ * steps applied, as torch's state["step"]) and the update of step s uses the
+ * 6-float entry adam_table[s - table_first] (device copy of ertd_adam_table's
+ * output); s must lie in [table_first, table_first + table_len).
+ * draw = 0: t (B) / noise (B,P) are inputs.  draw = 1: the step draws them
+ * itself into the same buffers (t ~ U{0..T-1}, noise ~ N(0,1), Philox4x32-10
+ * keyed by (seed, member, step s): reproducible, independent of the grid).  */
+int ertd_train_step_dev(const ertd_weights* w, const float* x0, int64_t* t, float* noise,
+                        const float* cond, const float* alpha_bar, int B, int L, const float* freq,
+                        float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                        int* step_dev, const float* adam_table, int table_first, int table_len,
+                        int draw, int T, uint64_t seed, float* loss_out, void* ws, size_t ws_bytes,
+                        void* stream);
+
+/* host: the Adam scalars of steps step_first ... step_first + n - 1 (6 floats
+ * each), formed as torch.optim.Adam forms them (Python-float bias corrections). */
+int ertd_adam_table(int step_first, int n, float lr, float beta1, float beta2, float eps,
+                    float* out);
 
 /* ---- build-defined conditional U-Net (SURVEY.md 8a'; north_star) -----------------
  * PARITY UNPINNED vs the reference: ERT_Conditional_Diffusion.py has no U-Net
@@ -428,8 +450,8 @@ int ertd_unet_plan_destroy(ertd_unet_plan* plan);
  * ertd_channel_sums: out_bc (B, C; row stride ldo, 0 = C) sums over HW; out_c (C) = sum over b
  *   (optional, ldo = C).
  * ertd_concat: dst = cat(srcs[0..n)) of contiguous fp32 tensors (sizes in elements).
- * ertd_encoder_train_pack: the encoder conv regions of the ertd_pack_weights layout
- *   (ertd_packed_floats() buffer) from condition_encoder.0 / .2 weights.
+ * ertd_encoder_train_pack: copies condition_encoder.0 / .2 weights into an
+ *   ertd_packed_floats() buffer (the layout ertd_encoder_train_fwd / _bwd read).
  * ertd_gemm_small: C[b][i][j] = alpha sum_k A[b][i][k] B[b][k][j] (+ bias[j]) with element
  *   strides (a_i, a_k, a_b, b_k, b_j, b_b, c_i, c_j, c_b).
  * ertd_softmax_rows: P = softmax(scale S) per row; ertd_softmax_backward: dS = scale P (dP - <dP, P>).

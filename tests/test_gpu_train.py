@@ -137,3 +137,104 @@ def test_train_step_deterministic(golden_weights, cuda_dev):
     assert outs[0][0] == outs[1][0]
     assert all(torch.equal(a, b) for a, b in zip(outs[0][1], outs[1][1]))
     assert all(np.isfinite(outs[0][0]))
+
+
+def _train_inputs(B, L, T, seed, dev):
+    x0 = torch.from_numpy(synth_normal((B, 29), seed)).to(dev)
+    cond = torch.from_numpy(synth_uniform((B, 14, L), seed + 1)).to(dev)
+    g = torch.Generator(device=dev).manual_seed(seed + 2)
+    ts = [torch.randint(0, T, (B,), device=dev, generator=g) for _ in range(4)]
+    ns = [torch.randn(B, 29, device=dev, generator=g) for _ in range(4)]
+    return x0, cond, ts, ns
+
+
+@pytest.mark.parametrize("B,L", [(32, 4693), (3, 37)])
+def test_train_plan_equals_eager(B, L, golden_weights, cuda_dev):
+    """TrainPlan (one captured graph per step, device-side Adam step count)
+    replays the eager train_step bit for bit: losses, gradients, parameters,
+    and the torch.optim.Adam state (step counters, exp_avg, exp_avg_sq)."""
+    T = 500
+    x0, cond, ts, ns = _train_inputs(B, L, T, 610, cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    m1 = _fresh_model(golden_weights, cuda_dev)
+    o1 = torch.optim.Adam(m1.parameters(), lr=1e-4)
+    l1 = [ertdiff.train_step(m1, o1, x0, cond, T, ab, t=ts[i], noise=ns[i]) for i in range(4)]
+    m2 = _fresh_model(golden_weights, cuda_dev)
+    o2 = torch.optim.Adam(m2.parameters(), lr=1e-4)
+    plan = ertdiff.TrainPlan(m2, o2, B, L, T, ab)
+    l2 = [plan.step(x0, cond, t=ts[i], noise=ns[i]) for i in range(4)]
+    assert l1 == l2
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p1, p2), k
+        assert torch.equal(p1.grad, p2.grad), k
+        s1, s2 = o1.state[p1], o2.state[p2]
+        assert float(s1["step"]) == float(s2["step"]) == 4.0
+        assert torch.equal(s1["exp_avg"], s2["exp_avg"]) and torch.equal(s1["exp_avg_sq"], s2["exp_avg_sq"])
+    # the eager path continues from the plan's state
+    la = ertdiff.train_step(m1, o1, x0, cond, T, ab, t=ts[0], noise=ns[0])
+    lb = ertdiff.train_step(m2, o2, x0, cond, T, ab, t=ts[0], noise=ns[0])
+    assert la == lb
+
+
+def test_train_plan_draws_match_torch(golden_weights, cuda_dev):
+    """The graph's draws are torch's own: after manual_seed, a replay draws the
+    t and noise that torch.randint / torch.randn_like draw eagerly (:312-313),
+    and the step equals the eager step on them."""
+    B, L, T = 8, 4693, 1000
+    x0, cond, _, _ = _train_inputs(B, L, T, 620, cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    m2 = _fresh_model(golden_weights, cuda_dev)
+    o2 = torch.optim.Adam(m2.parameters(), lr=1e-4)
+    plan = ertdiff.TrainPlan(m2, o2, B, L, T, ab, rng="torch")
+    m1 = _fresh_model(golden_weights, cuda_dev)
+    o1 = torch.optim.Adam(m1.parameters(), lr=1e-4)
+    for s in range(3):
+        torch.manual_seed(77 + s)
+        lp = plan.step(x0, cond)
+        torch.manual_seed(77 + s)
+        t = torch.randint(0, T, (B,), device=cuda_dev).long()
+        n = torch.randn_like(x0)
+        assert torch.equal(plan.t, t) and torch.equal(plan.noise, n), s
+        assert ertdiff.train_step(m1, o1, x0, cond, T, ab, t=t, noise=n) == lp, s
+    plan.run(5)
+    torch.cuda.synchronize()
+    assert float(o2.state_dict()["state"][0]["step"]) == 8.0
+    assert np.isfinite(float(plan.loss))
+
+
+def test_train_plan_philox_draws(golden_weights, cuda_dev):
+    """rng="philox": the step draws t ~ U{0..T-1} and noise ~ N(0,1) in its head
+    kernel (keyed by seed, member, Adam step); the step equals the eager step
+    on the drawn values, and a second plan with the same seed repeats it."""
+    B, L, T = 32, 4693, 1000
+    x0, cond, _, _ = _train_inputs(B, L, T, 630, cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    runs = []
+    for rep in range(2):
+        m2 = _fresh_model(golden_weights, cuda_dev)
+        o2 = torch.optim.Adam(m2.parameters(), lr=1e-4)
+        plan = ertdiff.TrainPlan(m2, o2, B, L, T, ab, seed=1234)
+        m1 = _fresh_model(golden_weights, cuda_dev)
+        o1 = torch.optim.Adam(m1.parameters(), lr=1e-4)
+        ts, ns, ls = [], [], []
+        for s in range(3):
+            lp = plan.step(x0, cond)
+            t, n = plan.t.clone(), plan.noise.clone()
+            assert int(t.min()) >= 0 and int(t.max()) < T
+            assert ertdiff.train_step(m1, o1, x0, cond, T, ab, t=t, noise=n) == lp, s
+            ts.append(t); ns.append(n); ls.append(lp)
+        assert not torch.equal(ts[0], ts[1]) and not torch.equal(ns[0], ns[1])
+        runs.append((ts, ns, ls))
+    assert runs[0][2] == runs[1][2]
+    assert all(torch.equal(a, b) for a, b in zip(runs[0][0], runs[1][0]))
+    # the draws are standard normal / uniform over many steps
+    m = _fresh_model(golden_weights, cuda_dev)
+    plan = ertdiff.TrainPlan(m, torch.optim.Adam(m.parameters(), lr=1e-4), B, L, T, ab, seed=99)
+    zs, tt = [], []
+    for _ in range(40):
+        plan.step(x0, cond, return_tensor=True)
+        zs.append(plan.noise.clone()); tt.append(plan.t.clone())
+    z = torch.cat(zs).double()
+    assert abs(float(z.mean())) < 0.05 and abs(float(z.std()) - 1.0) < 0.05
+    tv = torch.cat(tt).double()
+    assert abs(float(tv.mean()) - (T - 1) / 2) < 0.06 * T
