@@ -25,6 +25,7 @@ struct Ws {
   float* uring;                 // (R, B, 128) condition rows
   float* Vc;                    // (T, 128) time rows of the chain
   size_t zero_bytes;
+  unsigned* status;             // sampler status word (every faithful schedule)
 };
 
 // sync block (zeroed per call), one word per SYNC_PAD-word line:
@@ -52,10 +53,19 @@ size_t ws_layout(int B, int L, int T, int op, void* base, Ws* out) {
     off += align_up((size_t)(T > 0 ? T : 1) * H * sizeof(float));
     w.cond_emb = (float*)(p + off);
     off += align_up((size_t)B * H * sizeof(float));
+    if (!faithful_chain_may_run(B)) {
+      // the persistent chain cannot be resident at this B: no ring, no sync
+      // block (faithful mode runs the per-step schedule), just the status word
+      w.status = (unsigned*)(p + off);
+      off += align_up(SYNC_PAD * sizeof(unsigned));
+      if (out) *out = w;
+      return off;
+    }
     w.ring = (float*)(p + off);
     off += align_up((size_t)CHAIN_RING * B * S * C2 * sizeof(float));
     w.sync = (unsigned*)(p + off);
     w.zero_bytes = sync_words(B) * sizeof(unsigned);
+    w.status = status_word(w.sync, B);
     off += align_up(w.zero_bytes);
     w.uring = (float*)(p + off);
     off += align_up((size_t)CHAIN_RING * B * H * sizeof(float));
@@ -122,7 +132,7 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
   // launch for the whole chain (chain.hip); it needs every block resident, so
   // it is used when the grid fits (and for fp32, the precision it implements).
   if (mode == ERTD_MODE_FAITHFUL && precision == ERTD_PREC_FP32) {
-    const int grid = faithful_chain_grid(B, S);
+    const int grid = W.ring ? faithful_chain_grid(B, S) : 0;
     if (grid > 0) {
       ERTD_TRY(launch_zero_words(W.sync, W.zero_bytes / sizeof(unsigned), s));
       FaithfulChainArgs fa{};
@@ -151,7 +161,7 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
       fa.progress = fa.uflag + (size_t)CHAIN_RING * B * SYNC_PAD;
       fa.claim = fa.progress + (size_t)B * SYNC_PAD;
       fa.vready = fa.claim + (size_t)B * SYNC_PAD;
-      fa.status = status_word(W.sync, B);
+      fa.status = W.status;
       fa.uring = W.uring;
       fa.V = W.Vc;
       return rc(launch_faithful_chain(*w, packed, fa, grid, s));
@@ -160,7 +170,7 @@ int enqueue_sample(const ertd_weights* w, const float* packed, const float* cond
   // Per-step schedule (ERTD_MODE_FAITHFUL_STEPS, bf16, or grids too large to
   // be resident): encoder(t), head(t), encoder(t-1), ... on one stream.
   // (The status word is cleared so ertd_sample_status reads ok.)
-  ERTD_TRY(launch_zero_words(status_word(W.sync, B), 1, s));
+  ERTD_TRY(launch_zero_words(W.status, 1, s));
   // A pipeline over several streams was measured and rejected: cross-queue
   // event hops inside a graph cost ~10 us each on ROCm 7.
   HeadArgs a{};
@@ -319,7 +329,7 @@ int ertd_sample_status(const void* ws, int B, int L, int num_steps, int* status,
   if (!ws || !status || B < 1 || L < 1 || num_steps < 1) return ERTD_EINVAL;
   Ws W;
   ws_layout(B, L, num_steps, ERTD_OP_SAMPLE, const_cast<void*>(ws), &W);
-  const unsigned* dev = status_word(W.sync, B);
+  const unsigned* dev = W.status;
   unsigned v = 0;
   ERTD_TRY(hipMemcpyAsync(&v, dev, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)stream));
   ERTD_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -380,9 +390,17 @@ int capture_plan(ertd_plan** plan, Enqueue&& enqueue) {
   return ERTD_OK;
 }
 
-// ertd_sample_conditions' geometry checks; returns B = n_cond * n_samples or 0
-int conditions_batch(int n_cond, int n_samples, long long id_period) {
+// ertd_sample_conditions' geometry checks; returns B = n_cond * n_samples or 0.
+// member_id() computes member_offset + r * id_period + c in uint32: the slice
+// must fit one period (member_offset + n_cond <= id_period, as the Python
+// wrapper enforces) and the largest id must not wrap, or Philox ids of
+// different members (ranks, realisations) would coincide.
+int conditions_batch(int n_cond, int n_samples, long long id_period, uint32_t member_offset) {
   if (n_cond < 1 || n_samples < 1 || id_period < n_cond || id_period > 0x7fffffff) return 0;
+  if ((long long)member_offset + n_cond > id_period) return 0;
+  if ((unsigned long long)member_offset + (unsigned long long)(n_samples - 1) * (unsigned long long)id_period +
+          (unsigned long long)n_cond > 0x100000000ull)
+    return 0;
   const long long B = (long long)n_cond * n_samples;
   return B > (1 << 30) ? 0 : (int)B;
 }
@@ -410,7 +428,7 @@ int ertd_sample_conditions(const ertd_weights* w, const float* packed, const flo
                            const float* freq, const float* noise, uint64_t seed,
                            uint32_t member_offset, int mode, int precision, float* x_inout, void* ws,
                            size_t ws_bytes, void* stream) {
-  const int B = conditions_batch(n_cond, n_samples, id_period);
+  const int B = conditions_batch(n_cond, n_samples, id_period, member_offset);
   if (!B) return ERTD_EINVAL;
   return enqueue_sample(w, packed, cond, (long long)CIN * L, B, L, num_steps, t_first, n_run, c1, c2,
                         sigma, freq, noise, seed, member_offset, mode, precision, x_inout, ws,
@@ -424,7 +442,7 @@ int ertd_sample_conditions_plan_create(const ertd_weights* w, const float* packe
                                        const float* noise, uint64_t seed, uint32_t member_offset,
                                        int mode, int precision, float* x_inout, void* ws,
                                        size_t ws_bytes, ertd_plan** plan) {
-  const int B = conditions_batch(n_cond, n_samples, id_period);
+  const int B = conditions_batch(n_cond, n_samples, id_period, member_offset);
   if (!B) {
     if (plan) *plan = nullptr;
     return ERTD_EINVAL;

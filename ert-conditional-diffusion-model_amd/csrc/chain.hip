@@ -514,6 +514,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
 #endif
 }
 
+bool faithful_chain_may_run(int B) {
+  constexpr int MAX_CUS = 256;  // MI355X (gfx950): the most CUs a device of this target has
+  const long long nch = (B + CHAIN_MPB - 1) / CHAIN_MPB;
+  return B >= 1 && nch + 1 + B <= (long long)CHAIN_MAX_BPC * MAX_CUS;
+}
+
 int faithful_chain_grid(int B, int S) {
   static int cached[64];  // resident blocks per device (0 = not yet queried)
   int dev = 0;

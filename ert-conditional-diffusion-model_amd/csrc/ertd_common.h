@@ -289,6 +289,9 @@ constexpr int CHAIN_RING = ERTD_CHAIN_RING;
 constexpr int SYNC_PAD = 32;
 // grid for launch_faithful_chain (0: B too large for a resident grid)
 int faithful_chain_grid(int B, int S);
+// false where faithful_chain_grid(B, .) is 0 on any gfx950 device (device-
+// independent: sizes the sampler workspace's ring and sync block)
+bool faithful_chain_may_run(int B);
 hipError_t launch_zero_words(unsigned* p, size_t n, hipStream_t s);
 hipError_t launch_faithful_chain(const ertd_weights& w, const float* packed,
                                  const FaithfulChainArgs& a, int grid, hipStream_t s);

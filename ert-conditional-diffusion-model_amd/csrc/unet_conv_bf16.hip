@@ -676,6 +676,9 @@ size_t conv_bf16_image_bytes(int cin, int B, int H, int W, bool split) {
 template <int KS, int MODE, int ACT, int WO, int TPX, bool PRE = false, int DBG = 0, int SP = 1>
 static hipError_t launch_hgd(const ConvArgs& a, int B, hipStream_t s) {
   using G = GeomH<KS, MODE, WO, TPX, SP>;
+  // the epilogue writes GroupNorm partials only for 256-multiple pixel tiles:
+  // a caller asking for them (a.gnp) of any other tile would read unwritten memory
+  if (a.gnp && !(G::BM % 256 == 0 && (G::BM / 4) % 64 == 0)) return hipErrorInvalidValue;
   const size_t lds = G::LDS + 64 * sizeof(float2) + (ACT != ACT_NONE ? (size_t)a.Cin * sizeof(float2) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 65536)

@@ -97,7 +97,9 @@ def sample_realisations(model, condition, n_samples: int, T, betas, alphas, alph
     B = sample_kw.get("n_members") or condition.shape[0]
     seed = int(sample_kw.pop("seed", 0))
     if sample_kw.get("noise") == "philox" and sample_kw.get("member_offset"):
-        raise RuntimeError("ertdiff: sample_realisations assigns the member ids itself (r * B + b)")
+        raise RuntimeError("ertdiff: sample_realisations assigns the member ids itself (realisation r, "
+                           "member b -> id r * B + b under one seed); to offset the ids of a slice "
+                           "of conditions use sample_conditions(..., cond_offset=...)")
     if batched:
         if sample_kw.get("noise") != "philox" or sample_kw.get("shared_condition"):
             raise RuntimeError("ertdiff: batched realisations need noise='philox' and (B, 14, L) conditions")
