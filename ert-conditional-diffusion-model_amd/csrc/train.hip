@@ -55,6 +55,14 @@ constexpr int NG = NG_B2 + C2;  // 7584 (every region a multiple of 4 floats)
 constexpr int A1S_FLOATS = 2 * C1 * 64;
 constexpr int M2W_WORDS = 64 * 2;
 
+// k-major copies of the dense weights (written by enc_train_kernel each step)
+constexpr int WT_W3 = 0;                    // [64][128]   W3T[k][j] = W3[j][k]
+constexpr int WT_WT = WT_W3 + C2 * H;       // [128][128]  time_embed.0
+constexpr int WT_W0 = WT_WT + H * H;        // [K0][128]   mlp.0 (K0 = P + 256 <= 288)
+constexpr int WT_W2 = WT_W0 + (PMAX + 2 * H) * H;  // [128][32] mlp.2: W2T[k][o]
+constexpr int WT_FLOATS = WT_W2 + H * PMAX;
+
+constexpr int W2B_FRAG = 3 * 32 * 64;  // transposed-conv2 fragments (conv_bwd)
 // train_final_kernel's conv-column reduction (see there)
 constexpr int FIN_CB_COLS = 64;                                  // float4 columns per block
 constexpr int FIN_NCB = (NG / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;  // 30 column blocks
@@ -70,7 +78,8 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
     const float* __restrict__ w1, const float* __restrict__ b1, const float* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ cond, int L, int L1, int L2, int S,
     float* __restrict__ partial, float* __restrict__ a1s, uint32_t* __restrict__ m2w,
-    unsigned* __restrict__ fin_cnt, int* __restrict__ step_ctr) {
+    unsigned* __restrict__ fin_cnt, int* __restrict__ step_ctr, ertd_weights wd,
+    float* __restrict__ wt, float* __restrict__ w2b) {
   __shared__ __attribute__((aligned(16))) EncSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
@@ -79,18 +88,68 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
     if (tid < FIN_CNT_WORDS) fin_cnt[tid] = 0u;   // train_final_kernel's arrival counters
     if (tid == 0 && step_ctr) step_ctr[0] += 1;   // the Adam step of this train step
   }
+  // this step's transposed-conv2 fragments (conv_bwd's da1 A operand, one
+  // coalesced 256-B row per wave load): W2B[kk][s][lane] = W2[2s + (lane >> 5)][lane & 31][kk]
+  for (int e = item * 256 + tid; e < W2B_FRAG; e += gridDim.x * 256) {
+    const int kk = e >> 11, sl = e & 2047, st = sl >> 6, l = sl & 63;
+    w2b[e] = w2[((2 * st + (l >> 5)) * C1 + (l & 31)) * 3 + kk];
+  }
+  if (wt) {  // this step's k-major copies of the dense weights (the head's forward reads them)
+    const int P = wd.param_dim, K0 = P + 2 * H;
+    for (int e = item * 256 + tid; e < WT_FLOATS; e += gridDim.x * 256) {
+      float v;
+      if (e < WT_WT) {
+        v = wd.enc6_w[(e & (H - 1)) * C2 + (e >> 7)];
+      } else if (e < WT_W0) {
+        const int i = e - WT_WT;
+        v = wd.time_w[(i & (H - 1)) * H + (i >> 7)];
+      } else if (e < WT_W2) {
+        const int i = e - WT_W0, k = i >> 7;
+        v = k < K0 ? wd.mlp0_w[(size_t)(i & (H - 1)) * K0 + k] : 0.f;
+      } else {
+        const int i = e - WT_W2, o = i & (PMAX - 1);
+        v = o < P ? wd.mlp2_w[o * H + (i >> 5)] : 0.f;
+      }
+      wt[e] = v;
+    }
+  }
   const int b = item / S, strip = item - b * S;
   const int j0 = strip * J;
 
-  // conv1 fragment s of lane (o = l32, h): W1[o][c = s/3 + 7h][s % 3], contiguous in s
-  float wa[STEPS1];
+  // the conv weights through LDS (coalesced float4 loads; the fragment reads
+  // below are one ds_read_b32 each): W1 (32,42) and W2 (64,96), odd row pitches
+  __shared__ float w1s[C1][K1 + 1];
+  __shared__ float w2s[C2][K2 + 1];
   {
-    const float* src = w1 + l32 * K1 + 21 * h;
+    float4 v2[6], v1[2];
 #pragma unroll
-    for (int s = 0; s < STEPS1; ++s) wa[s] = src[s];
+    for (int k = 0; k < 6; ++k) v2[k] = reinterpret_cast<const float4*>(w2)[tid + 256 * k];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k;
+      v1[k] = i < C1 * K1 / 4 ? reinterpret_cast<const float4*>(w1)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int e = 4 * (tid + 256 * k), o = e / K2, c = e - o * K2;
+      w2s[o][c] = v2[k].x; w2s[o][c + 1] = v2[k].y; w2s[o][c + 2] = v2[k].z; w2s[o][c + 3] = v2[k].w;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = 4 * (tid + 256 * k);
+      if (e < C1 * K1) {
+        const float vv[4] = {v1[k].x, v1[k].y, v1[k].z, v1[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w1s[(e + j) / K1][(e + j) % K1] = vv[j];
+      }
+    }
   }
   stage_cond_f32(sm.X, cond + (size_t)b * CIN * L, L, 4 * j0 - 3, tid);
   __syncthreads();
+  // conv1 fragment s of lane (o = l32, h): W1[o][c = s/3 + 7h][s % 3], contiguous in s
+  float wa[STEPS1];
+#pragma unroll
+  for (int s = 0; s < STEPS1; ++s) wa[s] = w1s[l32][21 * h + s];
 
   {  // conv1 + bias + ReLU -> E / O (aliases X)
     const int par = wave >> 1, mt = wave & 1;
@@ -127,9 +186,8 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
     const int q = qt * 32 + l32, o = ot * 32 + l32;
     // conv2 fragment s of lane (o, h): W2[o][c = s/3 + 16h][s % 3], contiguous in s
     float w2r[STEPS2];
-    const float* src = w2 + o * K2 + 48 * h;
 #pragma unroll
-    for (int s = 0; s < STEPS2; ++s) w2r[s] = src[s];
+    for (int s = 0; s < STEPS2; ++s) w2r[s] = w2s[o][48 * h + s];
     const float* eb = &sm.E[0][0] + 16 * h * HS + q;
     f32x16 acc = {};
 #pragma unroll
@@ -165,71 +223,46 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// head forward / backward (one 256-thread block per member)
-// Forward layers y = W x + b (W row-major, as the parameters lie): a wave owns
-// 32 (or 8) rows, lane l the columns k = l + 64 i, so every weight load is a
-// coalesced 256-B row segment; the 64 lane partials of all its rows are summed
-// by one reduce-scatter (rows_reduce: 32 shuffles for 32 rows).  Backward
-// layers y = W^T x: a thread per output, the loads coalesced across threads,
-// 16 of them in flight.
+// head forward / backward (one 1024-thread block per member)
+// Every layer is split-k: thread (q, j) sums k in group q's range for output
+// j, the groups' partials are added in q order through LDS, so no dependent
+// chain is longer than 64 loads.  Forward layers y = W x read the k-major
+// copies WT[k][j] the encoder kernel wrote this step (coalesced across j);
+// backward layers y = W^T x read W itself (row j of W is contiguous in the
+// output index).
 // ---------------------------------------------------------------------------
+constexpr int HT = 1024;  // head block threads
 struct HeadSmem {
   float m[C2], e[H], c[H], te[H], hc[PMAX + 2 * H], h[H], eps[PMAX], nz[PMAX];
-  float dout[PMAX], dz5[H], dhc[2 * H], dz3[H], red[PMAX];
+  float dout[PMAX], dz5[H], dhc[PMAX + 2 * H], dz3[H], red[PMAX];
+  float part[HT];
   int t;
 };
 
-// v[r] holds this lane's partial of row r (NR = 2^m <= 32 rows): returns the
-// sum over all 64 lanes of row (lane >> (6 - m)) & (NR - 1), in a fixed order
-template <int NR>
-__device__ __forceinline__ float rows_reduce(float (&v)[NR], int lane) {
-  constexpr int LEVELS = NR == 32 ? 5 : NR == 16 ? 4 : NR == 8 ? 3 : NR == 4 ? 2 : NR == 2 ? 1 : 0;
-#pragma unroll
-  for (int lev = 0; lev < LEVELS; ++lev) {
-    const int msk = 32 >> lev, half = NR >> (lev + 1);
-    const bool hi = (lane & msk) != 0;
-#pragma unroll
-    for (int i = 0; i < half; ++i) {
-      const float send = hi ? v[i] : v[half + i];
-      const float keep = hi ? v[half + i] : v[i];
-      v[i] = keep + __shfl_xor(send, msk);
-    }
+// part[tid] = sum over k in group q's range of W(k, j) * x[k], (q, j) = (tid / NOUT, tid % NOUT),
+// W(k, j) = Wp[k * sk + j * sj]; j >= nout or an empty range gives 0
+template <int NOUT>
+__device__ __forceinline__ void splitk_part(const float* __restrict__ Wp, int sk, int sj, int K,
+                                            const float* x, int nout, float* part, int tid) {
+  constexpr int NQ = HT / NOUT;
+  const int j = tid % NOUT, q = tid / NOUT;
+  const int kc = (K + NQ - 1) / NQ, k0 = q * kc, k1 = min(K, k0 + kc);
+  float acc = 0.f;
+  if (j < nout) {
+    const float* wp = Wp + (size_t)j * sj;
+#pragma unroll 16
+    for (int k = k0; k < k1; ++k) acc = fmaf(wp[(size_t)k * sk], x[k], acc);
   }
-  float s = v[0];
-#pragma unroll
-  for (int msk = 32 >> LEVELS; msk >= 1; msk >>= 1) s += __shfl_xor(s, msk);
-  return s;
+  part[tid] = acc;
 }
-
-// out[row0 + r] = act(bias + W[row0 + r][0:K] . x[0:K]) for r < NR, rows < nrows;
-// x in LDS; KC = ceil(K / 64) column chunks
-template <int NR, int KC, bool RELU>
-__device__ __forceinline__ void rows_layer(const float* __restrict__ W, int ldw, int K,
-                                           const float* __restrict__ bias, const float* x, int row0,
-                                           int nrows, float* out, int lane) {
-  float xv[KC];
+// the NQ group partials of output j, in group order
+template <int NOUT>
+__device__ __forceinline__ float splitk_sum(const float* part, int j) {
+  constexpr int NQ = HT / NOUT;
+  float s = part[j];
 #pragma unroll
-  for (int i = 0; i < KC; ++i) xv[i] = (lane + 64 * i < K) ? x[lane + 64 * i] : 0.f;
-  float v[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int row = row0 + r < nrows ? row0 + r : nrows - 1;   // clamped: rows past nrows unused
-    const float* wr = W + (size_t)row * ldw;
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      const int k = lane + 64 * i;
-      acc = fmaf(k < K ? wr[k] : 0.f, xv[i], acc);
-    }
-    v[r] = acc;
-  }
-  constexpr int SH = NR == 32 ? 1 : NR == 16 ? 2 : NR == 8 ? 3 : NR == 4 ? 4 : 5;
-  const float s = rows_reduce<NR>(v, lane);
-  const int row = row0 + ((lane >> SH) & (NR - 1));
-  if ((lane & ((1 << SH) - 1)) == 0 && row < nrows) {
-    const float y = s + bias[row];
-    out[row] = RELU ? fmaxf(y, 0.f) : y;
-  }
+  for (int q = 1; q < NQ; ++q) s += part[q * NOUT + j];
+  return s;
 }
 
 struct HeadRng {  // the train step's own draws (TrainPlan): t ~ U{0..T-1}, noise ~ N(0,1)
@@ -242,12 +275,13 @@ struct HeadRng {  // the train step's own draws (TrainPlan): t ~ U{0..T-1}, nois
 constexpr uint32_t RNG_TAG_T = 0x7A11u, RNG_TAG_NOISE = 0x7A12u;
 
 __device__ __forceinline__ void head_forward(
-    const ertd_weights& w, const float* __restrict__ x_in, const float* __restrict__ x0,
-    const float* __restrict__ noise, const float* __restrict__ alpha_bar,
-    const int64_t* __restrict__ t_vec, const float* __restrict__ freq,
-    const float* __restrict__ partial, int S, int L2, float* __restrict__ V,
-    float* __restrict__ eps_out, const HeadRng* rng, HeadSmem& s, int b, int tid) {
-  const int P = w.param_dim, lane = tid & 63, wave = tid >> 6;
+    const ertd_weights& w, const float* __restrict__ wt, const float* __restrict__ x_in,
+    const float* __restrict__ x0, const float* __restrict__ noise,
+    const float* __restrict__ alpha_bar, const int64_t* __restrict__ t_vec,
+    const float* __restrict__ freq, const float* __restrict__ partial, int S, int L2,
+    float* __restrict__ V, float* __restrict__ eps_out, const HeadRng* rng, HeadSmem& s, int b,
+    int tid) {
+  const int P = w.param_dim;
   if (rng) {  // Philox keyed (seed, member, step): independent of the grid and of the schedule
     const uint32_t st = (uint32_t)*rng->step;
     if (tid == 0) {
@@ -257,21 +291,29 @@ __device__ __forceinline__ void head_forward(
       s.t = tv;
       rng->t_out[b] = tv;
     }
-    if (tid < P) {
-      const float z = philox_normal(rng->seed, (uint32_t)b, st, RNG_TAG_NOISE, tid);
-      s.nz[tid] = z;
-      rng->noise_out[(size_t)b * P + tid] = z;
+    if (tid >= 64 && tid < 64 + P) {
+      const int o = tid - 64;
+      const float z = philox_normal(rng->seed, (uint32_t)b, st, RNG_TAG_NOISE, o);
+      s.nz[o] = z;
+      rng->noise_out[(size_t)b * P + o] = z;
     }
   } else {
     if (tid == 0) s.t = (int)t_vec[b];
-    if (tid < P && noise) s.nz[tid] = noise[(size_t)b * P + tid];
+    if (tid >= 64 && tid < 64 + P && noise) s.nz[tid - 64] = noise[(size_t)b * P + tid - 64];
   }
-  if (tid < C2) {
+  {  // pool: strips k = q, q + 16, ... summed per group q, the groups in order
+    const int c = tid & 63, q = tid >> 6;
     float acc = 0.f;
-    for (int k = 0; k < S; ++k) acc += partial[((size_t)b * S + k) * C2 + tid];
-    s.m[tid] = acc / (float)L2;
+    for (int k = q; k < S; k += HT / 64) acc += partial[((size_t)b * S + k) * C2 + c];
+    s.part[tid] = acc;
   }
   __syncthreads();
+  if (tid < C2) {
+    float acc = s.part[tid];
+#pragma unroll
+    for (int q = 1; q < HT / 64; ++q) acc += s.part[q * 64 + tid];
+    s.m[tid] = acc / (float)L2;
+  }
   const int t = s.t;
   if (tid < P) {
     float xv;
@@ -283,45 +325,50 @@ __device__ __forceinline__ void head_forward(
       xv = sa * x0[(size_t)b * P + tid] + sb * s.nz[tid];
     }
     s.hc[tid] = xv;
-  }
-  if (tid >= H) {
-    const int k = tid - H;
+  } else if (tid >= 256 && tid < 256 + H) {
+    const int k = tid - 256;
     const float a = (float)t * freq[k < 64 ? k : k - 64];
     s.e[k] = k < 64 ? sinf(a) : cosf(a);
   }
   __syncthreads();
-  // cond_emb = relu(W3 m + b3) (waves 0-1), t_emb = relu(Wt e + bt) (waves 2-3)
-  if (wave < 2) {
-    rows_layer<32, 1, true>(w.enc6_w, C2, C2, w.enc6_b, s.m, wave * 64, H, s.c, lane);
-    rows_layer<32, 1, true>(w.enc6_w, C2, C2, w.enc6_b, s.m, wave * 64 + 32, H, s.c, lane);
-  } else {
-    rows_layer<32, 2, true>(w.time_w, H, H, w.time_b, s.e, (wave - 2) * 64, H, s.te, lane);
-    rows_layer<32, 2, true>(w.time_w, H, H, w.time_b, s.e, (wave - 2) * 64 + 32, H, s.te, lane);
+  // cond_emb = relu(W3 m + b3) (outputs 0-127), t_emb = relu(Wt e + bt) (128-255)
+  {
+    const int j = tid & 255;
+    if (j < H) splitk_part<256>(wt + WT_W3, H, 1, C2, s.m, H, s.part, tid);
+    else splitk_part<256>(wt + WT_WT - H, H, 1, H, s.e, 2 * H, s.part, tid);
   }
   __syncthreads();
-  if (tid < H) {
-    s.hc[P + tid] = s.te[tid];
-    s.hc[P + H + tid] = s.c[tid];
+  if (tid < 2 * H) {
+    const float y = splitk_sum<256>(s.part, tid);
+    if (tid < H) {
+      s.c[tid] = fmaxf(y + w.enc6_b[tid], 0.f);
+      s.hc[P + H + tid] = s.c[tid];
+    } else {
+      const int j = tid - H;
+      s.te[j] = fmaxf(y + w.time_b[j], 0.f);
+      s.hc[P + j] = s.te[j];
+    }
   }
   __syncthreads();
   const int K0 = P + 2 * H;
-  // h = relu(W0 hcat + b0)
-  rows_layer<32, (PMAX + 2 * H + 63) / 64, true>(w.mlp0_w, K0, K0, w.mlp0_b, s.hc, wave * 32, H, s.h,
-                                                 lane);
+  splitk_part<128>(wt + WT_W0, H, 1, K0, s.hc, H, s.part, tid);   // h = relu(W0 hcat + b0)
   __syncthreads();
-  // eps = W2 h + b2
-  rows_layer<8, 2, false>(w.mlp2_w, H, H, w.mlp2_b, s.h, wave * 8, P, s.eps, lane);
+  if (tid < H) s.h[tid] = fmaxf(splitk_sum<128>(s.part, tid) + w.mlp0_b[tid], 0.f);
+  __syncthreads();
+  splitk_part<32>(wt + WT_W2, PMAX, 1, H, s.h, P, s.part, tid);    // eps = W2 h + b2
   __syncthreads();
   if (tid < P) {
-    V[TV_EPS + tid] = s.eps[tid];
-    if (eps_out) eps_out[(size_t)b * P + tid] = s.eps[tid];
+    const float y = splitk_sum<32>(s.part, tid) + w.mlp2_b[tid];
+    s.eps[tid] = y;
+    V[TV_EPS + tid] = y;
+    if (eps_out) eps_out[(size_t)b * P + tid] = y;
   }
-  for (int i = tid; i < K0; i += 256) V[TV_HCAT + i] = s.hc[i];
-  if (tid < H) {
-    V[TV_E + tid] = s.e[tid];
-    V[TV_H + tid] = s.h[tid];
+  for (int i = tid; i < K0; i += HT) V[TV_HCAT + i] = s.hc[i];
+  if (tid >= 512 && tid < 512 + H) {
+    V[TV_E + tid - 512] = s.e[tid - 512];
+    V[TV_H + tid - 512] = s.h[tid - 512];
   }
-  if (tid < C2) V[TV_M + tid] = s.m[tid];
+  if (tid >= 768 && tid < 768 + C2) V[TV_M + tid - 768] = s.m[tid - 768];
 }
 
 //   dout: given (autograd) or MSE: (pred - noise) * (2/(B*P))   (mse_loss backward)
@@ -353,33 +400,30 @@ __device__ __forceinline__ void head_backward(
     for (int o = 0; o < P; ++o) acc += s.red[o];
     V[TV_SQ] = acc;
   }
-  if (tid < H) {  // dz5 = (W2^T dout) * [h > 0]
-    float acc = 0.f;
-#pragma unroll 8
-    for (int o = 0; o < P; ++o) acc = fmaf(w.mlp2_w[o * H + tid], s.dout[o], acc);
-    const float d = h_v[tid] > 0.f ? acc : 0.f;
+  splitk_part<128>(w.mlp2_w, H, 1, P, s.dout, H, s.part, tid);   // dz5 = (W2^T dout) * [h > 0]
+  __syncthreads();
+  if (tid < H) {
+    const float d = h_v[tid] > 0.f ? splitk_sum<128>(s.part, tid) : 0.f;
     s.dz5[tid] = d;
     V[TV_DZ5 + tid] = d;
   }
   __syncthreads();
   const int K0 = P + 2 * H;
-  {  // dhcat[P + k] for k < 256 (t_emb and cond_emb columns)
-    float acc = 0.f;
-#pragma unroll 16
-    for (int j = 0; j < H; ++j) acc = fmaf(w.mlp0_w[(size_t)j * K0 + P + tid], s.dz5[j], acc);
-    s.dhc[tid] = acc;
-  }
-  if (dx_out && tid < P) {  // dx = W0x^T dz5 (autograd w.r.t. the model input)
-    float acc = 0.f;
-#pragma unroll 16
-    for (int j = 0; j < H; ++j) acc = fmaf(w.mlp0_w[(size_t)j * K0 + tid], s.dz5[j], acc);
-    dx_out[(size_t)b * P + tid] = acc;
+  // dhcat[P + k] = (W0^T dz5)[P + k] for the t_emb / cond_emb columns
+  splitk_part<256>(w.mlp0_w + P, K0, 1, H, s.dz5, 2 * H, s.part, tid);
+  __syncthreads();
+  if (tid < 2 * H) s.dhc[tid] = splitk_sum<256>(s.part, tid);
+  if (dx_out) {  // dx = W0x^T dz5 (autograd w.r.t. the model input)
+    __syncthreads();
+    splitk_part<32>(w.mlp0_w, K0, 1, H, s.dz5, P, s.part, tid);
+    __syncthreads();
+    if (tid < P) dx_out[(size_t)b * P + tid] = splitk_sum<32>(s.part, tid);
   }
   __syncthreads();
   if (tid < H) {
     const float te = hcat_v[P + tid];
     V[TV_DZ4 + tid] = te > 0.f ? s.dhc[tid] : 0.f;
-  } else {
+  } else if (tid < 2 * H) {
     const int j = tid - H;
     const float c = hcat_v[P + H + j];
     const float d = c > 0.f ? s.dhc[tid] : 0.f;
@@ -387,30 +431,28 @@ __device__ __forceinline__ void head_backward(
     V[TV_DZ3 + j] = d;
   }
   __syncthreads();
-  if (tid < C2) {  // g = (W3^T dz3) / L2  (AdaptiveAvgPool backward)
-    float acc = 0.f;
-#pragma unroll 16
-    for (int j = 0; j < H; ++j) acc = fmaf(w.enc6_w[j * C2 + tid], s.dz3[j], acc);
-    V[TV_G + tid] = acc / (float)L2;
-  }
+  splitk_part<64>(w.enc6_w, C2, 1, H, s.dz3, C2, s.part, tid);   // g = (W3^T dz3) / L2
+  __syncthreads();
+  if (tid < C2) V[TV_G + tid] = splitk_sum<64>(s.part, tid) / (float)L2;
 }
 
 // MODE 0: forward only; 1: backward only (of the last forward's saved row);
 // 2: both (the train step; rng != null: the step draws its own t and noise)
 template <int MODE>
-__global__ __launch_bounds__(256) void train_head_kernel(
-    ertd_weights w, const float* __restrict__ x_in, const float* __restrict__ x0,
-    const float* __restrict__ noise, const float* __restrict__ alpha_bar,
-    const int64_t* __restrict__ t_vec, const float* __restrict__ freq,
-    const float* __restrict__ partial, int S, int L2, float* __restrict__ vec,
-    float* __restrict__ eps_out, const float* __restrict__ dout_in, float two_over_n,
-    float* __restrict__ dx_out, HeadRng rng) {
+__global__ __launch_bounds__(HT) void train_head_kernel(
+    ertd_weights w, const float* __restrict__ wt, const float* __restrict__ x_in,
+    const float* __restrict__ x0, const float* __restrict__ noise,
+    const float* __restrict__ alpha_bar, const int64_t* __restrict__ t_vec,
+    const float* __restrict__ freq, const float* __restrict__ partial, int S, int L2,
+    float* __restrict__ vec, float* __restrict__ eps_out, const float* __restrict__ dout_in,
+    float two_over_n, float* __restrict__ dx_out, HeadRng rng) {
   __shared__ HeadSmem s;
   const int b = blockIdx.x, tid = threadIdx.x;
   float* V = vec + (size_t)b * TV;
   const HeadRng* rp = rng.step ? &rng : nullptr;
   if constexpr (MODE != 1)
-    head_forward(w, x_in, x0, noise, alpha_bar, t_vec, freq, partial, S, L2, V, eps_out, rp, s, b, tid);
+    head_forward(w, wt, x_in, x0, noise, alpha_bar, t_vec, freq, partial, S, L2, V, eps_out, rp, s, b,
+                 tid);
   if constexpr (MODE == 2) {
     __syncthreads();
     head_backward(w, dout_in, s.nz, two_over_n, L2, V, dx_out, s.eps, s.h, s.hc, s, b, tid);
@@ -430,6 +472,9 @@ __global__ __launch_bounds__(256) void train_head_kernel(
 // LDS: phase A's dz2 / a1 images are dead in phase B, where the cond image and
 // the dW1 halves take their place: 51.6 KB -> 3 workgroups per CU.
 // ---------------------------------------------------------------------------
+#ifndef CBW_ABL
+#define CBW_ABL 0  // diagnostic variants only (tools/cbw_abl.sh): bit mask of skipped phases
+#endif
 constexpr int DZ2P = 65;   // dz2 row pitch (column reads conflict-free)
 constexpr int DZ1P = 129;  // dz1 row pitch
 struct ConvBwdSmem {
@@ -448,6 +493,34 @@ struct ConvBwdSmem {
   float db2p[4][C2];         // db2 partial sums of the four q' classes
 };
 
+// acc += sum_s A(s) x B(s) over N k-steps of v_mfma_f32_32x32x2_f32, the
+// operands of step s + AHEAD fetched (LDS reads) before step s's MFMA: a
+// read's latency hides behind AHEAD MFMAs instead of stalling the next one
+template <int N, int AHEAD, class FA, class FB>
+__device__ __forceinline__ void mfma_pipe(f32x16& acc, FA fa, FB fb) {
+  float ra[AHEAD], rb[AHEAD];
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i) {
+    ra[i] = fa(i);
+    rb[i] = fb(i);
+  }
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const float a = ra[s % AHEAD], b = rb[s % AHEAD];
+    if (s + AHEAD < N) {
+      ra[s % AHEAD] = fa(s + AHEAD);
+      rb[s % AHEAD] = fb(s + AHEAD);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    // keep the order: this step's reads (for s + AHEAD), then its MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  }
+}
+#ifndef CBW_AHEAD
+#define CBW_AHEAD 6
+#endif
+
 __device__ __forceinline__ void store_tile_rows(float (*red)[33], const f32x16& acc, int h, int l32) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[(r & 3) + 8 * (r >> 2) + 4 * h][l32] = acc[r];
@@ -462,11 +535,9 @@ __device__ __forceinline__ void dw2_tile(const ConvBwdSmem& sm, int tt, int h, i
   const float* ab = kk == 1 ? &sm.AO[c][h] : &sm.AE[c][h + (kk == 2 ? 1 : 0)];
   const float* zb = &sm.DZ2[ot * 32 + l32][h];
   f32x16 acc = {};
-#pragma unroll 8
-  for (int s = 0; s < 32; ++s) {
-    const float bv = (2 * s + h < J) ? ab[2 * s] : 0.f;  // q' = 63 is the halo: excluded
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(zb[2 * s], bv, acc, 0, 0, 0);
-  }
+  mfma_pipe<32, CBW_AHEAD>(acc, [&](int s) { return zb[2 * s]; },
+                           // q' = 63 is the halo: excluded
+                           [&](int s) { return (2 * s + h < J) ? ab[2 * s] : 0.f; });
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int o = ot * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -475,7 +546,7 @@ __device__ __forceinline__ void dw2_tile(const ConvBwdSmem& sm, int tt, int h, i
 }
 
 __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
-    const float* __restrict__ w2, const float* __restrict__ cond, const float* __restrict__ a1s,
+    const float* __restrict__ w2b, const float* __restrict__ cond, const float* __restrict__ a1s,
     const uint32_t* __restrict__ m2w, const float* __restrict__ g, int g_stride, int L, int L1,
     int L2, int S, float* __restrict__ gpart) {
   __shared__ __attribute__((aligned(16))) ConvBwdSmem sm;
@@ -487,16 +558,16 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
   float* G = gpart + (size_t)item * NG;
 
   // ---- transposed-conv2 fragments (the da1 A operand) first, into registers:
-  //   T_kk[s][lane] = W2[o = 2s + h][c = l32][kk]; even waves tap 1, odd waves taps 0 and 2
+  //   W2B[kk][s][lane] = W2[o = 2s + h][c = l32][kk]; even waves tap 1, odd waves taps 0 and 2
   const bool oddw = wave >= 2;
   float wt0[32], wt1[32];
   {
-    const float* base = w2 + h * K2 + l32 * 3;
+    const float* base = w2b + lane;
     const int k0 = oddw ? 0 : 1;
 #pragma unroll
-    for (int s = 0; s < 32; ++s) wt0[s] = base[s * 2 * K2 + k0];
+    for (int s = 0; s < 32; ++s) wt0[s] = base[(k0 * 32 + s) * 64];
 #pragma unroll
-    for (int s = 0; s < 32; ++s) wt1[s] = oddw ? base[s * 2 * K2 + 2] : 0.f;
+    for (int s = 0; s < 32; ++s) wt1[s] = oddw ? base[(2 * 32 + s) * 64] : 0.f;
   }
   // ---- the cond strip (phase B's image), loaded now, stored after phase A
   const float* cb = cond + (size_t)b * CIN * L;
@@ -559,19 +630,16 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     const int mcol = mt * 32 + l32;
     const float* db = &sm.DZ2[0][0] + h * DZ2P + mcol;
     f32x16 acc = {};
-    if (!oddw) {
+    if ((CBW_ABL & 1) != 0) {
+      for (int k = 0; k < 16; ++k) acc[k] = db[k] + wt0[k] + wt1[k];
+    } else if (!oddw) {
       // r = 2m: da1 = sum_o W2[o][c][1] dz2[o][m]
-#pragma unroll 8
-      for (int s = 0; s < 32; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wt0[s], db[2 * s * DZ2P], acc, 0, 0, 0);
+      mfma_pipe<32, CBW_AHEAD>(acc, [&](int s) { return wt0[s]; }, [&](int s) { return db[2 * s * DZ2P]; });
     } else {
       // r = 2m+1: da1 = sum_o W2[o][c][0] dz2[o][m+1] + W2[o][c][2] dz2[o][m]
-#pragma unroll 8
-      for (int s = 0; s < 32; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wt0[s], db[2 * s * DZ2P + 1], acc, 0, 0, 0);
-#pragma unroll 8
-      for (int s = 0; s < 32; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wt1[s], db[2 * s * DZ2P], acc, 0, 0, 0);
+      mfma_pipe<32, CBW_AHEAD>(acc, [&](int s) { return wt0[s]; },
+                               [&](int s) { return db[2 * s * DZ2P + 1]; });
+      mfma_pipe<32, CBW_AHEAD>(acc, [&](int s) { return wt1[s]; }, [&](int s) { return db[2 * s * DZ2P]; });
     }
     const int odd = oddw ? 1 : 0;
     const int r = 2 * mcol + odd;
@@ -583,9 +651,11 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
       sm.DZ1[c][r] = (owned && act > 0.f) ? acc[k] : 0.f;
     }
   }
-  if (wave == 0) { dw2_tile(sm, 0, h, l32, G); dw2_tile(sm, 1, h, l32, G); }
-  else if (wave == 1) { dw2_tile(sm, 2, h, l32, G); dw2_tile(sm, 3, h, l32, G); }
-  else dw2_tile(sm, 2 + wave, h, l32, G);
+  if constexpr ((CBW_ABL & 2) == 0) {
+    if (wave == 0) { dw2_tile(sm, 0, h, l32, G); dw2_tile(sm, 1, h, l32, G); }
+    else if (wave == 1) { dw2_tile(sm, 2, h, l32, G); dw2_tile(sm, 3, h, l32, G); }
+    else dw2_tile(sm, 2 + wave, h, l32, G);
+  }
   __syncthreads();
 
   // ---- cond image into the dead dz2 region; db2
@@ -607,14 +677,21 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     const float* xb = &sm.X[u0 & 3][c][u0 >> 2];
     const float* zb = &sm.DZ1[l32][h];
     f32x16 acc = {};
-#pragma unroll 8
-    for (int s = rh * 32; s < rh * 32 + 32; ++s) {
-      const float bv = nvalid ? xb[s] : pad;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(zb[2 * s], bv, acc, 0, 0, 0);
+    if constexpr ((CBW_ABL & 4) != 0) {
+      for (int k = 0; k < 16; ++k) acc[k] = zb[2 * k] + xb[k] + pad;
+    } else {
+      const float* zr = zb + 64 * rh;
+      const float* xr = xb + 32 * rh;
+      mfma_pipe<32, CBW_AHEAD>(acc, [&](int s) { return zr[2 * s]; },
+                               [&](int s) { return nvalid ? xr[s] : pad; });
     }
     store_tile_rows(sm.red[wave], acc, h, l32);  // red aliases the dead a1 images
   }
   __syncthreads();
+  if constexpr ((CBW_ABL & 8) != 0) {
+    if (item >= 0x7fffffff) G[tid] = sm.red[0][0][tid & 31];
+    return;
+  }
   for (int idx = tid; idx < C1 * K1; idx += 256) {  // r-halves combined in order
     const int o = idx / K1, n = idx - o * K1;
     const int nt = n >> 5, col = n & 31;
@@ -696,6 +773,8 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   __shared__ float4 red[4][FIN_CB_COLS];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // Adam's scalars first: their (dependent) loads overlap the gradient loads
+  const AdamHyper hy = a.param[0] ? fetch_hyper(a) : AdamHyper{};
   if ((int)blockIdx.x < FIN_NCB * FIN_RB) {
     const int cb = blockIdx.x / FIN_RB, rb = blockIdx.x - cb * FIN_RB;
     const int col4 = cb * FIN_CB_COLS + lane;
@@ -760,7 +839,6 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) gd[off + q] = gv[q];
     if (a.param[0]) {
-      const AdamHyper hy = fetch_hyper(a);
 #pragma unroll
       for (int q = 0; q < 4; ++q) adam_elem(a.param[k], a.m[k], a.v[k], off + q, gv[q], hy);
     }
@@ -800,7 +878,7 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
     for (int b = 0; b < a.B; ++b) acc = fmaf(pd[(size_t)b * TV], pi[(size_t)b * TV], acc);
   }
   a.grad[k][i] = acc;
-  if (a.param[0]) adam_elem(a.param[k], a.m[k], a.v[k], i, acc, fetch_hyper(a));
+  if (a.param[0]) adam_elem(a.param[k], a.m[k], a.v[k], i, acc, hy);
 }
 
 // ---------------------------------------------------------------------------
@@ -858,6 +936,8 @@ struct TrainWs {
   float* fin;      // (FIN_RB, NG)
   unsigned* cnt;   // (FIN_CNT_WORDS)
   float* vec;      // (B, TV); the reference train step only
+  float* wt;       // (WT_FLOATS) k-major dense weights; the reference train step only
+  float* w2b;      // (W2B_FRAG) transposed-conv2 fragments
 };
 
 // the encoder part (also the U-Net's condition branch), then the member rows
@@ -873,7 +953,11 @@ size_t ws_layout(int B, int L, bool with_vec, float* base, TrainWs* out) {
   w.gpart = base + o; o += al(items * NG);
   w.fin = base + o; o += al((size_t)FIN_RB * NG);
   w.cnt = reinterpret_cast<unsigned*>(base + o); o += al(FIN_CNT_WORDS);
-  if (with_vec) { w.vec = base + o; o += al((size_t)B * TV); }
+  w.w2b = base + o; o += al(W2B_FRAG);
+  if (with_vec) {
+    w.vec = base + o; o += al((size_t)B * TV);
+    w.wt = base + o; o += al(WT_FLOATS);
+  }
   if (out) *out = w;
   return o;
 }
@@ -906,18 +990,23 @@ void set_dense(FinalArgs& a, const ertd_weights& w, const TrainWs& W, int B, flo
   a.loss = loss_out;
 }
 
+// wd: the model's dense weights (their k-major copies go to W.wt), or null
 hipError_t launch_enc(const float* w1, const float* b1, const float* w2, const float* b2,
-                      const float* cond, int B, int L, const TrainWs& W, int* step_ctr, hipStream_t s) {
+                      const float* cond, int B, int L, const TrainWs& W, int* step_ctr,
+                      const ertd_weights* wd, hipStream_t s) {
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
   enc_train_kernel<<<dim3((unsigned)(B * S)), 256, 0, s>>>(w1, b1, w2, b2, cond, L, L1, L2, S, W.partial,
-                                                         W.a1s, W.m2w, W.cnt, step_ctr);
+                                                         W.a1s, W.m2w, W.cnt, step_ctr,
+                                                         wd ? *wd : ertd_weights{}, wd ? W.wt : nullptr,
+                                                         W.w2b);
   return hipGetLastError();
 }
 
-hipError_t launch_conv_bwd(const float* w2, const float* cond, const TrainWs& W, const float* g,
-                           int g_stride, int B, int L, hipStream_t s) {
+// (the W2 fragments are the ones the forward on this workspace wrote)
+hipError_t launch_conv_bwd(const float* cond, const TrainWs& W, const float* g, int g_stride, int B,
+                           int L, hipStream_t s) {
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
-  conv_bwd_kernel<<<dim3((unsigned)(B * S)), 256, 0, s>>>(w2, cond, W.a1s, W.m2w, g, g_stride, L, L1,
+  conv_bwd_kernel<<<dim3((unsigned)(B * S)), 256, 0, s>>>(W.w2b, cond, W.a1s, W.m2w, g, g_stride, L, L1,
                                                         L2, S, W.gpart);
   return hipGetLastError();
 }
@@ -941,10 +1030,10 @@ hipError_t launch_train_forward(const ertd_weights& w, const float* x_in, const 
   TrainWs W;
   ws_layout(B, L, true, ws, &W);
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
-  hipError_t e = launch_enc(w.enc0_w, w.enc0_b, w.enc2_w, w.enc2_b, cond, B, L, W, nullptr, s);
+  hipError_t e = launch_enc(w.enc0_w, w.enc0_b, w.enc2_w, w.enc2_b, cond, B, L, W, nullptr, &w, s);
   if (e != hipSuccess) return e;
-  train_head_kernel<0><<<B, 256, 0, s>>>(w, x_in, x0, noise, alpha_bar, t, freq, W.partial, S, L2,
-                                         W.vec, eps_out, nullptr, 0.f, nullptr, HeadRng{});
+  train_head_kernel<0><<<B, HT, 0, s>>>(w, W.wt, x_in, x0, noise, alpha_bar, t, freq, W.partial, S, L2,
+                                        W.vec, eps_out, nullptr, 0.f, nullptr, HeadRng{});
   return hipGetLastError();
 }
 
@@ -956,10 +1045,10 @@ hipError_t launch_train_backward(const ertd_weights& w, const float* dout, const
   const int P = w.param_dim;
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
   const float two_over_n = (float)(2.0 / ((double)B * P));
-  train_head_kernel<1><<<B, 256, 0, s>>>(w, nullptr, nullptr, noise, nullptr, nullptr, nullptr,
-                                         nullptr, S, L2, W.vec, nullptr, dout, two_over_n, dx_out,
-                                         HeadRng{});
-  hipError_t e = launch_conv_bwd(w.enc2_w, cond, W, W.vec + TV_G, TV, B, L, s);
+  train_head_kernel<1><<<B, HT, 0, s>>>(w, W.wt, nullptr, nullptr, noise, nullptr, nullptr, nullptr,
+                                        nullptr, S, L2, W.vec, nullptr, dout, two_over_n, dx_out,
+                                        HeadRng{});
+  hipError_t e = launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, s);
   if (e != hipSuccess) return e;
   FinalArgs a = final_args(W, B * S);
   set_dense(a, w, W, B, grads, loss_out);
@@ -976,7 +1065,8 @@ hipError_t launch_train_step(const ertd_weights& w, const float* x0, const int64
   const int P = w.param_dim;
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
   const float two_over_n = (float)(2.0 / ((double)B * P));
-  hipError_t e = launch_enc(w.enc0_w, w.enc0_b, w.enc2_w, w.enc2_b, cond, B, L, W, adam.step_dev, s);
+  hipError_t e =
+      launch_enc(w.enc0_w, w.enc0_b, w.enc2_w, w.enc2_b, cond, B, L, W, adam.step_dev, &w, s);
   if (e != hipSuccess) return e;
   HeadRng rng{};
   if (adam.draw) {
@@ -986,9 +1076,9 @@ hipError_t launch_train_step(const ertd_weights& w, const float* x0, const int64
     rng.t_out = const_cast<int64_t*>(t);
     rng.noise_out = const_cast<float*>(noise);
   }
-  train_head_kernel<2><<<B, 256, 0, s>>>(w, nullptr, x0, noise, alpha_bar, t, freq, W.partial, S, L2,
-                                         W.vec, nullptr, nullptr, two_over_n, nullptr, rng);
-  e = launch_conv_bwd(w.enc2_w, cond, W, W.vec + TV_G, TV, B, L, s);
+  train_head_kernel<2><<<B, HT, 0, s>>>(w, W.wt, nullptr, x0, noise, alpha_bar, t, freq, W.partial, S,
+                                        L2, W.vec, nullptr, nullptr, two_over_n, nullptr, rng);
+  e = launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, s);
   if (e != hipSuccess) return e;
   FinalArgs a = final_args(W, B * S);
   set_dense(a, w, W, B, grads, loss_out);
@@ -1021,7 +1111,7 @@ hipError_t launch_encoder_train(const float* w1, const float* b1, const float* w
   TrainWs W;
   ws_layout(B, L, false, ws, &W);
   *partial_out = W.partial;
-  return launch_enc(w1, b1, w2, b2, cond, B, L, W, nullptr, s);
+  return launch_enc(w1, b1, w2, b2, cond, B, L, W, nullptr, nullptr, s);
 }
 
 hipError_t launch_encoder_conv_backward(const float* w2, const float* cond, const float* g, int B,
@@ -1030,7 +1120,8 @@ hipError_t launch_encoder_conv_backward(const float* w2, const float* cond, cons
   TrainWs W;
   ws_layout(B, L, false, ws, &W);
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
-  hipError_t e = launch_conv_bwd(w2, cond, W, g, C2, B, L, s);
+  (void)w2;  // the fragments of the forward on this workspace
+  hipError_t e = launch_conv_bwd(cond, W, g, C2, B, L, s);
   if (e != hipSuccess) return e;
   FinalArgs a = final_args(W, B * S);
   a.grad[0] = dw1;
