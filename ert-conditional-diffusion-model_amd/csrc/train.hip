@@ -60,7 +60,8 @@ constexpr int WT_W3 = 0;                    // [64][128]   W3T[k][j] = W3[j][k]
 constexpr int WT_WT = WT_W3 + C2 * H;       // [128][128]  time_embed.0
 constexpr int WT_W0 = WT_WT + H * H;        // [K0][128]   mlp.0 (K0 = P + 256 <= 288)
 constexpr int WT_W2 = WT_W0 + (PMAX + 2 * H) * H;  // [128][32] mlp.2: W2T[k][o]
-constexpr int WT_FLOATS = WT_W2 + H * PMAX;
+constexpr int WT_W0B = WT_W2 + H * PMAX;    // [128][256]  mlp.0 columns P.. (16-B aligned rows): W0[j][P + k]
+constexpr int WT_FLOATS = WT_W0B + H * 2 * H;
 
 constexpr int W2B_FRAG = 3 * 32 * 64;  // transposed-conv2 fragments (conv_bwd)
 // train_final_kernel's conv-column reduction (see there)
@@ -106,9 +107,12 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
       } else if (e < WT_W2) {
         const int i = e - WT_W0, k = i >> 7;
         v = k < K0 ? wd.mlp0_w[(size_t)(i & (H - 1)) * K0 + k] : 0.f;
-      } else {
+      } else if (e < WT_W0B) {
         const int i = e - WT_W2, o = i & (PMAX - 1);
         v = o < P ? wd.mlp2_w[o * H + (i >> 5)] : 0.f;
+      } else {
+        const int i = e - WT_W0B;
+        v = wd.mlp0_w[(size_t)(i >> 8) * K0 + P + (i & 255)];
       }
       wt[e] = v;
     }
@@ -232,11 +236,21 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
 // output index).
 // ---------------------------------------------------------------------------
 constexpr int HT = 1024;  // head block threads
+#ifndef HEAD_ABL
+#define HEAD_ABL 0  // diagnostic variants only: bit 0 no sin/cos, bit 1 no V stores, bit 2 no weight loads
+#endif
+#ifdef HEAD_STAMPS   // diagnostic build only: phase times of block 0 (tools/train_ref_probe.py)
+__device__ unsigned long long g_hstamp[64];
+#define HSTAMP(i) \
+  do { if (blockIdx.x == 0 && threadIdx.x == 0) g_hstamp[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define HSTAMP(i) do { } while (0)
+#endif
 struct HeadSmem {
   float m[C2], e[H], c[H], te[H], hc[PMAX + 2 * H], h[H], eps[PMAX], nz[PMAX];
   float dout[PMAX], dz5[H], dhc[PMAX + 2 * H], dz3[H], red[PMAX];
   float part[HT];
-  int t;
+  float4 part4[HT];
 };
 
 // part[tid] = sum over k in group q's range of W(k, j) * x[k], (q, j) = (tid / NOUT, tid % NOUT),
@@ -255,6 +269,82 @@ __device__ __forceinline__ void splitk_part(const float* __restrict__ Wp, int sk
   }
   part[tid] = acc;
 }
+// the same split with the weight slice loaded into registers ahead of time
+// (the weights do not depend on the activations: a layer's loads are issued
+// before the layers it waits for); the same fma order as splitk_part
+template <int NOUT, int KCM>
+struct SplitK {
+  float w[KCM];
+  int k0, k1;
+  __device__ __forceinline__ void load(const float* __restrict__ Wp, int sk, int sj, int K, int nout,
+                                       int tid) {
+    constexpr int NQ = HT / NOUT;
+    const int j = tid % NOUT, q = tid / NOUT;
+    const int kc = (K + NQ - 1) / NQ;
+    k0 = q * kc;
+    k1 = min(K, k0 + kc);
+    if (j >= nout) k1 = k0;
+    const float* wp = Wp + (size_t)(j < nout ? j : 0) * sj;
+#pragma unroll
+    for (int i = 0; i < KCM; ++i) {
+      const int k = k0 + i;
+      if constexpr ((HEAD_ABL & 4) != 0) w[i] = k < k1 ? 1e-3f * (float)(k + j) : 0.f;
+      else w[i] = k < k1 ? wp[(size_t)k * sk] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void part(const float* x, float* part, int tid) const {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < KCM; ++i)
+      if (k0 + i < k1) acc = fmaf(w[i], x[k0 + i], acc);
+    part[tid] = acc;
+  }
+};
+// float4 form: thread (q, j4) owns outputs 4 j4 .. 4 j4 + 3 and the k range of
+// group q (NQ groups, NOUT / 4 * NQ <= HT threads active); the weights are
+// rows W[k][0 .. NOUT) with a 16-B aligned pitch sk, loaded ahead as float4s
+// (a quarter of the load instructions of the scalar form); partials to part4
+template <int NOUT, int NQ, int KCM>
+struct SplitK4 {
+  static_assert(NOUT / 4 * NQ <= HT, "threads");
+  float4 w[KCM];
+  int k0, k1;
+  __device__ __forceinline__ void load(const float* __restrict__ Wp, int sk, int K, int tid) {
+    constexpr int NJ = NOUT / 4;
+    const int j4 = tid % NJ, q = tid / NJ;
+    const int kc = (K + NQ - 1) / NQ;
+    k0 = q * kc;
+    k1 = q < NQ ? min(K, k0 + kc) : k0;
+#pragma unroll
+    for (int i = 0; i < KCM; ++i) {
+      const int k = k0 + i;
+      w[i] = k < k1 ? *reinterpret_cast<const float4*>(Wp + (size_t)k * sk + 4 * j4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ __forceinline__ void part(const float* x, float4* part4, int tid) const {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < KCM; ++i)
+      if (k0 + i < k1) {
+        const float xv = x[k0 + i];
+        acc.x = fmaf(w[i].x, xv, acc.x);
+        acc.y = fmaf(w[i].y, xv, acc.y);
+        acc.z = fmaf(w[i].z, xv, acc.z);
+        acc.w = fmaf(w[i].w, xv, acc.w);
+      }
+    if (tid < NOUT / 4 * NQ) part4[tid] = acc;
+  }
+  // output j: the NQ group partials in group order
+  __device__ __forceinline__ static float sum(const float4* part4, int j) {
+    constexpr int NJ = NOUT / 4;
+    const float* p = reinterpret_cast<const float*>(part4) + 4 * (j >> 2) + (j & 3);
+    float s = p[0];
+#pragma unroll
+    for (int q = 1; q < NQ; ++q) s += p[4 * NJ * q];
+    return s;
+  }
+};
 // the NQ group partials of output j, in group order
 template <int NOUT>
 __device__ __forceinline__ float splitk_sum(const float* part, int j) {
@@ -281,16 +371,17 @@ __device__ __forceinline__ void head_forward(
     const float* __restrict__ freq, const float* __restrict__ partial, int S, int L2,
     float* __restrict__ V, float* __restrict__ eps_out, const HeadRng* rng, HeadSmem& s, int b,
     int tid) {
+  HSTAMP(0);
   const int P = w.param_dim;
+  // this member's t, known to every thread (no LDS round trip before the
+  // loads that depend on it)
+  int tme;
   if (rng) {  // Philox keyed (seed, member, step): independent of the grid and of the schedule
     const uint32_t st = (uint32_t)*rng->step;
-    if (tid == 0) {
-      const u32x4 r = philox4x32_10(u32x4{0u, (uint32_t)b, st, RNG_TAG_T}, (uint32_t)rng->seed,
-                                    (uint32_t)(rng->seed >> 32));
-      const int tv = (int)(((uint64_t)r.x * (uint64_t)rng->T) >> 32);
-      s.t = tv;
-      rng->t_out[b] = tv;
-    }
+    const u32x4 r = philox4x32_10(u32x4{0u, (uint32_t)b, st, RNG_TAG_T}, (uint32_t)rng->seed,
+                                  (uint32_t)(rng->seed >> 32));
+    tme = (int)(((uint64_t)r.x * (uint64_t)rng->T) >> 32);
+    if (tid == 0) rng->t_out[b] = tme;
     if (tid >= 64 && tid < 64 + P) {
       const int o = tid - 64;
       const float z = philox_normal(rng->seed, (uint32_t)b, st, RNG_TAG_NOISE, o);
@@ -298,71 +389,88 @@ __device__ __forceinline__ void head_forward(
       rng->noise_out[(size_t)b * P + o] = z;
     }
   } else {
-    if (tid == 0) s.t = (int)t_vec[b];
+    tme = (int)t_vec[b];
     if (tid >= 64 && tid < 64 + P && noise) s.nz[tid - 64] = noise[(size_t)b * P + tid - 64];
   }
+  // the loads of the later phases that need no activation, issued now
+  float ab = 0.f, x0v = 0.f, frq = 0.f, bce = 0.f, bh = 0.f, be = 0.f;
+  if (tid < P) {
+    if (x_in) x0v = x_in[(size_t)b * P + tid];
+    else {
+      ab = alpha_bar[tme];
+      x0v = x0[(size_t)b * P + tid];
+    }
+    be = w.mlp2_b[tid];
+  }
+  if (tid >= 256 && tid < 256 + H) frq = freq[(tid - 256) & 63];
+  if (tid < 2 * H) bce = tid < H ? w.enc6_b[tid] : w.time_b[tid - H];
+  if (tid < H) bh = w.mlp0_b[tid];
+  // every forward layer's weight slice into registers now (k-major copies)
+  const int K0 = P + 2 * H;
+  // cond_emb (j4 < 32: outputs 0-127, K 64) and t_emb (j4 >= 32: 128-255, K 128) in one split:
+  // 16 groups of 4 / 8 k each
+  SplitK4<256, 16, 8> wce;
+  if ((tid & 63) < 32) wce.load(wt + WT_W3, H, C2, tid);
+  else wce.load(wt + WT_WT - H, H, H, tid);
+  SplitK4<128, 32, (PMAX + 2 * H + 31) / 32> wh;
+  wh.load(wt + WT_W0, H, K0, tid);
+  SplitK4<PMAX, 32, H / 32> we;
+  we.load(wt + WT_W2, PMAX, H, tid);
   {  // pool: strips k = q, q + 16, ... summed per group q, the groups in order
     const int c = tid & 63, q = tid >> 6;
     float acc = 0.f;
     for (int k = q; k < S; k += HT / 64) acc += partial[((size_t)b * S + k) * C2 + c];
     s.part[tid] = acc;
   }
-  __syncthreads();
+  __syncthreads(); HSTAMP(1);
   if (tid < C2) {
     float acc = s.part[tid];
 #pragma unroll
     for (int q = 1; q < HT / 64; ++q) acc += s.part[q * 64 + tid];
     s.m[tid] = acc / (float)L2;
   }
-  const int t = s.t;
   if (tid < P) {
-    float xv;
-    if (x_in) {
-      xv = x_in[(size_t)b * P + tid];
-    } else {  // q_sample (:97-99): one rounding per op
-      const float ab = alpha_bar[t];
+    float xv = x0v;
+    if (!x_in) {  // q_sample (:97-99): one rounding per op
       const float sa = sqrtf(ab), sb = sqrtf(1.0f - ab);
-      xv = sa * x0[(size_t)b * P + tid] + sb * s.nz[tid];
+      xv = sa * x0v + sb * s.nz[tid];
     }
     s.hc[tid] = xv;
   } else if (tid >= 256 && tid < 256 + H) {
     const int k = tid - 256;
-    const float a = (float)t * freq[k < 64 ? k : k - 64];
-    s.e[k] = k < 64 ? sinf(a) : cosf(a);
+    const float a = (float)tme * frq;
+    if constexpr ((HEAD_ABL & 1) != 0) s.e[k] = a * 1e-3f;
+    else s.e[k] = k < 64 ? sinf(a) : cosf(a);
   }
-  __syncthreads();
+  __syncthreads(); HSTAMP(2);
   // cond_emb = relu(W3 m + b3) (outputs 0-127), t_emb = relu(Wt e + bt) (128-255)
-  {
-    const int j = tid & 255;
-    if (j < H) splitk_part<256>(wt + WT_W3, H, 1, C2, s.m, H, s.part, tid);
-    else splitk_part<256>(wt + WT_WT - H, H, 1, H, s.e, 2 * H, s.part, tid);
-  }
-  __syncthreads();
+  wce.part((tid & 63) < 32 ? s.m : s.e, s.part4, tid);
+  __syncthreads(); HSTAMP(3);
   if (tid < 2 * H) {
-    const float y = splitk_sum<256>(s.part, tid);
+    const float y = SplitK4<256, 16, 8>::sum(s.part4, tid);
     if (tid < H) {
-      s.c[tid] = fmaxf(y + w.enc6_b[tid], 0.f);
+      s.c[tid] = fmaxf(y + bce, 0.f);
       s.hc[P + H + tid] = s.c[tid];
     } else {
       const int j = tid - H;
-      s.te[j] = fmaxf(y + w.time_b[j], 0.f);
+      s.te[j] = fmaxf(y + bce, 0.f);
       s.hc[P + j] = s.te[j];
     }
   }
-  __syncthreads();
-  const int K0 = P + 2 * H;
-  splitk_part<128>(wt + WT_W0, H, 1, K0, s.hc, H, s.part, tid);   // h = relu(W0 hcat + b0)
-  __syncthreads();
-  if (tid < H) s.h[tid] = fmaxf(splitk_sum<128>(s.part, tid) + w.mlp0_b[tid], 0.f);
-  __syncthreads();
-  splitk_part<32>(wt + WT_W2, PMAX, 1, H, s.h, P, s.part, tid);    // eps = W2 h + b2
-  __syncthreads();
+  __syncthreads(); HSTAMP(4);
+  wh.part(s.hc, s.part4, tid);   // h = relu(W0 hcat + b0)
+  __syncthreads(); HSTAMP(5);
+  if (tid < H) s.h[tid] = fmaxf(SplitK4<128, 32, (PMAX + 2 * H + 31) / 32>::sum(s.part4, tid) + bh, 0.f);
+  __syncthreads(); HSTAMP(6);
+  we.part(s.h, s.part4, tid);    // eps = W2 h + b2
+  __syncthreads(); HSTAMP(7);
   if (tid < P) {
-    const float y = splitk_sum<32>(s.part, tid) + w.mlp2_b[tid];
+    const float y = SplitK4<PMAX, 32, H / 32>::sum(s.part4, tid) + be;
     s.eps[tid] = y;
     V[TV_EPS + tid] = y;
     if (eps_out) eps_out[(size_t)b * P + tid] = y;
   }
+  if constexpr ((HEAD_ABL & 2) != 0) return;
   for (int i = tid; i < K0; i += HT) V[TV_HCAT + i] = s.hc[i];
   if (tid >= 512 && tid < 512 + H) {
     V[TV_E + tid - 512] = s.e[tid - 512];
@@ -375,10 +483,20 @@ __device__ __forceinline__ void head_forward(
 // eps_v / h_v / hcat_v / nz_v: the forward's prediction, relu(z5), [x | t_emb |
 // cond_emb] and noise (LDS in the fused kernel; the saved row / the noise input otherwise)
 __device__ __forceinline__ void head_backward(
-    const ertd_weights& w, const float* __restrict__ dout_in, const float* nz_v, float two_over_n,
+    const ertd_weights& w, const float* __restrict__ wt, const float* __restrict__ dout_in,
+    const float* nz_v, float two_over_n,
     int L2, float* __restrict__ V, float* __restrict__ dx_out, const float* eps_v, const float* h_v,
     const float* hcat_v, HeadSmem& s, int b, int tid) {
   const int P = w.param_dim;
+  const int K0 = P + 2 * H;
+  // every backward layer's weight slice into registers now (W itself: rows
+  // contiguous in the output index)
+  SplitK4<H, 8, PMAX / 8> w5;            // dz5: W2 rows (o), 128 columns
+  w5.load(w.mlp2_w, H, P, tid);
+  SplitK4<2 * H, 16, H / 16> w0;          // dhcat: W0B rows (j), 256 columns
+  w0.load(wt + WT_W0B, 2 * H, H, tid);
+  SplitK4<C2, 16, H / 16> w3;             // g: W3 rows (j), 64 columns
+  w3.load(w.enc6_w, C2, H, tid);
   if (tid < PMAX) {
     float d = 0.f, sq = 0.f;
     if (tid < P) {
@@ -394,32 +512,31 @@ __device__ __forceinline__ void head_backward(
     s.red[tid] = sq;
     V[TV_DOUT + tid] = d;
   }
-  __syncthreads();
+  __syncthreads(); HSTAMP(8);
   if (tid == 0) {
     float acc = 0.f;
     for (int o = 0; o < P; ++o) acc += s.red[o];
     V[TV_SQ] = acc;
   }
-  splitk_part<128>(w.mlp2_w, H, 1, P, s.dout, H, s.part, tid);   // dz5 = (W2^T dout) * [h > 0]
-  __syncthreads();
+  w5.part(s.dout, s.part4, tid);   // dz5 = (W2^T dout) * [h > 0]
+  __syncthreads(); HSTAMP(9);
   if (tid < H) {
-    const float d = h_v[tid] > 0.f ? splitk_sum<128>(s.part, tid) : 0.f;
+    const float d = h_v[tid] > 0.f ? SplitK4<H, 8, PMAX / 8>::sum(s.part4, tid) : 0.f;
     s.dz5[tid] = d;
     V[TV_DZ5 + tid] = d;
   }
-  __syncthreads();
-  const int K0 = P + 2 * H;
+  __syncthreads(); HSTAMP(10);
   // dhcat[P + k] = (W0^T dz5)[P + k] for the t_emb / cond_emb columns
-  splitk_part<256>(w.mlp0_w + P, K0, 1, H, s.dz5, 2 * H, s.part, tid);
-  __syncthreads();
-  if (tid < 2 * H) s.dhc[tid] = splitk_sum<256>(s.part, tid);
+  w0.part(s.dz5, s.part4, tid);
+  __syncthreads(); HSTAMP(11);
+  if (tid < 2 * H) s.dhc[tid] = SplitK4<2 * H, 16, H / 16>::sum(s.part4, tid);
   if (dx_out) {  // dx = W0x^T dz5 (autograd w.r.t. the model input)
-    __syncthreads();
+    __syncthreads(); HSTAMP(12);
     splitk_part<32>(w.mlp0_w, K0, 1, H, s.dz5, P, s.part, tid);
-    __syncthreads();
+    __syncthreads(); HSTAMP(13);
     if (tid < P) dx_out[(size_t)b * P + tid] = splitk_sum<32>(s.part, tid);
   }
-  __syncthreads();
+  __syncthreads(); HSTAMP(14);
   if (tid < H) {
     const float te = hcat_v[P + tid];
     V[TV_DZ4 + tid] = te > 0.f ? s.dhc[tid] : 0.f;
@@ -430,10 +547,10 @@ __device__ __forceinline__ void head_backward(
     s.dz3[j] = d;
     V[TV_DZ3 + j] = d;
   }
-  __syncthreads();
-  splitk_part<64>(w.enc6_w, C2, 1, H, s.dz3, C2, s.part, tid);   // g = (W3^T dz3) / L2
-  __syncthreads();
-  if (tid < C2) V[TV_G + tid] = splitk_sum<64>(s.part, tid) / (float)L2;
+  __syncthreads(); HSTAMP(15);
+  w3.part(s.dz3, s.part4, tid);   // g = (W3^T dz3) / L2
+  __syncthreads(); HSTAMP(16);
+  if (tid < C2) V[TV_G + tid] = SplitK4<C2, 16, H / 16>::sum(s.part4, tid) / (float)L2;
 }
 
 // MODE 0: forward only; 1: backward only (of the last forward's saved row);
@@ -454,11 +571,11 @@ __global__ __launch_bounds__(HT) void train_head_kernel(
     head_forward(w, wt, x_in, x0, noise, alpha_bar, t_vec, freq, partial, S, L2, V, eps_out, rp, s, b,
                  tid);
   if constexpr (MODE == 2) {
-    __syncthreads();
-    head_backward(w, dout_in, s.nz, two_over_n, L2, V, dx_out, s.eps, s.h, s.hc, s, b, tid);
+    __syncthreads(); HSTAMP(17);
+    head_backward(w, wt, dout_in, s.nz, two_over_n, L2, V, dx_out, s.eps, s.h, s.hc, s, b, tid);
   }
   if constexpr (MODE == 1) {
-    head_backward(w, dout_in, noise ? noise + (size_t)b * w.param_dim : nullptr, two_over_n, L2, V,
+    head_backward(w, wt, dout_in, noise ? noise + (size_t)b * w.param_dim : nullptr, two_over_n, L2, V,
                   dx_out, V + TV_EPS, V + TV_H, V + TV_HCAT, s, b, tid);
   }
 }
@@ -712,14 +829,18 @@ static_assert(sizeof(AdamHyper) == ADAM_TABLE_FLOATS * sizeof(float), "AdamHyper
 // torch.optim.Adam's single-tensor update (no weight decay / amsgrad), as torch
 // forms it: exp_avg.lerp_(grad, 1-b1); exp_avg_sq.mul_(b2).addcmul_(grad, grad,
 // 1-b2); denom = sqrt(exp_avg_sq) / sqrt(bc2) + eps; param.addcdiv_(exp_avg, denom, -lr/bc1)
+__device__ __forceinline__ void adam_vals(float& p, float& m, float& v, float g, const AdamHyper& a) {
+  m = m + a.one_minus_b1 * (g - m);
+  v = v * a.b2;
+  v = v + a.one_minus_b2 * g * g;
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  p = p + a.step_size_neg * (m / denom);
+}
 __device__ __forceinline__ void adam_elem(float* __restrict__ p, float* __restrict__ m,
                                           float* __restrict__ v, int e, float g, const AdamHyper& a) {
-  float mm = m[e];
-  mm = mm + a.one_minus_b1 * (g - mm);
-  float vv = v[e] * a.b2;
-  vv = vv + a.one_minus_b2 * g * g;
-  const float denom = sqrtf(vv) / a.bc2_sqrt + a.eps;
-  p[e] = p[e] + a.step_size_neg * (mm / denom);
+  float pp = p[e], mm = m[e], vv = v[e];
+  adam_vals(pp, mm, vv, g, a);
+  p[e] = pp;
   m[e] = mm;
   v[e] = vv;
 }
@@ -779,6 +900,22 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
     const int cb = blockIdx.x / FIN_RB, rb = blockIdx.x - cb * FIN_RB;
     const int col4 = cb * FIN_CB_COLS + lane;
     const bool ok = col4 < NG / 4;
+    const int e0 = col4 * 4;
+    int k, off;
+    if (e0 < NG_W2) { k = 0; off = e0 - NG_W1; }        // condition_encoder.0.weight
+    else if (e0 < NG_B1) { k = 2; off = e0 - NG_W2; }   // condition_encoder.2.weight
+    else if (e0 < NG_B2) { k = 1; off = e0 - NG_B1; }   // condition_encoder.0.bias
+    else { k = 3; off = e0 - NG_B2; }                   // condition_encoder.2.bias
+    // Adam's operands of the lane's 4 elements, prefetched (used by the last block only)
+    float pv[4] = {}, mv[4] = {}, vv[4] = {};
+    if (a.param[0] && ok && wave == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pv[q] = a.param[k][off + q];
+        mv[q] = a.m[k][off + q];
+        vv[q] = a.v[k][off + q];
+      }
+    }
     const int rpb = (a.rows + FIN_RB - 1) / FIN_RB;
     const int r0 = rb * rpb, r1 = min(a.rows, r0 + rpb);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -829,18 +966,18 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) gv[e] += ld_wt(f + e);
     }
-    const int e0 = col4 * 4;
-    int k, off;
-    if (e0 < NG_W2) { k = 0; off = e0 - NG_W1; }        // condition_encoder.0.weight
-    else if (e0 < NG_B1) { k = 2; off = e0 - NG_W2; }   // condition_encoder.2.weight
-    else if (e0 < NG_B2) { k = 1; off = e0 - NG_B1; }   // condition_encoder.0.bias
-    else { k = 3; off = e0 - NG_B2; }                   // condition_encoder.2.bias
     float* gd = a.grad[k];
 #pragma unroll
     for (int q = 0; q < 4; ++q) gd[off + q] = gv[q];
     if (a.param[0]) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) adam_elem(a.param[k], a.m[k], a.v[k], off + q, gv[q], hy);
+      for (int q = 0; q < 4; ++q) {
+        float mm = mv[q];
+        adam_vals(pv[q], mm, vv[q], gv[q], hy);
+        a.param[k][off + q] = pv[q];
+        a.m[k][off + q] = mm;
+        a.v[k][off + q] = vv[q];
+      }
     }
     return;
   }
@@ -866,6 +1003,12 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   } else {
     return;
   }
+  float pv = 0.f, mv = 0.f, vv = 0.f;
+  if (a.param[0]) {   // Adam's operands first: their loads overlap the chain's
+    pv = a.param[k][i];
+    mv = a.m[k][i];
+    vv = a.v[k][i];
+  }
   const int row = bias ? i : i / kdim, col = bias ? 0 : i - row * kdim;
   const float* pd = a.vec + dz_off + row;
   const float* pi = a.vec + in_off + col;
@@ -878,7 +1021,12 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
     for (int b = 0; b < a.B; ++b) acc = fmaf(pd[(size_t)b * TV], pi[(size_t)b * TV], acc);
   }
   a.grad[k][i] = acc;
-  if (a.param[0]) adam_elem(a.param[k], a.m[k], a.v[k], i, acc, hy);
+  if (a.param[0]) {
+    adam_vals(pv, mv, vv, acc, hy);
+    a.param[k][i] = pv;
+    a.m[k][i] = mv;
+    a.v[k][i] = vv;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1153,5 +1301,11 @@ hipError_t launch_adam(const ertd_weights& w, float* const* grads, float* const*
   adam_kernel<<<(off + 255) / 256, 256, 0, s>>>(a);
   return hipGetLastError();
 }
+
+#ifdef HEAD_STAMPS
+extern "C" int ertd_diag_head_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hstamp), sizeof(g_hstamp));
+}
+#endif
 
 }  // namespace ertd

@@ -77,6 +77,14 @@ def main():
     e1.record(st)
     torch.cuda.synchronize()
     print(f"graph.replay only  B={B}: events {e0.elapsed_time(e1) / a.steps * 1e3:8.1f} us/step", flush=True)
+    lib = ertdiff._lib.lib()
+    if hasattr(lib, "ertd_diag_head_stamps"):   # a HEAD_STAMPS variant library
+        import ctypes
+        buf = (ctypes.c_ulonglong * 64)()
+        lib.ertd_diag_head_stamps(buf)
+        st = list(buf)
+        n = max(i for i in range(64) if st[i]) + 1
+        print("head phases (cycles from entry):", [int(st[i] - st[0]) for i in range(n)])
 
 
 if __name__ == "__main__":
