@@ -64,11 +64,17 @@ constexpr int WT_W0B = WT_W2 + H * PMAX;    // [128][256]  mlp.0 columns P.. (16
 constexpr int WT_FLOATS = WT_W0B + H * 2 * H;
 
 constexpr int W2B_FRAG = 3 * 32 * 64;  // transposed-conv2 fragments (conv_bwd)
+#ifndef ENC_ABL
+#define ENC_ABL 0  // diagnostic variants only: bit 0 no a1s stores, 1 no mask words, 2 no weight copies, 3 no LDS weight staging
+#endif
 // train_final_kernel's conv-column reduction (see there)
 constexpr int FIN_CB_COLS = 64;                                  // float4 columns per block
 constexpr int FIN_NCB = (NG / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;  // 30 column blocks
-constexpr int FIN_RB = 8;                                        // row blocks
-constexpr int FIN_MAXR = 48;                                     // rows per wave held in flight
+#ifndef FIN_RB_N
+#define FIN_RB_N 4
+#endif
+constexpr int FIN_RB = FIN_RB_N;                                 // row blocks
+constexpr int FIN_MAXR = FIN_RB < 8 ? 48 : 384 / FIN_RB;   // rows per wave held in flight
 constexpr int FIN_CNT_WORDS = 64;
 static_assert(FIN_NCB <= FIN_CNT_WORDS, "counter words");
 
@@ -91,11 +97,12 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
   }
   // this step's transposed-conv2 fragments (conv_bwd's da1 A operand, one
   // coalesced 256-B row per wave load): W2B[kk][s][lane] = W2[2s + (lane >> 5)][lane & 31][kk]
+  if constexpr ((ENC_ABL & 4) == 0)
   for (int e = item * 256 + tid; e < W2B_FRAG; e += gridDim.x * 256) {
     const int kk = e >> 11, sl = e & 2047, st = sl >> 6, l = sl & 63;
     w2b[e] = w2[((2 * st + (l >> 5)) * C1 + (l & 31)) * 3 + kk];
   }
-  if (wt) {  // this step's k-major copies of the dense weights (the head's forward reads them)
+  if ((ENC_ABL & 4) == 0 && wt) {  // this step's k-major copies of the dense weights (the head's forward reads them)
     const int P = wd.param_dim, K0 = P + 2 * H;
     for (int e = item * 256 + tid; e < WT_FLOATS; e += gridDim.x * 256) {
       float v;
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
   // below are one ds_read_b32 each): W1 (32,42) and W2 (64,96), odd row pitches
   __shared__ float w1s[C1][K1 + 1];
   __shared__ float w2s[C2][K2 + 1];
-  {
+  if constexpr ((ENC_ABL & 8) == 0) {
     float4 v2[6], v1[2];
 #pragma unroll
     for (int k = 0; k < 6; ++k) v2[k] = reinterpret_cast<const float4*>(w2)[tid + 256 * k];
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
     }
   }
   __syncthreads();
-  {  // the strip's conv1 images -> a1s: 1,024 float4 rows, 4 per thread
+  if constexpr ((ENC_ABL & 1) == 0) {  // the strip's conv1 images -> a1s: 1,024 float4 rows, 4 per thread
     float4* dst = reinterpret_cast<float4*>(a1s + (size_t)item * A1S_FLOATS);
     const float* img = &sm.E[0][0];
 #pragma unroll
@@ -214,7 +221,7 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
       if (lane == r) word = (uint32_t)bal;
       if (lane == 16 + r) word = (uint32_t)(bal >> 32);
     }
-    if (lane < 32) {
+    if ((ENC_ABL & 2) == 0 && lane < 32) {
       const int rr = lane & 15, hh = lane >> 4;
       const int qw = qt * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * hh;
       m2w[(size_t)item * M2W_WORDS + qw * 2 + ot] = word;
@@ -871,6 +878,7 @@ struct FinalArgs {
   const float* hyper_tab;  //   of step *step_ctr: hyper_tab[(s - tab_first)], clamped
   const int* step_ctr;
   int tab_first, tab_len;
+  int conv_off;          // diagnostic variants only (FIN_ABL): block index offset
 };
 
 __device__ __forceinline__ AdamHyper fetch_hyper(const FinalArgs& a) {
@@ -896,8 +904,9 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Adam's scalars first: their (dependent) loads overlap the gradient loads
   const AdamHyper hy = a.param[0] ? fetch_hyper(a) : AdamHyper{};
-  if ((int)blockIdx.x < FIN_NCB * FIN_RB) {
-    const int cb = blockIdx.x / FIN_RB, rb = blockIdx.x - cb * FIN_RB;
+  const int bx = blockIdx.x + a.conv_off;
+  if (bx < FIN_NCB * FIN_RB) {
+    const int cb = bx / FIN_RB, rb = bx - cb * FIN_RB;
     const int col4 = cb * FIN_CB_COLS + lane;
     const bool ok = col4 < NG / 4;
     const int e0 = col4 * 4;
@@ -983,7 +992,7 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   }
   // dense layers: one thread per element, a chain over the members
   const int H0 = a.P + 2 * H;
-  int i = (blockIdx.x - FIN_NCB * FIN_RB) * 256 + tid;
+  int i = (bx - FIN_NCB * FIN_RB) * 256 + tid;
   int dz_off, in_off, kdim, k;
   bool bias = false;
   if (i < H * C2) { dz_off = TV_DZ3; in_off = TV_M; kdim = C2; k = 4; }
@@ -1113,8 +1122,13 @@ size_t ws_layout(int B, int L, bool with_vec, float* base, TrainWs* out) {
 int dense_count(int P) { return H * C2 + H + H * H + H + H * (P + 2 * H) + H + P * H + P + 1; }
 
 // conv_grads: FIN_NCB * FIN_RB conv blocks; dense: the member-row part too
+#ifndef FIN_ABL
+#define FIN_ABL 0  // diagnostic variants only: 1 = conv part only, 2 = dense part only
+#endif
 hipError_t launch_final(FinalArgs& a, bool dense, hipStream_t s) {
-  const int blocks = FIN_NCB * FIN_RB + (dense ? (dense_count(a.P) + 255) / 256 : 0);
+  if ((FIN_ABL & 1) != 0) dense = false;
+  int blocks = FIN_NCB * FIN_RB + (dense ? (dense_count(a.P) + 255) / 256 : 0);
+  if ((FIN_ABL & 2) != 0) { a.conv_off = FIN_NCB * FIN_RB; blocks -= FIN_NCB * FIN_RB; }
   train_final_kernel<<<blocks, 256, 0, s>>>(a);
   return hipGetLastError();
 }

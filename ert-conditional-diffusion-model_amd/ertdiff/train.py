@@ -22,6 +22,7 @@ import ctypes
 
 import torch
 import torch.nn.functional as F
+from torch.autograd.graph import increment_version
 
 from . import _lib
 from .schedule import timestep_frequencies
@@ -147,6 +148,7 @@ def train_step(model, optimizer, x0, cond, T, alpha_bar, *, t=None, noise=None,
             _lib.ptr_array(exp_avg), _lib.ptr_array(exp_avg_sq), step, lr, b1, b2, eps,
             loss.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_of(dev)), "train_step")
     model._packed_key = None  # parameters changed in place behind autograd's back: re-pack
+    increment_version(params)  # ... and say so to autograd
     return loss if return_tensor else loss.item()
 
 
@@ -269,8 +271,23 @@ class TrainPlan:
             self._graphs[draw] = g
         return g
 
+    def _sync_step(self):
+        """Follow Adam steps taken outside the plan (eager train_step, a
+        user's optimizer.step()): the step counters are host tensors."""
+        st = self._steps[0]
+        if st.device.type != "cpu":
+            return
+        s = int(st.item())
+        if s != self.host_step:
+            if self.table_first <= s + 1 < self.table_first + self.TABLE:
+                self.step_dev.fill_(s)
+                self.host_step = s
+            else:
+                self._table_at(s)
+
     @torch.no_grad()
     def _replay(self, draw: bool):
+        self._sync_step()
         if self.host_step + 1 >= self.table_first + self.TABLE:
             self._table_at(self.host_step)
         g = self._graph(draw)

@@ -174,6 +174,17 @@ def test_train_plan_equals_eager(B, L, golden_weights, cuda_dev):
     la = ertdiff.train_step(m1, o1, x0, cond, T, ab, t=ts[0], noise=ns[0])
     lb = ertdiff.train_step(m2, o2, x0, cond, T, ab, t=ts[0], noise=ns[0])
     assert la == lb
+    # ... and the plan from weights and Adam steps changed outside it (eager
+    # steps, a user's in-place edit): it follows the step count
+    with torch.no_grad():
+        for m in (m1, m2):
+            m.condition_encoder[0].weight.mul_(0.75)
+            m.condition_encoder[2].weight.add_(0.01)
+    la = [ertdiff.train_step(m1, o1, x0, cond, T, ab, t=ts[i], noise=ns[i]) for i in (1, 2)]
+    lb = [plan.step(x0, cond, t=ts[i], noise=ns[i]) for i in (1, 2)]
+    assert la == lb
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p1, p2), k
 
 
 def test_train_plan_draws_match_torch(golden_weights, cuda_dev):
