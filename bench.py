@@ -57,6 +57,11 @@ CONV_FLOP_PER_MEMBER = 6_308_736 + 14_426_112
 # ... and of one full faithful step per member incl. Linear layers
 STEP_FLOP_PER_MEMBER = 20_864_384
 COND_BYTES_PER_MEMBER = 14 * L_MEAS * 4
+STRIPS_MEAS = -(-(((L_MEAS + 2 - 3) // 2 + 1 + 2 - 3) // 2 + 1) // 63)   # encoder strips (63 conv2 outputs each) at L_MEAS
+# the encoder convs' backward (loss.backward()'s Conv1d part, :317) per member:
+# conv2 input-gradient + conv2 weight-gradient (each = conv2's forward MACs x2)
+# + conv1 weight-gradient (= conv1's forward); conv1's input gradient is not needed
+CONV_BWD_FLOP_PER_MEMBER = 2 * 14_426_112 + 6_308_736
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
 PEAK_BF16_TFLOPS = 2500.0    # dense bf16 MFMA
 PEAK_HBM_GBS = 8000.0
@@ -260,17 +265,21 @@ def strip_kernel_roofline(model, cond, B, precision, reps, dev):
             "hbm_gbs_algorithmic": round(COND_BYTES_PER_MEMBER * B / (avg_ms * 1e-3) / 1e9, 1)}
 
 
-def train_bench(dev, steps=200, B=32, T=500):
-    """Reference train step (:309-319) at the reference batch size, fused GPU path."""
+def train_bench(dev, steps=200, B=32, T=500, reps=200):
+    """Reference train step (:309-319) at the reference batch size: eager
+    ertdiff.train_step (host-driven, 4 launches) and ertdiff.TrainPlan (the same
+    kernels captured in one graph, draws inside), wall clock around `steps`
+    steps; plus the roofline of the step's dominant kernel (the encoder-conv
+    backward), HIP events around back-to-back launches on its stream."""
     torch.manual_seed(42)
-    model = ertdiff.ConditionalDiffusionModel(P, 128).to(dev).train()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     g = torch.Generator(device=dev).manual_seed(7)
     x0 = torch.randn(B, P, device=dev, generator=g) * 2
     cond = torch.rand(B, 14, L_MEAS, device=dev, generator=g)
     _, _, ab = ertdiff.get_diffusion_schedule(T, device=dev)
     ts = torch.randint(0, T, (steps + 20, B), device=dev, generator=g)
     ns = torch.randn(steps + 20, B, P, device=dev, generator=g)
+    model = ertdiff.ConditionalDiffusionModel(P, 128).to(dev).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     for i in range(20):
         ertdiff.train_step(model, opt, x0, cond, T, ab, t=ts[i], noise=ns[i], return_tensor=True)
     torch.cuda.synchronize(dev)
@@ -279,9 +288,62 @@ def train_bench(dev, steps=200, B=32, T=500):
         loss = ertdiff.train_step(model, opt, x0, cond, T, ab, t=ts[20 + i], noise=ns[20 + i],
                                   return_tensor=True)
     torch.cuda.synchronize(dev)
+    el_eager = time.perf_counter() - t0
+    # the plan: a fresh model, the same inputs, t / noise drawn in the graph
+    torch.manual_seed(42)
+    model = ertdiff.ConditionalDiffusionModel(P, 128).to(dev).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    plan = ertdiff.TrainPlan(model, opt, B, L_MEAS, T, ab, seed=1234)
+    plan.x0.copy_(x0)
+    plan.cond.copy_(cond)
+    plan.run(20)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    plan.run(steps)
+    torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    return {"train_steps_per_s": round(steps / el, 1), "train_batch": B,
-            "train_ms_per_step": round(el / steps * 1e3, 4), "train_final_loss": round(float(loss), 5)}
+    out = {"train_steps_per_s": round(steps / el, 1), "train_batch": B,
+           "train_ms_per_step": round(el / steps * 1e3, 4), "train_final_loss": round(float(plan.loss), 5),
+           "train_basis": f"ertdiff.TrainPlan.run({steps}) wall clock (one hipGraph replay per step: "
+                          "encoder forward, head forward+backward, conv backward, gradients + Adam; "
+                          "t / noise drawn in the graph)",
+           "train_eager_steps_per_s": round(steps / el_eager, 1),
+           "train_eager_final_loss": round(float(loss), 5)}
+    # train_roofline: the conv backward alone on the state the plan's last step left
+    stream = torch.cuda.current_stream(dev)
+    lib = _lib.lib()
+
+    def launch():
+        _lib.check(lib.ertd_train_conv_backward(plan.cond.data_ptr(), B, L_MEAS, plan.ws.data_ptr(),
+                                                plan.ws.numel(), stream.cuda_stream), "train_conv_backward")
+    for _ in range(20):
+        launch()
+    rounds = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            launch()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        rounds.append(e0.elapsed_time(e1) / reps)
+    avg_ms = sum(rounds) / len(rounds)
+    flop = CONV_BWD_FLOP_PER_MEMBER * B
+    executed = 512 * 2 * 32 * 32 * 2 * B * STRIPS_MEAS   # 512 v_mfma_f32_32x32x2 per workgroup
+    ach = flop / (avg_ms * 1e-3) / 1e12
+    out["train_roofline"] = {
+        "kernel": "conv_bwd_kernel", "bound": "mfma", "achieved": round(ach, 3),
+        "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+        "executed_frac": round(executed / (avg_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+        "traffic": _traffic(f"train_conv_bwd_B{B}"),
+        "avg_us": round(avg_ms * 1e3, 2), "min_round_us": round(min(rounds) * 1e3, 2),
+        "timing": f"HIP events around {reps} back-to-back launches x 5 rounds on the launching stream "
+                  "(includes the ~1 us dispatch gap)",
+        "algorithmic_flop_per_launch": flop,
+        "flop_basis": f"{CONV_BWD_FLOP_PER_MEMBER} FLOP per member (conv2 dX + conv2 dW + conv1 dW at "
+                      f"L={L_MEAS}) x {B} members",
+        "executed_flop_per_launch": executed}
+    return out
 
 
 def _time_op(fn, reps, dev):

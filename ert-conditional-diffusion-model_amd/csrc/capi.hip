@@ -534,6 +534,13 @@ int ertd_train_step(const ertd_weights* w, float* packed, const float* x0, const
                               exp_avg_sq, adam, loss_out, (float*)ws, (hipStream_t)stream));
 }
 
+int ertd_train_conv_backward(const float* cond, int B, int L, void* ws, size_t ws_bytes,
+                             void* stream) {
+  if (!cond || !ws || B < 1 || L < 1) return ERTD_EINVAL;
+  if (train_ws_floats(B, L) * sizeof(float) > ws_bytes) return ERTD_ENOSPC;
+  return rc(launch_train_conv_backward(cond, B, L, (float*)ws, (hipStream_t)stream));
+}
+
 int ertd_adam_table(int step_first, int n, float lr, float beta1, float beta2, float eps,
                     float* out) {
   if (!out || step_first < 1 || n < 1) return ERTD_EINVAL;

@@ -309,6 +309,7 @@ struct TrainAdam {
 };
 constexpr int ADAM_TABLE_FLOATS = 6;  // floats per step entry
 void adam_table_host(int step_first, int n, float lr, float beta1, float beta2, float eps, float* out);
+hipError_t launch_train_conv_backward(const float* cond, int B, int L, float* ws, hipStream_t s);
 hipError_t launch_train_forward(const ertd_weights& w, const float* x_in, const float* x0,
                                 const float* noise, const float* alpha_bar, const int64_t* t,
                                 const float* cond, int B, int L, const float* freq, float* eps_out,

@@ -588,11 +588,17 @@ __global__ __launch_bounds__(HT) void train_head_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// conv backward, one 256-thread workgroup per (member, strip of J conv2 outputs)
-//   phase A: dz2 = g * mask -> da1 (transposed conv2) -> dz1 = da1 * [a1 > 0]
-//            (waves 0-1: even conv1 positions, 1 tap; waves 2-3: odd, 2 taps)
-//            and dW2 = dz2 x a1 (6 tiles: 2 + 2 + 1 + 1) -- 96 MFMAs per wave
-//   phase B: dW1 = dz1 x cond (+ db1 from a ones column of the padded N), 32 per wave
+// conv backward: two 256-thread workgroups per (member, strip of J conv2
+// outputs), one launch -- the first B*S blocks the dz1 chain, the next B*S the
+// rest of dW2 (the two touch disjoint columns of the strip's gradient row):
+//   chain, phase A: dz2 = g * mask -> da1 (transposed conv2) -> dz1 = da1 * [a1 > 0]
+//            (waves 0-1: even conv1 positions, 1 tap + one dW2 tile each;
+//            waves 2-3: odd positions, 2 taps) -- 64 MFMAs per wave
+//   chain, phase B: dW1 = dz1 x cond (+ db1 from a ones column of the padded N), 32 per wave
+//   dW2 blocks: dz2 -> dW2 tiles 2-5 (one per wave, 32 MFMAs) and db2
+// Every wave of a chain block runs 96 MFMAs (128 before the split, in one
+// block per item: 608 blocks for 768 slots at B = 32 left the CUs that got
+// three blocks as the critical path); the short dW2 blocks fill the gaps.
 // LDS: phase A's dz2 / a1 images are dead in phase B, where the cond image and
 // the dW1 halves take their place: 51.6 KB -> 3 workgroups per CU.
 // ---------------------------------------------------------------------------
@@ -641,6 +647,9 @@ __device__ __forceinline__ void mfma_pipe(f32x16& acc, FA fa, FB fb) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
   }
 }
+#ifndef CBW_ORDER
+#define CBW_ORDER 1
+#endif
 #ifndef CBW_AHEAD
 #define CBW_AHEAD 6
 #endif
@@ -669,46 +678,12 @@ __device__ __forceinline__ void dw2_tile(const ConvBwdSmem& sm, int tt, int h, i
   }
 }
 
-__global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
-    const float* __restrict__ w2b, const float* __restrict__ cond, const float* __restrict__ a1s,
-    const uint32_t* __restrict__ m2w, const float* __restrict__ g, int g_stride, int L, int L1,
-    int L2, int S, float* __restrict__ gpart) {
-  __shared__ __attribute__((aligned(16))) ConvBwdSmem sm;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, l32 = lane & 31;
-  const int item = blockIdx.x;
-  const int b = item / S, strip = item - b * S;
-  const int j0 = strip * J;
-  float* G = gpart + (size_t)item * NG;
-
-  // ---- transposed-conv2 fragments (the da1 A operand) first, into registers:
-  //   W2B[kk][s][lane] = W2[o = 2s + h][c = l32][kk]; even waves tap 1, odd waves taps 0 and 2
-  const bool oddw = wave >= 2;
-  float wt0[32], wt1[32];
-  {
-    const float* base = w2b + lane;
-    const int k0 = oddw ? 0 : 1;
-#pragma unroll
-    for (int s = 0; s < 32; ++s) wt0[s] = base[(k0 * 32 + s) * 64];
-#pragma unroll
-    for (int s = 0; s < 32; ++s) wt1[s] = oddw ? base[(2 * 32 + s) * 64] : 0.f;
-  }
-  // ---- the cond strip (phase B's image), loaded now, stored after phase A
-  const float* cb = cond + (size_t)b * CIN * L;
-  const int pos = 4 * j0 - 3 + tid;
-  const bool cin = pos >= 0 && pos < L;
-  float cv[CIN];
-  {
-    const int pc = pos < 0 ? 0 : (pos >= L ? L - 1 : pos);
-#pragma unroll
-    for (int c = 0; c < CIN; ++c) cv[c] = cb[(size_t)c * L + pc];
-  }
-  const int tc = tid >> 2, tu = 256 + (tid & 3);
-  const int pt = 4 * j0 - 3 + tu;
-  float cvt = 0.f;
-  if (tid < CIN * 4) cvt = cb[(size_t)tc * L + (pt < 0 ? 0 : (pt >= L ? L - 1 : pt))];
-
-  // ---- a1 images (the forward's float4 rows) and dz2 = g * mask
+// the a1 images (the forward's float4 rows) and dz2 = g * mask (+ the db2
+// partial sums of the four q' classes) into LDS
+__device__ __forceinline__ void conv_bwd_images(ConvBwdSmem& sm, const float* __restrict__ a1s,
+                                                const uint32_t* __restrict__ m2w,
+                                                const float* __restrict__ g, int g_stride, int b,
+                                                int item, int strip, int S, int tid) {
   {
     const float4* src = reinterpret_cast<const float4*>(a1s + (size_t)item * A1S_FLOATS);
     float4 v[4];
@@ -746,6 +721,62 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     }
     sm.db2p[qb][o] = dsum;
   }
+}
+
+__global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
+    const float* __restrict__ w2b, const float* __restrict__ cond, const float* __restrict__ a1s,
+    const uint32_t* __restrict__ m2w, const float* __restrict__ g, int g_stride, int L, int L1,
+    int L2, int S, float* __restrict__ gpart, int c1, int c2) {
+  __shared__ __attribute__((aligned(16))) ConvBwdSmem sm;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  // dispatch order: chain items [0, c1), dW2 items [0, c2), the remaining chain
+  // items, the remaining dW2 items -- c1 = 2 and c2 = 1 per CU, so the first
+  // round of slots holds at most two chain blocks per CU
+  const int nit = (int)gridDim.x / 2, bi = (int)blockIdx.x;
+  const bool w2blk = CBW_ORDER ? (bi >= c1 && bi < c1 + c2) || bi >= nit + c2 : bi >= nit;
+  const int item = !CBW_ORDER ? (w2blk ? bi - nit : bi)
+                 : bi < c1 ? bi : bi < c1 + c2 ? bi - c1 : bi < nit + c2 ? bi - c2 : bi - nit;
+  const int b = item / S, strip = item - b * S;
+  const int j0 = strip * J;
+  float* G = gpart + (size_t)item * NG;
+
+  if (w2blk) {
+    conv_bwd_images(sm, a1s, m2w, g, g_stride, b, item, strip, S, tid);
+    __syncthreads();
+    if constexpr ((CBW_ABL & 2) == 0) dw2_tile(sm, 2 + wave, h, l32, G);
+    if (tid < C2) G[NG_B2 + tid] = sm.db2p[0][tid] + sm.db2p[1][tid] + sm.db2p[2][tid] + sm.db2p[3][tid];
+    return;
+  }
+
+  // ---- transposed-conv2 fragments (the da1 A operand) first, into registers:
+  //   W2B[kk][s][lane] = W2[o = 2s + h][c = l32][kk]; even waves tap 1, odd waves taps 0 and 2
+  const bool oddw = wave >= 2;
+  float wt0[32], wt1[32];
+  {
+    const float* base = w2b + lane;
+    const int k0 = oddw ? 0 : 1;
+#pragma unroll
+    for (int s = 0; s < 32; ++s) wt0[s] = base[(k0 * 32 + s) * 64];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) wt1[s] = oddw ? base[(2 * 32 + s) * 64] : 0.f;
+  }
+  // ---- the cond strip (phase B's image), loaded now, stored after phase A
+  const float* cb = cond + (size_t)b * CIN * L;
+  const int pos = 4 * j0 - 3 + tid;
+  const bool cin = pos >= 0 && pos < L;
+  float cv[CIN];
+  {
+    const int pc = pos < 0 ? 0 : (pos >= L ? L - 1 : pos);
+#pragma unroll
+    for (int c = 0; c < CIN; ++c) cv[c] = cb[(size_t)c * L + pc];
+  }
+  const int tc = tid >> 2, tu = 256 + (tid & 3);
+  const int pt = 4 * j0 - 3 + tu;
+  float cvt = 0.f;
+  if (tid < CIN * 4) cvt = cb[(size_t)tc * L + (pt < 0 ? 0 : (pt >= L ? L - 1 : pt))];
+
+  conv_bwd_images(sm, a1s, m2w, g, g_stride, b, item, strip, S, tid);
   __syncthreads();
 
   // ---- phase A
@@ -776,17 +807,14 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     }
   }
   if constexpr ((CBW_ABL & 2) == 0) {
-    if (wave == 0) { dw2_tile(sm, 0, h, l32, G); dw2_tile(sm, 1, h, l32, G); }
-    else if (wave == 1) { dw2_tile(sm, 2, h, l32, G); dw2_tile(sm, 3, h, l32, G); }
-    else dw2_tile(sm, 2 + wave, h, l32, G);
+    if (!oddw) dw2_tile(sm, wave, h, l32, G);   // tiles 0, 1 (2-5: the dW2 blocks)
   }
   __syncthreads();
 
-  // ---- cond image into the dead dz2 region; db2
+  // ---- cond image into the dead dz2 region
 #pragma unroll
   for (int c = 0; c < CIN; ++c) sm.X[tid & 3][c][tid >> 2] = cin ? cv[c] : 0.f;
   if (tid < CIN * 4) sm.X[tu & 3][tc][tu >> 2] = (pt >= 0 && pt < L) ? cvt : 0.f;
-  if (tid < C2) G[NG_B2 + tid] = sm.db2p[0][tid] + sm.db2p[1][tid] + sm.db2p[2][tid] + sm.db2p[3][tid];
   __syncthreads();
 
   // ---- phase B: dW1[o][n = c*3+kk] = sum_r dz1[o][r] * cond[c][4*j0 + 2r - 1 + kk];
@@ -1168,14 +1196,24 @@ hipError_t launch_enc(const float* w1, const float* b1, const float* w2, const f
 hipError_t launch_conv_bwd(const float* cond, const TrainWs& W, const float* g, int g_stride, int B,
                            int L, hipStream_t s) {
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
-  conv_bwd_kernel<<<dim3((unsigned)(B * S)), 256, 0, s>>>(W.w2b, cond, W.a1s, W.m2w, g, g_stride, L, L1,
-                                                        L2, S, W.gpart);
+  const int nit = B * S, cus = device_cu_count();
+  const int c1 = nit < 2 * cus ? nit : 2 * cus, c2 = nit < cus ? nit : cus;
+  conv_bwd_kernel<<<dim3((unsigned)(2 * nit)), 256, 0, s>>>(W.w2b, cond, W.a1s, W.m2w, g, g_stride, L, L1,
+                                                            L2, S, W.gpart, c1, c2);
   return hipGetLastError();
 }
 
 }  // namespace
 
 size_t train_ws_floats(int B, int L) { return ws_layout(B, L, true, nullptr, nullptr); }
+
+// the encoder-conv backward kernel alone, on the state the last train forward /
+// step left in ws (its dL/dpooled rows): per-kernel timing (bench.py train_roofline)
+hipError_t launch_train_conv_backward(const float* cond, int B, int L, float* ws, hipStream_t s) {
+  TrainWs W;
+  ws_layout(B, L, true, ws, &W);
+  return launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, s);
+}
 
 void adam_table_host(int step_first, int n, float lr, float beta1, float beta2, float eps,
                      float* out) {

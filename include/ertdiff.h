@@ -268,6 +268,14 @@ int ertd_train_step_dev(const ertd_weights* w, const float* x0, int64_t* t, floa
                         int draw, int T, uint64_t seed, float* loss_out, void* ws, size_t ws_bytes,
                         void* stream);
 
+/* The condition encoder's conv backward alone (the Conv1d part of
+ * loss.backward(), :317), re-run on the state the last ertd_train_step /
+ * ertd_train_step_dev / ertd_train_backward left in ws (same B, L, cond): it
+ * rewrites the per-strip gradient rows in ws and nothing else.  For timing the
+ * step's dominant kernel on its own (bench.py train_roofline).               */
+int ertd_train_conv_backward(const float* cond, int B, int L, void* ws, size_t ws_bytes,
+                             void* stream);
+
 /* host: the Adam scalars of steps step_first ... step_first + n - 1 (6 floats
  * each), formed as torch.optim.Adam forms them (Python-float bias corrections). */
 int ertd_adam_table(int step_first, int n, float lr, float beta1, float beta2, float eps,
