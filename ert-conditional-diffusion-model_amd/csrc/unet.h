@@ -42,6 +42,27 @@ enum Mode { MODE_S1 = 0, MODE_S2 = 1, MODE_UP = 2,
             // 2x2 convs at the source resolution (launch_pack_conv_up weights)
             MODE_UPP = 3 };
 
+// GroupNorm partials per (sample, channel, part) -> {scale, shift} (see launch_gn_finalize below)
+struct GnPartArgs {
+  const float2* pa; int npa; int Ca;   // (B, Ca, npa) partials of channels [0, Ca)
+  const float2* pb; int npb; int Cb;   // (B, Cb, npb) of channels [Ca, Ca+Cb), or null
+  int HW, groups;
+  const float* gamma; const float* beta;
+  float2* out;           // (B, Ca+Cb) {gamma*rstd, beta - mean*gamma*rstd}
+  float2* mr;            // optional (B, groups) {mean, rstd}
+};
+
+// The consumer GroupNorm's finalize folded into the producing conv: the MFMA
+// waves store their partials write-through, every finished item adds one to
+// its sample's counter, and once its items are done, workgroup w waits for
+// the counts of samples w, w + grid, ... and finalizes them -- no finalize launch.
+struct GnFold {
+  GnPartArgs g;          // g.pa = the conv's own partials (ConvArgs::gnp), g.out the consumer's {scale, shift}
+  unsigned* cnt;         // (B) arrival counters: zero before the launch, left zero by it
+  int target;            // arrivals (items) per sample
+  int B;                 // samples: workgroup w finalizes samples w, w + grid, ...
+};
+
 struct ConvArgs {
   const float* srcA;     // (B, Ca, Hs, Ws)  channels [0, Ca)
   const float* srcB;     // (B, Cb, Hs, Ws)  channels [Ca, Ca+Cb) (skip concat) or null
@@ -70,6 +91,10 @@ struct ConvArgs {
                          // kernel emits none and gnp must be null)
   int split;             // bf16 kernels: 1 = split-bf16 operands (hi + lo planes: weights
                          // packed with split = true, images of conv_bf16_image_bytes(.., true))
+  GnFold fold;           // fp32 Winograd F(4x4) kernels with gnp: the next GroupNorm's finalize
+                         // (fold.cnt null: none; conv_gn_fold_ok says where it is taken)
+  unsigned* zero_words;  // conv_in: zero these zero_n words (the fold counters of the walk)
+  int zero_n;
 };
 
 // GroupNorm statistics without a second read of the activation: the fp32
@@ -80,14 +105,6 @@ struct ConvArgs {
 // fixed order in float64 (Chan's parallel formula) into the conv prologue's
 // {scale, shift} (and {mean, rstd}) -- the 35 full-tensor reads of
 // gn_stats_kernel per U2 step become 5.
-struct GnPartArgs {
-  const float2* pa; int npa; int Ca;   // (B, Ca, npa) partials of channels [0, Ca)
-  const float2* pb; int npb; int Cb;   // (B, Cb, npb) of channels [Ca, Ca+Cb), or null
-  int HW, groups;
-  const float* gamma; const float* beta;
-  float2* out;           // (B, Ca+Cb) {gamma*rstd, beta - mean*gamma*rstd}
-  float2* mr;            // optional (B, groups) {mean, rstd}
-};
 hipError_t launch_gn_finalize(const GnPartArgs& a, int B, hipStream_t s);
 // x (B, C, HW) -> (B, C, np) partials of 256 pixels: HW == 256 np
 hipError_t launch_gn_partials(const float* x, int C, int HW, int np, float2* out, int B, hipStream_t s);
@@ -97,6 +114,11 @@ int conv_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B);
 // the same for the bf16 / split-bf16 convs (unet_conv_bf16.hip)
 int conv_bf16_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B);
 int wino_gn_parts(const ConvArgs& a, int B);
+// true where the kernel launch_conv would dispatch (fp32) takes ConvArgs::fold:
+// the Winograd F(4x4) register-weight kernel without a K split
+bool conv_gn_fold_ok(int ks, int mode, int act, const ConvArgs& a, int B);
+// its MFMA-wave arrivals per sample (GnFold::target)
+int conv_gn_fold_target(const ConvArgs& a, int B);
 
 // sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), the same bits in
 // every lane of the row (fixed pairing: quad swaps, then the half-row and row
@@ -107,6 +129,116 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
   return v;
+}
+
+// ---- the GroupNorm finalize folded into the producing conv (GnFold) --------------
+// write-through (agent-coherent) float2 store / load of the partials: the
+// arriving waves of other workgroups (other XCDs' L2s) see them
+__device__ __forceinline__ void st_f2_wt(float2* p, float2 v) {
+  unsigned* u = reinterpret_cast<unsigned*>(p);
+  __hip_atomic_store(u, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(u + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld_f2_wt(const float2* p) {
+  const unsigned* u = reinterpret_cast<const unsigned*>(p);
+  return make_float2(__uint_as_float(__hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                     __uint_as_float(__hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+// running {count, mean, M2} in float64; chan_add merges a part (Chan et al.)
+#ifndef FOLD_BATCH
+#define FOLD_BATCH 4   // parts loaded per round trip and lane (registers: the producer's epilogue)
+#endif
+struct ChanAcc {
+  double n, mean, m2;
+};
+__device__ __forceinline__ void chan_add(ChanAcc& a, double nb, double meanb, double m2b) {
+  const double n = a.n + nb;
+  const double d = meanb - a.mean;
+  const double f = n > 0.0 ? nb / n : 0.0;   // two empty states stay empty
+  a.mean = a.mean + d * f;
+  a.m2 = a.m2 + m2b + d * d * a.n * f;
+  a.n = n;
+}
+// Groups [part * ceil(G / nparts), ...) of sample b finalized by the calling
+// wave -- the one GroupNorm finalize of the fp32 U-Net, run by
+// gn_finalize_kernel and by the producing convs' fold alike, so a group's
+// {scale, shift} has the same bits whichever runs it: GN_LPG lanes per group,
+// each streaming the group's parts k = sub, sub + GN_LPG, ... (channel-major,
+// A then B) through chan_add, then the lanes' states merged in a fixed
+// butterfly (the lower lane's state first, so every lane holds the same bits).
+// WT: the A partials were written in this launch (write-through loads).
+constexpr int GN_LPG = 16;
+template <bool WT>
+__device__ __forceinline__ void gn_group_finalize(const GnPartArgs& g, int b, int lane, int part,
+                                                  int nparts) {
+  const int G = g.groups, C = g.Ca + g.Cb, cpg = C / G;
+  const int gper = (G + nparts - 1) / nparts, gfirst = part * gper;
+  const int gcnt = G - gfirst < gper ? G - gfirst : gper;
+  if (gcnt <= 0) return;
+  constexpr int LPG = GN_LPG;
+  const double na = (double)(g.HW / g.npa), nb = g.Cb > 0 ? (double)(g.HW / g.npb) : 1.0;
+  for (int gbase = 0; gbase < gcnt; gbase += 64 / LPG) {
+    const int gl = gbase + lane / LPG, sub = lane % LPG;
+    const bool live = gl < gcnt;
+    const int gi = gfirst + gl;
+    const int c0 = live ? gi * cpg : 0;
+    const int nA = !live ? 0 : (c0 < g.Ca ? (g.Ca - c0 < cpg ? g.Ca - c0 : cpg) : 0);
+    const int itemsA = nA * g.npa, items = !live ? 0 : itemsA + (cpg - nA) * (g.Cb > 0 ? g.npb : 0);
+    const float2* pa = g.pa + ((size_t)b * g.Ca + c0) * g.npa;
+    const float2* pb = g.Cb > 0 && live ? g.pb + ((size_t)b * g.Cb + (c0 + nA - g.Ca)) * g.npb : nullptr;
+    ChanAcc acc{0.0, 0.0, 0.0};
+    for (int k0 = sub; k0 < items; k0 += FOLD_BATCH * LPG) {
+      float2 v[FOLD_BATCH];
+#pragma unroll
+      for (int j = 0; j < FOLD_BATCH; ++j) {
+        const int k = k0 + j * LPG;
+        v[j] = k >= items ? make_float2(0.f, 0.f) : (k < itemsA ? (WT ? ld_f2_wt(pa + k) : pa[k]) : pb[k - itemsA]);
+      }
+#pragma unroll
+      for (int j = 0; j < FOLD_BATCH; ++j) {
+        const int k = k0 + j * LPG;
+        if (k < items) {
+          const double n = k < itemsA ? na : nb;
+          chan_add(acc, n, (double)v[j].x / n, (double)v[j].y);
+        }
+      }
+    }
+    for (int m = 1; m < LPG; m <<= 1) {
+      ChanAcc o{__shfl_xor(acc.n, m), __shfl_xor(acc.mean, m), __shfl_xor(acc.m2, m)};
+      const bool lower = (sub & m) == 0;
+      ChanAcc x = lower ? acc : o;
+      const ChanAcc y = lower ? o : acc;
+      chan_add(x, y.n, y.mean, y.m2);
+      acc = x;
+    }
+    if (!live) continue;
+    double var = acc.m2 / acc.n;
+    var = var > 0.0 ? var : 0.0;
+    const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
+    const float mean = (float)acc.mean;
+    if (g.mr && sub == 0) g.mr[(size_t)b * G + gi] = make_float2(mean, rstd);
+    for (int cl = sub; cl < cpg; cl += LPG) {
+      const int c = c0 + cl;
+      const float scale = rstd * g.gamma[c];
+      const float shift = -scale * mean + g.beta[c];
+      g.out[(size_t)b * C + c] = make_float2(scale, shift);
+    }
+  }
+}
+// called by every MFMA wave of a producing conv once per item, after its
+// partials of sample b are stored with st_f2_wt (whole wave active): the
+// item's last wave (an LDS count over the nw MFMA waves) adds the item's one
+// arrival to the sample's counter -- without waiting for the atomic's return
+// (same-address device atomics serialize: the count is read at the tail)
+__device__ __forceinline__ void gn_fold_item_done(const GnFold& f, int b, int* lds_cnt, int nw, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = atomicAdd(lds_cnt, 1);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old == nw - 1 && lane == 0) {
+    *lds_cnt = 0;
+    (void)__hip_atomic_fetch_add(f.cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s);
@@ -156,6 +288,8 @@ bool wino4_ksplit(int cin, int cout, int wo, int B);
 // is true where wino4s_ok is, and launch_conv_wino then dispatches it.
 bool wino4s_ok(int cin, int ca, int cout, int wo, int B);
 int wino4s_items(int cout, int wo, int B);
+bool wino4s_fold_ok(const ConvArgs& a, bool up, int B);
+int wino4s_fold_target(const ConvArgs& a);
 // the same kernel for the fp32 Upsample conv (MODE_UP, no activation; wo = the
 // OUTPUT width): conv3x3 of the nearest-x2 source through the F(4x4) packing
 bool wino4s_up_ok(int cin, int ca, int cout, int wo, int B);

@@ -205,6 +205,7 @@ Layout layout(const ertd_unet_config* c) {
   return L;
 }
 
+
 // ---- forward walk -----------------------------------------------------------------
 struct Walk {
   const ertd_unet_config* c;
@@ -235,7 +236,59 @@ struct Walk {
     if (err == hipSuccess && e != hipSuccess) err = e;
   }
 
-  float2* gnbuf = nullptr;
+  float2* gnbuf = nullptr;  // the {scale, shift} the next GN+act conv reads: one of gnb
+  float2* gnb[2] = {nullptr, nullptr};   // alternated per GroupNorm (a folded finalize writes
+                                         // the other one while its producer still reads this one)
+  // ---- GroupNorm finalize folded into the producing conv (unet.h GnFold) ----
+  // OFF by default (ERTD_UNET_GNFOLD=1 in a diagnostic build): measured on one
+  // box, U2 B=64, 248.2 steps/s without vs 238.4 with -- the per-item
+  // write-through partials + arrival and the tail's count wait and finalize
+  // add ~6 us per producing conv, more than the ~5 us finalize launch they
+  // replace (profiles/r05_gnfold_ab.txt).
+  // The walk's conv and GroupNorm calls are recorded as events; a dry pass of
+  // the same walk (plan_folds) finds each fold-capable conv whose output is
+  // the A input of the very next GroupNorm, and the real walk hands that conv
+  // the GroupNorm's finalize (the GroupNorm then launches nothing).
+  struct Ev {
+    bool gn;            // GroupNorm (else conv)
+    bool foldable;      // conv: its dispatched kernel takes ConvArgs::fold
+    int prod = -1;      // GroupNorm: the conv event that produced A (-1: none)
+    int prodB = -2;     // GroupNorm: ... produced Bs (-2: no Bs, -1: unknown)
+    int Cb = 0, HW = 0;
+    std::string name;
+  };
+  std::vector<Ev> evs;
+  std::vector<const float*> ev_out;          // event -> the conv's output tensor (null: GroupNorm)
+  std::map<const float*, int> producer;      // tensor -> conv event
+  std::vector<int> fold_at;                  // real walk: conv event -> folded GroupNorm event
+  std::vector<Ev> plan_evs;
+  unsigned* fold_cnt = nullptr;              // (B) arrival counters (fixed(); zeroed by conv_in)
+  bool cnt_zeroed = false;                   // conv_in ran with the zeroing: folds may follow
+  struct PendFold {
+    int gn_ev = -1;
+    float2* buf = nullptr;
+  } pfold;
+  static int fold_env() {
+    static const int v = [] {
+      return ERTD_KNOB("UNET_GNFOLD", 0);
+    }();
+    return v;
+  }
+  float2* next_gnbuf() const { return gnbuf == gnb[0] ? gnb[1] : gnb[0]; }
+  void plan_folds() {
+    Walk d{c, L, pk, nullptr, 0, B, nullptr, true};
+    d.fold_cnt = reinterpret_cast<unsigned*>(16);   // plan as the real walk (never dereferenced)
+    d.unet(nullptr, nullptr, nullptr);
+    plan_evs = d.evs;
+    fold_at.assign(plan_evs.size(), -1);
+    for (size_t i = 0; i < plan_evs.size(); ++i) {
+      if (plan_evs[i].gn || !plan_evs[i].foldable) continue;
+      size_t j = i + 1;
+      while (j < plan_evs.size() && !plan_evs[j].gn) ++j;
+      if (j == plan_evs.size() || plan_evs[j].prod != (int)i || plan_evs[j].prodB == -1) continue;
+      fold_at[i] = (int)j;
+    }
+  }
   // plan capture only: a side stream (forked/joined with events) on which a
   // ResBlock's 1x1 skip conv runs concurrently with its conv1 -- a branch of
   // the step graph that fills conv1's tail
@@ -285,17 +338,44 @@ struct Walk {
 
   void gn_stats(const float* A, int Ca, const float* Bs, int Cb, int HW, const std::string& n,
                 bool fusable = false) {
+    {
+      Ev e{true, false};
+      const auto pa = producer.find(A);
+      e.prod = pa != producer.end() ? pa->second : -1;
+      if (Cb > 0) {
+        const auto pb = producer.find(Bs);
+        e.prodB = pb != producer.end() ? pb->second : -1;
+      }
+      e.Cb = Cb;
+      e.HW = HW;
+      e.name = n;
+      evs.push_back(e);
+      ev_out.push_back(nullptr);
+    }
+    if (pfold.gn_ev >= 0) {   // finalized by its producer's last arrivals
+      const bool mine = pfold.gn_ev == (int)evs.size() - 1;
+      if (!mine) chk(hipErrorInvalidValue);   // the plan and the walk disagree
+      gnbuf = pfold.buf;
+      pfold = PendFold{};
+      if (mine && fold_env() < 2) return;
+      // diagnostic builds: the finalize launched as well, into the other buffer
+      // (ERTD_UNET_GNFOLD=2) or over the folded one (3)
+      if (fold_env() == 2) gnbuf = next_gnbuf();
+    } else {
+      gnbuf = next_gnbuf();
+    }
+    float2* const out = gnbuf;
     if (gn_parts_on() && HW % 256 == 0) {
       const PartRec ra = parts_of(A, Ca, HW);
       const PartRec rb = Cb > 0 ? parts_of(Bs, Cb, HW) : PartRec{nullptr, 0};
       if (dry) return;
       GnPartArgs g{ra.p, ra.np, Ca, rb.p, rb.np, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"),
-                   gnbuf, nullptr};
+                   out, nullptr};
       chk(launch_gn_finalize(g, B, s));
       return;
     }
     if (dry) return;
-    GnArgs g{A, Bs, Ca, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"), gnbuf};
+    GnArgs g{A, Bs, Ca, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"), out};
     if (fusable && bf_prec(c->precision) && fuse_gn_env() &&
         gn_act_bf16_fits(Ca + Cb, c->groups, HW)) {
       pend = g;
@@ -331,19 +411,34 @@ struct Walk {
     // fp32: GroupNorm partials of the output, when the dispatched kernel emits
     // them (the geometry-only part of the dispatch: sentinel pointers in dry runs)
     float2* gnp = nullptr;
+    int gnp_np = 0;
+    ConvArgs q{};   // the dispatch geometry (sentinel pointers)
+    q.Ca = Ca; q.Cb = Cb; q.Cin = Cin; q.Cout = Cout;
+    q.Hs = Hs; q.Ws = Ws; q.Ho = Ho; q.Wo = Wo;
+    q.ebias = ebias; q.res = res;
+    q.wpk_wino = L->offw.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
+    q.wpk_wino4 = L->offw4.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
+    q.ksplit_buf = want_split ? reinterpret_cast<float*>(16) : nullptr;
     if (gn_parts_on() && gn_out) {
-      ConvArgs q{};
-      q.Ca = Ca; q.Cb = Cb; q.Cin = Cin; q.Cout = Cout;
-      q.Hs = Hs; q.Ws = Ws; q.Ho = Ho; q.Wo = Wo;
-      q.wpk_wino = L->offw.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
-      q.wpk_wino4 = L->offw4.count(n + ".weight") ? reinterpret_cast<const float*>(16) : nullptr;
-      q.ksplit_buf = want_split ? reinterpret_cast<float*>(16) : nullptr;
       const int np = bf_prec(c->precision) ? conv_bf16_gn_parts(ks, mode, act, q, B)
                                            : conv_gn_parts(ks, mode, act, q, B);
       if (np > 0) {
         gnp = (float2*)alloc((size_t)B * Cout * np * 2);
+        gnp_np = np;
         parts[out] = PartRec{gnp, np};
       }
+    }
+    const bool fp32 = c->precision == ERTD_PREC_FP32;
+    const bool zero_cnt = fp32 && fold_cnt && fold_env() && conv_in_ok(q, ks, mode, act);
+    if (zero_cnt) cnt_zeroed = true;
+    const int ev = (int)evs.size();
+    {
+      Ev e{false, false};
+      e.foldable = gnp && fp32 && fold_cnt && cnt_zeroed && fold_env() &&
+                   conv_gn_fold_ok(ks, mode, act, q, B);
+      evs.push_back(e);
+      ev_out.push_back(out);
+      producer[out] = ev;
     }
     if (dry) return out;
     if (Cin != Ca + Cb) {
@@ -369,6 +464,22 @@ struct Walk {
     a.ksplit_buf = kbuf;
     a.gnp = gnp;
     a.split = split ? 1 : 0;
+    if (zero_cnt) {
+      a.zero_words = fold_cnt;
+      a.zero_n = B;
+    }
+    if (ev < (int)fold_at.size() && fold_at[ev] >= 0 && gnp) {
+      const Ev& g = plan_evs[fold_at[ev]];
+      const float* Bs2 = g.Cb > 0 ? ev_out[g.prodB] : nullptr;
+      const PartRec rb = g.Cb > 0 ? parts_of(Bs2, g.Cb, g.HW) : PartRec{nullptr, 0};
+      float2* const tgt = next_gnbuf();
+      a.fold.g = GnPartArgs{gnp, gnp_np, Cout, rb.p, rb.np, g.Cb, g.HW, c->groups,
+                            P(g.name + ".weight"), P(g.name + ".bias"), tgt, nullptr};
+      a.fold.cnt = fold_cnt;
+      a.fold.target = conv_gn_fold_target(a, B);
+      a.fold.B = B;
+      pfold = PendFold{fold_at[ev], tgt};
+    }
     if (has_pend) {
       has_pend = false;
       if (bimg && ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) {
@@ -414,6 +525,7 @@ struct Walk {
 
   // x (B, image^2) -> eps (B, image^2); emb_act source = ebias_all (B, ebtotal)
   void unet(const float* x, const float* ebias_all, float* eps) {
+    if (!dry && fold_cnt && fold_env() && c->precision == ERTD_PREC_FP32) plan_folds();
     const int nl = c->n_levels;
     int Hh = c->image;
     std::vector<std::pair<const float*, int>> hs;
@@ -514,7 +626,10 @@ Fixed fixed(Walk& w, int L) {
   f.partial = w.alloc((size_t)B * S * C2);
   f.Uscr = w.alloc((size_t)B * H);
   f.tdev = (int*)w.alloc(64);
-  w.gnbuf = (float2*)w.alloc((size_t)B * w.max_cin() * 2);
+  w.gnb[0] = (float2*)w.alloc((size_t)B * w.max_cin() * 2);
+  w.gnb[1] = (float2*)w.alloc((size_t)B * w.max_cin() * 2);
+  w.gnbuf = w.gnb[0];
+  w.fold_cnt = (unsigned*)w.alloc((size_t)B);
   return f;
 }
 

@@ -513,9 +513,24 @@ int conv_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B) {
   return 0;
 }
 
+bool conv_gn_fold_ok(int ks, int mode, int act, const ConvArgs& a, int B) {
+  if (conv_gn_parts(ks, mode, act, a, B) == 0) return false;
+  if (ks == 3 && mode == MODE_S1 && wino_dispatchable(a, B))
+    return a.wpk_wino4 && wino4s_ok(a.Cin, a.Ca, a.Cout, a.Wo, B) && wino4s_fold_ok(a, false, B);
+  if (wino4s_up_dispatchable(ks, mode, act, a, B)) return wino4s_fold_ok(a, true, B);
+  return false;
+}
+
+int conv_gn_fold_target(const ConvArgs& a, int B) {
+  (void)B;
+  return wino4s_fold_target(a);
+}
+
 hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
   if (a.gnp && conv_gn_parts(ks, mode, act, a, B) == 0) return hipErrorInvalidValue;
+  if (a.fold.cnt && (!a.gnp || a.fold.g.pa != a.gnp || !conv_gn_fold_ok(ks, mode, act, a, B)))
+    return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN)

@@ -300,6 +300,8 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvArgs a) {
     wl[i] = PK == PK_F32 ? packed_w0_f32(a.wpk, co, tap) : packed_w0_bf16(a.wpk, co, tap, PK == PK_SPLIT);
   }
   for (int i = tid; i < Cout; i += 256) bl[i] = a.bias ? a.bias[i] : 0.f;
+  if (a.zero_words && blockIdx.x == 0 && blockIdx.y == 0)   // the walk's GroupNorm-fold counters
+    for (int i = tid; i < a.zero_n; i += 256) a.zero_words[i] = 0u;
   constexpr int HW = WO * WO;
   const int p = blockIdx.x * 256 + tid;
   const int y = p / WO, x = p - y * WO;

@@ -111,6 +111,24 @@ __device__ __forceinline__ void at6(const f32x2 (&m)[6], f32x2 (&y)[4]) {
   y[3] = fmac(m[3], 0.125f, fmac(m[4], -8.f, d + m[5]));
 }
 
+// the GroupNorm fold's finalizes, after the MFMA waves' last item (the
+// producer waves have exited: the barrier counts the MFMA waves): samples
+// bid, bid + grid, ... -- wave 0 waits for the sample's item count (all
+// workgroups are resident: one per CU, grid <= CUs) and re-arms the counter,
+// then every MFMA wave finalizes its share of the sample's groups
+__device__ __forceinline__ void wino4s_fold_tail(const GnFold& f, int lane, int wave, int nmw) {
+  for (int b = blockIdx.x; b < f.B; b += gridDim.x) {
+    if (wave == 0 && lane == 0) {
+      const unsigned* c = f.cnt + b;
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)f.target)
+        __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_store(f.cnt + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    gn_group_finalize<true>(f.g, b, lane, wave, nmw);
+  }
+}
+
 // item it -> (K half, co group, 16-tile block): the K halves of a (co group,
 // block) adjacent, then co group, then block
 struct Item {
@@ -139,6 +157,8 @@ template <int WO, int ACT, bool UP, int XS>
 __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvArgs a, int nitems, int ksp) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* vbuf = smem;                  // [2][V_FL]
+  __shared__ int fold_items;         // GroupNorm fold: MFMA waves done with the current item
+  if (threadIdx.x == 0) fold_items = 0;
 
   constexpr int TPR = WO / 4;
   constexpr int HW = WO * WO;
@@ -591,8 +611,13 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
       if ((ln & 15) == 0) {
         const int np = TS / 16, part = (flatw % TS) / 16;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a.gnp[((size_t)smpl * a.Cout + co0 + i) * np + part] = pr[i];
+        for (int i = 0; i < 4; ++i) {
+          float2* d = a.gnp + ((size_t)smpl * a.Cout + co0 + i) * np + part;
+          if (a.fold.cnt) st_f2_wt(d, pr[i]);
+          else *d = pr[i];
+        }
       }
+      if (a.fold.cnt) gn_fold_item_done(a.fold, smpl, &fold_items, NMW, ln);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -601,6 +626,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
                                                i * HW * 4 + r * WO * 4, 0);
   }
+  if (a.fold.cnt) wino4s_fold_tail(a.fold, lane, wave, NMW);
   } else {
   // =================== MFMA waves, xi split over two waves ===================
   constexpr int NP = 9;                        // xi pairs per wave
@@ -804,8 +830,13 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
       if ((ln & 15) == 0) {
         const int np = TS / 16, part = (flatw % TS) / 16;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a.gnp[((size_t)smpl * a.Cout + co0 + i) * np + part] = pr[i];
+        for (int i = 0; i < 2; ++i) {
+          float2* d = a.gnp + ((size_t)smpl * a.Cout + co0 + i) * np + part;
+          if (a.fold.cnt) st_f2_wt(d, pr[i]);
+          else *d = pr[i];
+        }
       }
+      if (a.fold.cnt) gn_fold_item_done(a.fold, smpl, &fold_items, 4 * XS, ln);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -814,6 +845,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
                                                i * HW * 4 + r * WO * 4, 0);
   }
+  if (a.fold.cnt) wino4s_fold_tail(a.fold, lane, wave, 4 * XS);
   }
 
 }
@@ -891,6 +923,18 @@ hipError_t launch_act4s(const ConvArgs& a, int B, hipStream_t s, int cus) {
 }  // namespace
 
 int wino4s_items(int cout, int wo, int B) { return (wo / 4) * (wo / 4) / 16 * B * (cout / 64); }
+
+// the GroupNorm fold (ConvArgs::fold) rides on the emitted partials: items
+// without a K split; every MFMA wave of an item arrives once
+bool wino4s_fold_ok(const ConvArgs& a, bool up, int B) {
+  if (a.Cin % CCH || a.Ca % 2 || a.Cout % 64) return false;
+  (void)B;
+  const int xs = wino4s_xs() == 2 && a.Cin >= 16 ? 2 : 1;
+  if (xs == 2 && !up && wino4s_ksplit(a.Cin, a.Cout, a.Wo, B) && wino4s_items(a.Cout, a.Wo, B) < device_cu_count())
+    return false;
+  return true;
+}
+int wino4s_fold_target(const ConvArgs& a) { return (a.Wo / 4) * (a.Wo / 4) / 16 * (a.Cout / 64); }
 
 // ERTD_WINO4S_UP=0 keeps the sub-pixel direct kernel for the Upsample convs (A/B)
 bool wino4s_up_ok(int cin, int ca, int cout, int wo, int B) {

@@ -146,79 +146,16 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
 
-// One wave per (sample, group): lanes take the group's (channel, part)
-// items k = lane, lane + 64, ... (channel-major, possibly across both tensors
-// of a skip concatenation), float64 sums reduced in a fixed order: mean =
-// sum S / N, then M2 = sum_p [M2_p + n_p (S_p / n_p - mean)^2] (Chan et al.),
-// var = M2 / N (biased, as GroupNorm); {scale, shift} as gn_stats_kernel.
-// Channel-major items of one tensor are contiguous in its (B, C, np) partials.
+// One wave per (sample, GN_LPG-group chunk): unet.h gn_group_finalize (the
+// same arithmetic as the producing convs' GroupNorm fold): float64 Chan merge
+// of the parts {sum, M2 about the part mean} in a fixed order, var = M2 / N
+// (biased, as GroupNorm); {scale, shift} as gn_stats_kernel.
 __global__ __launch_bounds__(256) void gn_finalize_kernel(GnPartArgs a, int B) {
+  const int nparts = (a.groups + 64 / GN_LPG - 1) / (64 / GN_LPG);
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (wv >= B * a.groups) return;
-  const int b = wv / a.groups, g = wv - b * a.groups;
-  const int C = a.Ca + a.Cb, cpg = C / a.groups, c0 = g * cpg;
-  // items of the group: channels [c0, c0+cpg); channel c has np(c) parts
-  const int nA = c0 < a.Ca ? (a.Ca - c0 < cpg ? a.Ca - c0 : cpg) : 0;   // channels in tensor A
-  const int itemsA = nA * a.npa, items = itemsA + (cpg - nA) * (a.Cb > 0 ? a.npb : 0);
-  // 1 / n_p: exact for the U-Net's power-of-two part sizes
-  const double ina = 1.0 / (double)(a.HW / a.npa), inb = a.Cb > 0 ? 1.0 / (double)(a.HW / a.npb) : 0.0;
-  const double na = (double)(a.HW / a.npa), nb = a.Cb > 0 ? (double)(a.HW / a.npb) : 0.0;
-  const float2* pa = a.pa + ((size_t)b * a.Ca + c0) * a.npa;              // item k < itemsA at pa[k]
-  const float2* pb = a.Cb > 0 ? a.pb + ((size_t)b * a.Cb + (c0 + nA - a.Ca)) * a.npb : nullptr;
-  auto item = [&](int k, bool& inB) -> float2 {
-    inB = k >= itemsA;
-    if (!inB) return pa[k];                       // channel-major items are contiguous
-    return pb[k - itemsA];
-  };
-  // gamma / beta of the lane's channel loaded first (cpg <= 64 in every U-Net
-  // config; wider groups re-read them below): no memory round trip after the
-  // two reductions
-  const float gam = lane < cpg ? a.gamma[c0 + lane] : 0.f;
-  const float bet = lane < cpg ? a.beta[c0 + lane] : 0.f;
-  // at most 4 items per lane held in registers (groups up to 256 items)
-  float2 it[4];
-  bool ib[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = lane + 64 * j;
-    ib[j] = false;
-    it[j] = k < items ? item(k, ib[j]) : make_float2(0.f, 0.f);
-  }
-  double S = 0.0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) S += (double)it[j].x;
-  for (int k = lane + 256; k < items; k += 64) {   // wider groups (one group over 512 channels)
-    bool q;
-    S += (double)item(k, q).x;
-  }
-  S = wave_sum_d(S);
-  const double N = (double)cpg * a.HW;
-  const double mean = S / N;
-  double M2 = 0.0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (lane + 64 * j < items) {
-      const double n = ib[j] ? nb : na;
-      const double d = (double)it[j].x * (ib[j] ? inb : ina) - mean;
-      M2 += (double)it[j].y + n * d * d;
-    }
-  for (int k = lane + 256; k < items; k += 64) {
-    bool q;
-    const float2 v = item(k, q);
-    const double d = (double)v.x * (q ? inb : ina) - mean;
-    M2 += (double)v.y + (q ? nb : na) * d * d;
-  }
-  M2 = wave_sum_d(M2);
-  double var = M2 / N;
-  var = var > 0.0 ? var : 0.0;
-  const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
-  if (a.mr && lane == 0) a.mr[(size_t)b * a.groups + g] = make_float2((float)mean, rstd);
-  for (int cl = lane; cl < cpg; cl += 64) {
-    const int c = c0 + cl;
-    const float scale = rstd * (cl < 64 ? gam : a.gamma[c]);
-    const float shift = -scale * (float)mean + (cl < 64 ? bet : a.beta[c]);
-    a.out[(size_t)b * C + c] = make_float2(scale, shift);
-  }
+  if (wv >= B * nparts) return;
+  const int b = wv / nparts;
+  gn_group_finalize<false>(a, b, lane, wv - b * nparts, nparts);
 }
 
 hipError_t launch_gn_finalize(const GnPartArgs& a, int B, hipStream_t s) {
@@ -226,7 +163,7 @@ hipError_t launch_gn_finalize(const GnPartArgs& a, int B, hipStream_t s) {
   if (!a.pa || a.npa < 1 || a.Ca < 1 || (a.Cb > 0 && (!a.pb || a.npb < 1)) || a.groups < 1 ||
       C % a.groups || a.HW % a.npa || (a.Cb > 0 && a.HW % a.npb))
     return hipErrorInvalidValue;
-  const int n = B * a.groups;   // one wave each
+  const int n = B * ((a.groups + 64 / GN_LPG - 1) / (64 / GN_LPG));   // one wave each
   gn_finalize_kernel<<<(n + 3) / 4, 256, 0, s>>>(a, B);
   return hipGetLastError();
 }
