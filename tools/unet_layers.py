@@ -11,7 +11,7 @@ import sys
 cfgname = sys.argv[2] if len(sys.argv) > 2 else "U2"
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 64
 CFG = {"U1": (32, 32, (1, 2), 2, False), "U2": (64, 64, (1, 2, 4), 2, False),
-       "U3": (64, 64, (1, 2, 4), 2, True)}[cfgname]
+       "U3": (64, 64, (1, 2, 4), 2, True), "U5": (128, 128, (1, 1, 2, 2), 2, True)}[cfgname]
 image, ch0, mult, nres, attn = CFG
 
 
