@@ -648,7 +648,7 @@ __device__ __forceinline__ void mfma_pipe(f32x16& acc, FA fa, FB fb) {
   }
 }
 #ifndef CBW_ORDER
-#define CBW_ORDER 1
+#define CBW_ORDER 0   // 1: chain items two per CU first (A/B: 21.8 vs 19.5 us, slower)
 #endif
 #ifndef CBW_AHEAD
 #define CBW_AHEAD 6
@@ -730,9 +730,9 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
   __shared__ __attribute__((aligned(16))) ConvBwdSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
-  // dispatch order: chain items [0, c1), dW2 items [0, c2), the remaining chain
-  // items, the remaining dW2 items -- c1 = 2 and c2 = 1 per CU, so the first
-  // round of slots holds at most two chain blocks per CU
+  // dispatch order: all chain blocks, then all dW2 blocks (CBW_ORDER = 1: chain
+  // items [0, c1), dW2 items [0, c2), the remaining chain items, the remaining
+  // dW2 items, c1 = 2 and c2 = 1 per CU -- measured slower)
   const int nit = (int)gridDim.x / 2, bi = (int)blockIdx.x;
   const bool w2blk = CBW_ORDER ? (bi >= c1 && bi < c1 + c2) || bi >= nit + c2 : bi >= nit;
   const int item = !CBW_ORDER ? (w2blk ? bi - nit : bi)

@@ -214,6 +214,127 @@ __global__ __launch_bounds__(1024) void conv_out_kernel(ConvArgs a) {
   *reinterpret_cast<float4*>(a.out + o) = v;
 }
 
+// W = 64 (U2 / U3): one wave per 64-pixel image row strip of CO64_R rows,
+// lane = column, the column neighbours by full-wave DPP shifts (zero fill =
+// the conv's padding); the 4 waves of a workgroup take channels w, w + 4, ...
+// of the same strip and their sums meet in LDS in a fixed order.  Every input
+// value is loaded and activated once per strip (R + 2 rows for R outputs), the
+// loads of the next CO64_PF channels in flight over the current one's fmas.
+// Per output and channel the 9 taps run in (ky, kx) order, as the MFMA kernels.
+#ifndef CO64_R
+#define CO64_R 8
+#endif
+#ifndef CO64_PF
+#define CO64_PF 2
+#endif
+__device__ __forceinline__ float wave_shr1(float v) {   // lane i <- lane i - 1, lane 0 <- 0
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float wave_shl1(float v) {   // lane i <- lane i + 1, lane 63 <- 0
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, true));
+}
+template <int ACT, int PK>
+__global__ __launch_bounds__(256) void conv_out64_kernel(ConvArgs a) {
+  constexpr int W = 64, R = CO64_R, NR = R + 2, NW = 4, PF = CO64_PF;
+  constexpr bool BF = PK == PK_BF16;
+  extern __shared__ __attribute__((aligned(16))) float smo[];
+  const int Cin = a.Cin, Ca = a.Ca;
+  float* wl = smo;                                         // [Cin][9]
+  float2* gtab = reinterpret_cast<float2*>(smo + ((Cin * 9 + 1) & ~1));   // [Cin]
+  float* red = reinterpret_cast<float*>(gtab + Cin);       // [NW][R][64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.y, y0 = blockIdx.x * R;
+  for (int i = tid; i < Cin * 9; i += 256) {
+    const int ci = i / 9, tap = i - ci * 9;
+    wl[i] = PK == PK_F32 ? packed_w_f32(a.wpk, ci, tap) : packed_w_bf16(a.wpk, ci, tap, PK == PK_SPLIT);
+  }
+  if constexpr (ACT != ACT_NONE) {
+    for (int c = tid; c < Cin; c += 256) gtab[c] = a.gn[(size_t)b * Cin + c];
+  }
+  constexpr size_t plane = (size_t)W * W;
+  auto ldrows = [&](int c, float (&v)[NR]) {
+    if (c >= Cin) return;
+    const float* src = c < Ca ? a.srcA + ((size_t)b * Ca + c) * plane : a.srcB + ((size_t)b * a.Cb + (c - Ca)) * plane;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int iy = y0 - 1 + r;
+      v[r] = (iy >= 0 && iy < W) ? src[iy * W + lane] : 0.f;
+    }
+  };
+  float ring[PF + 1][NR];
+  float acc[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int q = 0; q < PF; ++q) ldrows(wave + NW * q, ring[q]);
+  __syncthreads();   // weights and the GroupNorm table
+  const int nch = (Cin - wave + NW - 1) / NW;             // this wave's channels
+  for (int k = 0; k < nch; k += PF + 1) {
+#pragma unroll
+    for (int q = 0; q <= PF; ++q) {
+      // channel k + q in ring slot q; the load of channel k + q + PF into slot (q + PF) % (PF + 1)
+      if (k + q >= nch) break;
+      const int c = wave + NW * (k + q);
+      ldrows(c + NW * PF, ring[(q + PF) % (PF + 1)]);
+      const float* wp = wl + c * 9;
+      float g0 = 1.f, g1 = 0.f;
+      if constexpr (ACT != ACT_NONE) {
+        const float2 g = gtab[c];
+        g0 = g.x;
+        g1 = g.y;
+      }
+      float w[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) w[t] = wp[t];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int iy = y0 - 1 + r;
+        float v = ring[q][r];
+        if constexpr (ACT != ACT_NONE) {
+          v = fmaf(v, g0, g1);
+          if constexpr (ACT == ACT_GN_SILU) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+        }
+        if constexpr (BF) v = round_bf16(v);
+        v = (iy >= 0 && iy < W) ? v : 0.f;                 // the padding rows (after the activation)
+        const float l = wave_shr1(v), rr = wave_shl1(v);
+#pragma unroll
+        for (int ky = 2; ky >= 0; --ky) {                  // output row j = r - ky: its ky-th input row
+          const int j = r - ky;
+          if (j >= 0 && j < R) {
+            acc[j] = fmaf(w[ky * 3], l, acc[j]);
+            acc[j] = fmaf(w[ky * 3 + 1], v, acc[j]);
+            acc[j] = fmaf(w[ky * 3 + 2], rr, acc[j]);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) red[(wave * R + j) * 64 + lane] = acc[j];
+  __syncthreads();
+  // the waves' partial sums in wave order, then the MFMA kernels' epilogue order
+  const float bb = a.bias ? a.bias[0] : 0.f;
+  const float e = a.ebias ? a.ebias[(size_t)b * a.eb_stride] : 0.f;
+  for (int o = tid; o < R * 64; o += 256) {
+    const int j = o >> 6, x = o & 63;
+    float v = (red[(0 * R + j) * 64 + x] + red[(1 * R + j) * 64 + x]) + (red[(2 * R + j) * 64 + x] + red[(3 * R + j) * 64 + x]);
+    v = v + bb;
+    if (a.ebias) v = v + e;
+    const size_t oi = (size_t)b * plane + (size_t)(y0 + j) * W + x;
+    if (a.res) v = v + a.res[oi];
+    a.out[oi] = v;
+  }
+}
+
+template <int ACT, int PK>
+hipError_t launch_co64(const ConvArgs& a, int B, hipStream_t s) {
+  constexpr int R = CO64_R;
+  const size_t lds = (((size_t)a.Cin * 9 + 1) & ~(size_t)1) * 4 + (size_t)a.Cin * 8 + (size_t)4 * R * 64 * 4;
+  if (lds > 65536) return hipErrorInvalidValue;
+  conv_out64_kernel<ACT, PK><<<dim3(64 / R, (unsigned)B), 256, lds, s>>>(a);
+  return hipGetLastError();
+}
+
 template <int ACT, int WO, int RWS, int BF, int NS>
 hipError_t launch_co(const ConvArgs& a, int B, hipStream_t s) {
   using G = OutGeom<WO, RWS, NS>;
@@ -238,6 +359,9 @@ static int conv_out_ns() {
   return v;
 }
 
+#ifndef CONV_OUT_RDIV
+#define CONV_OUT_RDIV 1   // A/B: rows per workgroup divided by this (more, smaller workgroups)
+#endif
 // rows per workgroup: 256 threads per channel group (16 rows; 8 at W = 128;
 // the whole image at W = 16).  Measured on a U2 B=64 step (64x64), one group:
 // 16 rows (256 workgroups) 60.5 us, 4 rows (1024 one-wave workgroups) 70.5 us
@@ -246,11 +370,20 @@ static int conv_out_ns() {
 template <int ACT, int WO, int BF>
 hipError_t launch_co_r(const ConvArgs& a, int B, hipStream_t s) {
   constexpr int TPR = WO / 4;
-  constexpr int R = (256 / TPR) < WO ? (256 / TPR) : WO;
+  constexpr int R0 = (256 / TPR) < WO ? (256 / TPR) : WO;
+  constexpr int R = CONV_OUT_RDIV > 1 && R0 / CONV_OUT_RDIV * TPR >= 64 ? R0 / CONV_OUT_RDIV : R0;
   const int ns = conv_out_ns();
   if (ns == 1) return launch_co<ACT, WO, R, BF, 1>(a, B, s);
   if (ns == 2) return launch_co<ACT, WO, R, BF, 2>(a, B, s);
   return launch_co<ACT, WO, R, BF, 4>(a, B, s);
+}
+
+// ERTD_CONV_OUT64=0 keeps the LDS-staged kernel at W = 64 (A/B)
+static int conv_out64_env() {
+  static const int v = [] {
+    return ERTD_KNOB("CONV_OUT64", 1);
+  }();
+  return v;
 }
 
 template <int ACT, int BF>
@@ -258,7 +391,7 @@ hipError_t launch_co_w(const ConvArgs& a, int B, hipStream_t s) {
   switch (a.Wo) {
     case 16: return launch_co_r<ACT, 16, BF>(a, B, s);
     case 32: return launch_co_r<ACT, 32, BF>(a, B, s);
-    case 64: return launch_co_r<ACT, 64, BF>(a, B, s);
+    case 64: return conv_out64_env() ? launch_co64<ACT, BF>(a, B, s) : launch_co_r<ACT, 64, BF>(a, B, s);
     case 128: return launch_co_r<ACT, 128, BF>(a, B, s);
     default: return hipErrorInvalidValue;
   }

@@ -58,6 +58,9 @@ constexpr int NRS = 3;                        // producer register sets
 #ifndef WINO4S_MPRIO
 #define WINO4S_MPRIO 1                        // s_setprio of the xh = 1 MFMA waves (0 = none): +0.3-0.7 % U2 B=64
 #endif
+#ifndef WINO4S_XCD
+#define WINO4S_XCD 1                          // XCD-aware item walk (0: blockIdx order)
+#endif
 #ifndef WINO4S_PACK
 #define WINO4S_PACK 1                         // producer stage on packed fp32 pairs
 #endif
@@ -143,6 +146,12 @@ __device__ __forceinline__ Item item_of(int it, int ncog, int ksp) {
   return r;
 }
 
+// a workgroup's items in walk order: item base + il stride
+struct ItemWalk {
+  int base, stride, ncog, ksp;
+  __device__ __forceinline__ Item at(int il) const { return item_of(base + il * stride, ncog, ksp); }
+};
+
 // UP: the Upsample conv, conv3x3 of the nearest-x2 upsampled source (WO / 2)^2:
 // the window rows 4ty-1 .. 4ty+4 of the upsampled image are source rows 2ty-1,
 // 2ty, 2ty, 2ty+1, 2ty+1, 2ty+2 and a lane's two columns one source column, so
@@ -175,7 +184,15 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   // added by a separate pass -- layers whose items would fill only half the CUs
   const int nchunk = Cin / CCH / ksp;          // chunks per item
   const int ncog = a.Cout / 64;
-  const int bid = blockIdx.x, G = gridDim.x;
+  // XCD-aware item walk: workgroups are dealt round-robin to the 8 XCDs
+  // (blockIdx % 8); the remap hands each XCD runs of consecutive items (a
+  // sample's tile rows and co groups), so the tile-row halos and the input a
+  // sample's co groups share come from that XCD's L2 (U2 B=64: 8.6 -> 7.9 GB
+  // of HBM traffic per step, time unchanged within noise)
+  const int G = gridDim.x;
+  const int bid = (WINO4S_XCD && G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8)
+                                             : (int)blockIdx.x;
+  const ItemWalk wk{bid, G, ncog, ksp};
   const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;
   const int gtot = nloc * nchunk;
 
@@ -196,7 +213,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     unsigned roff[6];   // per window row (UP: per distinct source row, 4)
     f32x4 cur_pad;
     auto set_item = [&](int il) {
-      const Item itm = item_of(bid + il * G, ncog, ksp);
+      const Item itm = wk.at(il);
       cur_k0 = itm.half * nchunk;
       const int flat0 = itm.blk * 16;
       cur_b = flat0 / TS;
@@ -415,7 +432,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   int u_il = 0, u_ks = 0;
   int u_base = 0;                              // byte offset of (cog, ks = 0) of item u_il
   auto u_item = [&](int il) {
-    const Item itm = item_of(bid + il * G, ncog, ksp);
+    const Item itm = wk.at(il);
     u_base = itm.cog * nks * 36864;
   };
   auto u_advance = [&]() {
@@ -526,7 +543,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
       continue;
     }
     // ---- output transform: lane l holds M[xi] of co = 16 cb + 4 (l >> 4) + i, tile l & 15
-    const Item itm = item_of(bid + il * G, ncog, ksp);
+    const Item itm = wk.at(il);
     const int flatw = itm.blk * 16;
     const int smpl = flatw / TS;
     const bool has_eb = a.ebias != nullptr, has_res = a.res != nullptr, has_bias = a.bias != nullptr;
@@ -642,7 +659,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   // U cursor over the item's k-steps [u_ks0, u_end) (its K half)
   int u_il = 0, u_ks = 0, u_end = 0, u_base = 0;
   auto u_item = [&](int il) {
-    const Item itm = item_of(bid + il * G, ncog, ksp);
+    const Item itm = wk.at(il);
     u_base = itm.cog * nks * 36864;
     u_ks = itm.half * nchunk * 2;
     u_end = u_ks + nchunk * 2;
@@ -769,7 +786,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
           y[1][r][x + 1] = q1.y;
         }
     }
-    const Item itm = item_of(bid + il * G, ncog, ksp);
+    const Item itm = wk.at(il);
     const int flatw = itm.blk * 16;
     const int smpl = flatw / TS;
     const bool part2 = itm.half != 0;          // second K half: raw sums to ksplit_buf
