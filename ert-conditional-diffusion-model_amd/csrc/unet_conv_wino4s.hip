@@ -184,14 +184,17 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   // added by a separate pass -- layers whose items would fill only half the CUs
   const int nchunk = Cin / CCH / ksp;          // chunks per item
   const int ncog = a.Cout / 64;
-  // XCD-aware item walk: workgroups are dealt round-robin to the 8 XCDs
-  // (blockIdx % 8); the remap hands each XCD runs of consecutive items (a
-  // sample's tile rows and co groups), so the tile-row halos and the input a
-  // sample's co groups share come from that XCD's L2 (U2 B=64: 8.6 -> 7.9 GB
-  // of HBM traffic per step, time unchanged within noise)
+  // XCD-aware item walk for layers of one or two co groups: workgroups are
+  // dealt round-robin to the 8 XCDs (blockIdx % 8); the remap hands each XCD
+  // runs of consecutive items (a sample's tile rows and its co groups), so the
+  // tile-row halos and the input both co groups read come from that XCD's L2.
+  // With 4-8 co groups (the 16x16 level, the 16 -> 32 Upsample conv) the
+  // blockIdx order keeps one co group's transformed weights (2.4-9.4 MB of
+  // them) per XCD (cog = bid % ncog), which saves more (PMC, U2 B=64:
+  // profiles/r05_u2_layer_traffic.txt).
   const int G = gridDim.x;
-  const int bid = (WINO4S_XCD && G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8)
-                                             : (int)blockIdx.x;
+  const int bid = (WINO4S_XCD && G % 8 == 0 && ncog <= 2)
+                      ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const ItemWalk wk{bid, G, ncog, ksp};
   const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;
   const int gtot = nloc * nchunk;

@@ -27,7 +27,7 @@ a = ap.parse_args()
 
 CFGS = {"U1": (32, 32, (1, 2), 2, False), "U2": (64, 64, (1, 2, 4), 2, False),
         "U3": (64, 64, (1, 2, 4), 2, True), "U5": (128, 128, (1, 1, 2, 2), 2, True)}
-KEYS = ("conv_kernel<", "conv_out_kernel<", "conv_in_kernel<", "conv_wino_kernel<", "conv_wino4_kernel<",
+KEYS = ("conv_kernel<", "conv_out_kernel<", "conv_out64_kernel<", "conv_in_kernel<", "conv_wino_kernel<", "conv_wino4_kernel<",
         "conv_wino4s_kernel<", "conv1x1_kernel<", "conv_bf16_kernel<")
 
 
@@ -149,5 +149,12 @@ if a.json:
         "by_conv_kernel": {k: {"launches": n, "hbm_bytes": int(p), "alg_bytes": int(q)} for k, (n, p, q) in fam.items()},
         "other_kernels": {k: {"launches": n, "hbm_bytes": int(b)} for k, (n, b) in other.items()},
         "step_hbm_bytes": int(tot_pmc + tot_other), "convs_alg_bytes": int(tot_alg),
+    }
+    # the step total under the key bench.py's headline roofline reads (traffic)
+    rec[f"unet_{a.cfg}_B{B}_fp32_step"] = {
+        "kernel": "all ertd::unet:: kernels of one U-Net sampler step",
+        "hbm_bytes_per_launch": int(tot_pmc + tot_other),
+        "method": rec[key]["method"], "per_kernel_key": key,
+        "workload": f"tools/unet_probe.py {a.cfg} fp32 B={B} L=4693, the last sampler step of the run",
     }
     json.dump(rec, open(a.json, "w"), indent=1)
