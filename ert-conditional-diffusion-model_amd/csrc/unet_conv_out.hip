@@ -225,7 +225,7 @@ __global__ __launch_bounds__(1024) void conv_out_kernel(ConvArgs a) {
 #define CO64_R 8
 #endif
 #ifndef CO64_PF
-#define CO64_PF 2
+#define CO64_PF 3
 #endif
 __device__ __forceinline__ float wave_shr1(float v) {   // lane i <- lane i - 1, lane 0 <- 0
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, true));
