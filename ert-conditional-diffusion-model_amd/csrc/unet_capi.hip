@@ -797,6 +797,11 @@ struct ertd_unet_plan {
   hipEvent_t evf = nullptr, evj = nullptr, eve = nullptr;
   hipGraph_t g_head = nullptr, g_step = nullptr;
   hipGraphExec_t x_head = nullptr, x_step = nullptr;
+  // MULTI consecutive steps captured as one graph: one launch (and its ~8 us
+  // graph-boundary gap) per MULTI steps instead of per step
+  hipGraph_t g_multi = nullptr;
+  hipGraphExec_t x_multi = nullptr;
+  int multi = 0;
 };
 
 extern "C" {
@@ -1374,16 +1379,24 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evj, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->eve, hipEventDisableTiming);
   }
-  for (int k = 0; e == hipSuccess && k < 2; ++k) {
+  const int multi = ERTD_KNOB("UNET_MULTI", 8);   // U2 B=64: 248.6 (1) vs 249.0 (4) vs 249.4 (8) steps/s
+  const int ngraphs = multi > 1 && n_run >= 2 * multi ? 3 : 2;
+  for (int k = 0; e == hipSuccess && k < ngraphs; ++k) {
     e = hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal);
     if (e != hipSuccess) break;
-    r = k == 0 ? p->call.head(p->stream) : p->call.step(p->stream, p->side, p->evf, p->evj, p->eve);
+    if (k == 0) {
+      r = p->call.head(p->stream);
+    } else {
+      for (int i = 0; r == ERTD_OK && i < (k == 1 ? 1 : multi); ++i)
+        r = p->call.step(p->stream, p->side, p->evf, p->evj, p->eve);
+    }
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(p->stream, &g);
-    (k == 0 ? p->g_head : p->g_step) = g;
+    (k == 0 ? p->g_head : k == 1 ? p->g_step : p->g_multi) = g;
     if (r != ERTD_OK) break;
     if (e == hipSuccess)
-      e = hipGraphInstantiate(k == 0 ? &p->x_head : &p->x_step, g, nullptr, nullptr, 0);
+      e = hipGraphInstantiate(k == 0 ? &p->x_head : k == 1 ? &p->x_step : &p->x_multi, g, nullptr, nullptr, 0);
+    if (k == 2 && e == hipSuccess) p->multi = multi;
   }
   if (r != ERTD_OK || e != hipSuccess) {
     ertd_unet_plan_destroy(p);
@@ -1397,7 +1410,10 @@ int ertd_unet_plan_launch_steps(ertd_unet_plan* p, int n_steps, void* stream) {
   if (!p || !p->x_head || !p->x_step || n_steps < 0 || n_steps > p->call.n_run) return ERTD_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipGraphLaunch(p->x_head, s);
-  for (int i = 0; e == hipSuccess && i < n_steps; ++i) e = hipGraphLaunch(p->x_step, s);
+  int i = 0;
+  if (p->x_multi)
+    for (; e == hipSuccess && i + p->multi <= n_steps; i += p->multi) e = hipGraphLaunch(p->x_multi, s);
+  for (; e == hipSuccess && i < n_steps; ++i) e = hipGraphLaunch(p->x_step, s);
   return rcode(e);
 }
 
@@ -1410,6 +1426,8 @@ int ertd_unet_plan_destroy(ertd_unet_plan* p) {
   if (!p) return ERTD_OK;
   if (p->x_head) (void)hipGraphExecDestroy(p->x_head);
   if (p->x_step) (void)hipGraphExecDestroy(p->x_step);
+  if (p->x_multi) (void)hipGraphExecDestroy(p->x_multi);
+  if (p->g_multi) (void)hipGraphDestroy(p->g_multi);
   if (p->g_head) (void)hipGraphDestroy(p->g_head);
   if (p->g_step) (void)hipGraphDestroy(p->g_step);
   if (p->stream) (void)hipStreamDestroy(p->stream);

@@ -189,37 +189,45 @@ __global__ __launch_bounds__(256) void dense_kernel(DenseArgs a) {
     }
   }
   __syncthreads();
-  const int o = blockIdx.x * 256 + tid;
-  if (o >= a.O) return;
+  // 64 outputs per workgroup, K split in four quarters (one per wave): each
+  // thread runs one k-ordered fma chain over its quarter with every weight
+  // load of a 64-step batch in flight (K = 256: one memory latency instead of
+  // four), the quarters then added in order (q0 + q1) + (q2 + q3)
+  __shared__ float part[4][64];
+  const int ol = tid & 63, q = tid >> 6;
+  const int o = blockIdx.x * 64 + ol;
+  const int kq = (K + 3) / 4, kb = q * kq, ke = min(K, kb + kq);
   float acc = 0.f;
-  // 64 (then 16) weight loads in flight per batch: a load per k-step consumed
-  // at once waited a full memory latency each (K = 256: 4 latencies instead of
-  // 16, same k-ordered chain, bitwise equal); the K % 16 tail continues the
-  // same chain (any ch the config check accepts, e.g. ch = 8 or 24)
-  const int K64 = K & ~63, K16 = K & ~15;
-  for (int k0 = 0; k0 < K64; k0 += 64) {
-    float w[64];
+  if (o < a.O) {
+    int k0 = kb;
+    for (; k0 + 64 <= ke; k0 += 64) {
+      float w[64];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) w[j] = a.wt[(size_t)(k0 + j) * a.O + o];
+      for (int j = 0; j < 64; ++j) w[j] = a.wt[(size_t)(k0 + j) * a.O + o];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) acc = fmaf(xin[k0 + j], w[j], acc);
+      for (int j = 0; j < 64; ++j) acc = fmaf(xin[k0 + j], w[j], acc);
+    }
+    for (; k0 + 16 <= ke; k0 += 16) {
+      float w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = a.wt[(size_t)(k0 + j) * a.O + o];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc = fmaf(xin[k0 + j], w[j], acc);
+    }
+    for (; k0 < ke; ++k0) acc = fmaf(xin[k0], a.wt[(size_t)k0 * a.O + o], acc);
   }
-  for (int k0 = K64; k0 < K16; k0 += 16) {
-    float w[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = a.wt[(size_t)(k0 + j) * a.O + o];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc = fmaf(xin[k0 + j], w[j], acc);
-  }
-  for (int k = K16; k < K; ++k) acc = fmaf(xin[k], a.wt[(size_t)k * a.O + o], acc);
-  float v = acc + a.bias[o];
+  part[q][ol] = acc;
+  __syncthreads();
+  if (q != 0 || o >= a.O) return;
+  float v = (part[0][ol] + part[1][ol]) + (part[2][ol] + part[3][ol]);
+  v = v + a.bias[o];
   if (a.add) v = v + a.add[(size_t)(a.add_bcast ? 0 : b) * a.add_stride + o];
   a.y[(size_t)b * a.y_stride + o] = v;
 }
 
 hipError_t launch_dense(int din, const DenseArgs& a, int B, hipStream_t s) {
   if (a.K < 1 || a.O < 1) return hipErrorInvalidValue;
-  dim3 grid((a.O + 255) / 256, B);
+  dim3 grid((a.O + 63) / 64, B);
   const size_t lds = (size_t)a.K * sizeof(float);
   if (din == DIN_PLAIN) dense_kernel<DIN_PLAIN><<<grid, 256, lds, s>>>(a);
   else if (din == DIN_SILU) dense_kernel<DIN_SILU><<<grid, 256, lds, s>>>(a);
