@@ -757,12 +757,13 @@ struct SampleCall {
     w.chk(launch_set_word(f.tdev, t_first, s));
     return rcode(w.err);
   }
+  // skip_side: the ResBlock skip convs on s2 too (else only the embedding branch)
   int step(hipStream_t s, hipStream_t s2 = nullptr, hipEvent_t evf = nullptr,
-           hipEvent_t evj = nullptr, hipEvent_t eve = nullptr) const {
+           hipEvent_t evj = nullptr, hipEvent_t eve = nullptr, bool skip_side = true) const {
     const Layout Lo = layout_with_freq(c);
     Walk w{c, &Lo, packed, (char*)ws, 0, B, s, false};
     w.cap = ws_bytes;
-    w.s2 = s2;
+    w.s2 = skip_side ? s2 : nullptr;
     w.evf = evf;
     w.evj = evj;
     const Fixed f = fixed(w, L);
@@ -802,6 +803,7 @@ struct ertd_unet_plan {
   hipGraph_t g_multi = nullptr;
   hipGraphExec_t x_multi = nullptr;
   int multi = 0;
+  bool skip_side = false;                // the skip convs on the side stream too
 };
 
 extern "C" {
@@ -1373,7 +1375,12 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
   // ERTD_UNET_SIDE=0/1 overrides (A/B).
   const int sv = ERTD_KNOB("UNET_SIDE", -1);
   const bool side = sv >= 0 ? sv != 0 : bf_prec(c->precision);
-  if (e == hipSuccess && side) {
+  // the embedding branch alone beside conv_in and the first GroupNorm
+  // (ERTD_UNET_SIDE_EMB=1, A/B): slower, U2 B=64 246.1 vs 249.7 steps/s -- the
+  // cross-queue event waits of a forked graph cost more than the overlap
+  const bool side_emb = ERTD_KNOB("UNET_SIDE_EMB", 0) != 0;
+  p->skip_side = side;
+  if (e == hipSuccess && (side || side_emb)) {
     e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evf, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->evj, hipEventDisableTiming);
@@ -1388,7 +1395,7 @@ int ertd_unet_sample_plan_create(const ertd_unet_config* c, const float* packed,
       r = p->call.head(p->stream);
     } else {
       for (int i = 0; r == ERTD_OK && i < (k == 1 ? 1 : multi); ++i)
-        r = p->call.step(p->stream, p->side, p->evf, p->evj, p->eve);
+        r = p->call.step(p->stream, p->side, p->evf, p->evj, p->eve, p->skip_side);
     }
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(p->stream, &g);
