@@ -653,6 +653,10 @@ __device__ __forceinline__ void mfma_pipe(f32x16& acc, FA fa, FB fb) {
 #ifndef CBW_AHEAD
 #define CBW_AHEAD 6
 #endif
+#ifndef CBW_PB16
+#define CBW_PB16 1   // phase B: 32x32 tile + 16x16x4 edge tiles (0: two padded 32x32 tiles)
+#endif
+using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 __device__ __forceinline__ void store_tile_rows(float (*red)[33], const f32x16& acc, int h, int l32) {
 #pragma unroll
@@ -819,6 +823,79 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
 
   // ---- phase B: dW1[o][n = c*3+kk] = sum_r dz1[o][r] * cond[c][4*j0 + 2r - 1 + kk];
   //      column n = 42 (padding) multiplies by ones: db1[o] = sum_r dz1[o][r]
+#if CBW_PB16
+  // columns 0-31: one 32x32x2 tile, its 64 k-steps split 24/24/8/8 over the
+  // four waves; columns 32-47 (the 10 remaining weights and the db1 column):
+  // 16x16x4 tiles, rows 0-15 in wave 2, 16-31 in wave 3 (32 k-steps each, two
+  // accumulators) -- 1536 MFMA cycles per wave instead of 2048 for a 64-wide
+  // N padded to two 32x32 tiles
+  f32x4 acc1 = {};
+  {
+    const int c = l32 / 3, kk = l32 - 3 * (l32 / 3);
+    const int u0 = 2 * h + 2 + kk;  // u = 4s + u0 for r = 2s + h
+    const int s0 = wave < 2 ? 24 * wave : 48 + 8 * (wave - 2);
+    const float* xr = &sm.X[u0 & 3][c][u0 >> 2] + s0;
+    const float* zr = &sm.DZ1[l32][h] + 2 * s0;
+    f32x16 acc = {};
+    if (wave < 2) {
+      mfma_pipe<24, CBW_AHEAD>(acc, [&](int s) { return zr[2 * s]; }, [&](int s) { return xr[s]; });
+    } else {
+      mfma_pipe<8, CBW_AHEAD>(acc, [&](int s) { return zr[2 * s]; }, [&](int s) { return xr[s]; });
+      // lane: row o = 16 (wave - 2) + q, column n = 32 + q, k: r = 64 half + 16 kq + s
+      // (DZ1 reads conflict-free: bank = q + 16 kq + s)
+      const int q = lane & 15, kq = lane >> 4;
+      const int n1 = 32 + q;
+      const bool nv = n1 < K1;
+      const float pad = n1 == K1 ? 1.f : 0.f;
+      const int cc = nv ? n1 / 3 : 0, k1 = nv ? n1 - 3 * (n1 / 3) : 0;
+      // u = 2r + 2 + k1 = 128 half + 32 kq + 4 (s >> 1) + w, w = 2 + k1 + 2 (s & 1)
+      const int w0 = 2 + k1, w1 = 4 + k1;
+      const float* xe = &sm.X[w0 & 3][cc][8 * kq + (w0 >> 2)];
+      const float* xo = &sm.X[w1 & 3][cc][8 * kq + (w1 >> 2)];
+      const float* zq = &sm.DZ1[16 * (wave - 2) + q][16 * kq];
+      f32x4 a0 = {}, a1 = {};
+      float ra[4], rb[4];
+      auto fa = [&](int t) { return zq[64 * (t >> 4) + (t & 15)]; };
+      auto fb = [&](int t) {
+        const int s = t & 15, off = 32 * (t >> 4) + (s >> 1);
+        return nv ? ((s & 1) ? xo[off] : xe[off]) : pad;
+      };
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ra[i] = fa(i);
+        rb[i] = fb(i);
+      }
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        const float a = ra[t & 3], b = rb[t & 3];
+        if (t + 4 < 32) {
+          ra[t & 3] = fa(t + 4);
+          rb[t & 3] = fb(t + 4);
+        }
+        if (t & 1) a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, a1, 0, 0, 0);
+        else a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, a0, 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      acc1 = a0 + a1;
+    }
+    store_tile_rows(sm.red[wave], acc, h, l32);  // red aliases the dead a1 images
+  }
+  if (wave >= 2) {  // rows o = 16 (wave - 2) + 4 (lane >> 4) + i, column 32 + (lane & 15)
+    const int n1 = 32 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = 16 * (wave - 2) + 4 * (lane >> 4) + i;
+      if (n1 < K1) G[NG_W1 + o * K1 + n1] = acc1[i];
+      else if (n1 == K1) G[NG_B1 + o] = acc1[i];
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < C1 * 32; idx += 256) {  // the k-quarters combined in order
+    const int o = idx >> 5, col = idx & 31;
+    G[NG_W1 + o * K1 + col] = (sm.red[0][o][col] + sm.red[1][o][col]) + (sm.red[2][o][col] + sm.red[3][o][col]);
+  }
+#else
   {
     const int nt = wave & 1, rh = wave >> 1;
     const int n = nt * 32 + l32;
@@ -850,6 +927,7 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     G[NG_W1 + idx] = sm.red[nt][o][col] + sm.red[2 + nt][o][col];
   }
   if (tid < C1) G[NG_B1 + tid] = sm.red[1][tid][K1 - 32] + sm.red[3][tid][K1 - 32];
+#endif
 }
 
 // ---------------------------------------------------------------------------
