@@ -329,7 +329,9 @@ def train_bench(dev, steps=200, B=32, T=500, reps=200):
         rounds.append(e0.elapsed_time(e1) / reps)
     avg_ms = sum(rounds) / len(rounds)
     flop = CONV_BWD_FLOP_PER_MEMBER * B
-    executed = 512 * 2 * 32 * 32 * 2 * B * STRIPS_MEAS   # 512 v_mfma_f32_32x32x2 per workgroup
+    # per (member, strip): 448 v_mfma_f32_32x32x2 + 64 v_mfma_f32_16x16x4 (the dW1 edge
+    # columns, half the FLOP each) over its chain and dW2 workgroups
+    executed = (448 + 64 // 2) * 2 * 32 * 32 * 2 * B * STRIPS_MEAS
     ach = flop / (avg_ms * 1e-3) / 1e12
     out["train_roofline"] = {
         "kernel": "conv_bwd_kernel", "bound": "mfma", "achieved": round(ach, 3),
