@@ -507,7 +507,10 @@ static bool wino4s_up_dispatchable(int ks, int mode, int act, const ConvArgs& a,
 
 int conv_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B) {
   if (a.Cout == 1 && ks == 3 && mode == MODE_S1 && act != ACT_GN) return 0;   // conv_out
-  if (conv_in_ok(a, ks, mode, act)) return 0;
+#ifndef CONV_IN_PARTS
+#define CONV_IN_PARTS 1   // 0 (A/B only): conv_in emits no partials, the walk runs a partials pass
+#endif
+  if (conv_in_ok(a, ks, mode, act)) return CONV_IN_PARTS ? a.Wo * a.Wo / 256 : 0;   // conv_in_kernel: one part per 256 px
   if (ks == 3 && mode == MODE_S1 && wino_dispatchable(a, B)) return wino_gn_parts(a, B);
   if (wino4s_up_dispatchable(ks, mode, act, a, B)) return (a.Wo / 4) * (a.Wo / 4) / 16;
   return 0;

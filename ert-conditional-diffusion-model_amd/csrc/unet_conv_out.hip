@@ -400,11 +400,11 @@ hipError_t launch_co_w(const ConvArgs& a, int B, hipStream_t s) {
 // ---- one-INPUT-channel 3x3 convolution (conv_in: x (B,1,H,W) -> (B,Cout,H,W)) ----
 // The MFMA kernels pad Cin = 1 to a whole K chunk (4 / 16 channels): 31.9 us
 // per U2 B=64 step at 6 % of the fp32 peak for a layer whose floor is its
-// output write (67 MB).  Here a thread owns one output pixel: its 9 taps in
-// registers (zero padding), the weights of all output channels in LDS
-// (broadcast reads), one fp32 fma chain of 9 taps per channel in (ky, kx)
-// order, and a coalesced store per channel (consecutive threads =
-// consecutive pixels).  bf16: the input tap is rounded to bf16 (RNE) and the
+// output write (67 MB).  Here a thread owns four consecutive output pixels:
+// their 3 x 6 input window in registers (zero padding), the weights of the
+// workgroup's 64 output channels in LDS (broadcast reads), one fp32 fma chain
+// of 9 taps per pixel and channel in (ky, kx) order, and a float4 store per
+// channel (consecutive lanes = consecutive pixels).  bf16: the input tap is rounded to bf16 (RNE) and the
 // weights come from the bf16 packing, so the products equal the bf16 MFMA's.
 // W[co][0][tap] in the fp32 packing (ks 3: 4-channel chunks, [tile][chunk][9 step pairs][lane][2])
 __device__ __forceinline__ float packed_w0_f32(const float* w, int co, int tap) {
@@ -420,51 +420,101 @@ __device__ __forceinline__ float packed_w0_bf16(const float* w, int co, int tap,
   return hi + lo;
 }
 
+// wave sum, the same value in every lane: row16_sum, then the rows as (r0 + r1) + (r2 + r3)
+__device__ __forceinline__ float wave_sum_rl(float v) {
+  v = row16_sum(v);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
+// A workgroup = one 256-pixel part (the GroupNorm partial's unit) x 64 output
+// channels, 16 per wave; lane l owns pixels 4l .. 4l+3 of the part (one row
+// segment: WO % 4 == 0), so each channel is one float4 store per lane.  With
+// a.gnp the wave also emits the channel's partial {sum, M2 about the part
+// mean} (DPP / readlane wave sums), and the walk needs no partials pass over
+// the output.
 template <int WO, int PK>
 __global__ __launch_bounds__(256) void conv_in_kernel(ConvArgs a) {
   constexpr bool BF = PK == PK_BF16;
-  extern __shared__ __attribute__((aligned(16))) float smi[];
-  float* wl = smi;                    // [Cout][9]
-  float* bl = smi + a.Cout * 9;       // [Cout]
-  const int tid = threadIdx.x, b = blockIdx.y;
+  constexpr int HW = WO * WO, NP = HW / 256;
+  static_assert(HW % 256 == 0 && WO % 4 == 0, "whole 256-pixel parts of whole float4s");
+  __shared__ float wl[64 * 9];        // [channel of the workgroup][tap]
+  __shared__ float bl[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.y, part = blockIdx.x, cg = blockIdx.z * 64;
   const int Cout = a.Cout;
-  for (int i = tid; i < Cout * 9; i += 256) {
-    const int co = i / 9, tap = i - co * 9;
-    wl[i] = PK == PK_F32 ? packed_w0_f32(a.wpk, co, tap) : packed_w0_bf16(a.wpk, co, tap, PK == PK_SPLIT);
+  for (int i = tid; i < 64 * 9; i += 256) {
+    const int co = cg + i / 9, tap = i - (i / 9) * 9;
+    wl[i] = co >= Cout ? 0.f
+            : PK == PK_F32 ? packed_w0_f32(a.wpk, co, tap) : packed_w0_bf16(a.wpk, co, tap, PK == PK_SPLIT);
   }
-  for (int i = tid; i < Cout; i += 256) bl[i] = a.bias ? a.bias[i] : 0.f;
-  if (a.zero_words && blockIdx.x == 0 && blockIdx.y == 0)   // the walk's GroupNorm-fold counters
+  if (tid < 64) bl[tid] = (a.bias && cg + tid < Cout) ? a.bias[cg + tid] : 0.f;
+  if (a.zero_words && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)   // the walk's GroupNorm-fold counters
     for (int i = tid; i < a.zero_n; i += 256) a.zero_words[i] = 0u;
-  constexpr int HW = WO * WO;
-  const int p = blockIdx.x * 256 + tid;
-  const int y = p / WO, x = p - y * WO;
+  const int p = part * 256 + 4 * lane;
+  const int y = p / WO, x0 = p - y * WO;
   const float* src = a.srcA + (size_t)b * HW;
-  float v[9];
+  float v[3][6];      // rows y-1 .. y+1, columns x0-1 .. x0+4
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int iy = y - 1 + ky, ix = x - 1 + kx;
+    for (int j = 0; j < 6; ++j) {
+      const int iy = y - 1 + ky, ix = x0 - 1 + j;
       float t = (iy >= 0 && iy < WO && ix >= 0 && ix < WO) ? src[iy * WO + ix] : 0.f;
       if constexpr (BF) t = round_bf16(t);
-      v[ky * 3 + kx] = t;
+      v[ky][j] = t;
     }
   __syncthreads();
   float* out = a.out + (size_t)b * Cout * HW + p;
-  for (int co = 0; co < Cout; ++co) {
-    const float* wp = wl + co * 9;
-    float acc = 0.f;
+  const int c0 = cg + wave * 16;
+  const int nc = Cout - c0 < 16 ? Cout - c0 : 16;   // this wave's channels (wave-uniform)
+  if (nc <= 0) return;
+  float r[16][4];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) acc = fmaf(wp[tap], v[tap], acc);
-    out[(size_t)co * HW] = acc + bl[co];
+  for (int k = 0; k < 16; ++k) {
+    if (k < nc) {
+      const float* wp = wl + (wave * 16 + k) * 9;
+      float w[9];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) w[tap] = wp[tap];
+      const float bk = bl[wave * 16 + k];
+#pragma unroll
+      for (int px = 0; px < 4; ++px) {
+        float acc = 0.f;   // one fma chain of the 9 taps in (ky, kx) order, then the bias
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) acc = fmaf(w[tap], v[tap / 3][tap % 3 + px], acc);
+        r[k][px] = acc + bk;
+      }
+      *reinterpret_cast<float4*>(out + (size_t)(c0 + k) * HW) = make_float4(r[k][0], r[k][1], r[k][2], r[k][3]);
+    }
   }
+  if (!a.gnp) return;
+  // per channel: wave sums by DPP row sums + the four rows' readlanes (VALU
+  // only, no LDS round trips), {sum, M2 about the part mean}; lane k keeps
+  // channel k's pair for one coalesced store
+  float s_ = 0.f, q_ = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k < nc) {
+      const float sm = wave_sum_rl((r[k][0] + r[k][1]) + (r[k][2] + r[k][3]));
+      const float mu = sm * (1.0f / 256.0f);
+      const float dx = r[k][0] - mu, dy = r[k][1] - mu, dz = r[k][2] - mu, dw = r[k][3] - mu;
+      const float m2 = wave_sum_rl(fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, dw * dw))));
+      if (lane == k) { s_ = sm; q_ = m2; }
+    }
+  }
+  if (lane < nc) a.gnp[((size_t)b * Cout + c0 + lane) * NP + part] = make_float2(s_, q_);
 }
 
+// (measured: the same kernel looping over items with the next window prefetched,
+// 1 / 2 / 4 workgroups per CU, ran 30.4 / 24.4 / 24.5 us against 24.4)
 template <int WO, int BF>
 hipError_t launch_ci(const ConvArgs& a, int B, hipStream_t s) {
-  const size_t lds = (size_t)a.Cout * 10 * sizeof(float);
-  if (lds > 65536) return hipErrorInvalidValue;
-  conv_in_kernel<WO, BF><<<dim3((unsigned)(WO * WO / 256), (unsigned)B), 256, lds, s>>>(a);
+  if (a.Cout < 1 || a.Cout > 1024) return hipErrorInvalidValue;
+  conv_in_kernel<WO, BF><<<dim3((unsigned)(WO * WO / 256), (unsigned)B, (unsigned)((a.Cout + 63) / 64)), 256, 0, s>>>(a);
   return hipGetLastError();
 }
 

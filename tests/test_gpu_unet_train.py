@@ -614,6 +614,8 @@ def test_unet_train_step_u5_runs(cuda_dev):
     (128, 64, 128, 32, 0, 1, 4),   # concat input
     (128, 0, 128, 16, 2, 0, 4),    # Upsample conv 16 -> 32
     (64, 0, 64, 64, 0, 1, 32),     # the train batch
+    (1, 0, 64, 64, 0, 0, 4),       # conv_in (one input channel)
+    (1, 0, 96, 32, 0, 0, 2),       # conv_in, a partial 64-channel group
 ])
 def test_conv2d_gn_parts_finalize(Ca, Cb, Cout, H, mode, act, B, cuda_dev):
     """ertd_conv2d_gn / _run_gn (the train walk's forward convs): the same output

@@ -12,7 +12,7 @@ B=ert-conditional-diffusion-model_amd/build; mkdir -p "$(dirname "$out")" ab/obj
 IFS=',' read -ra SRCS <<< "$src"
 objs=$(ls $B/*.o); new=""
 for s in "${SRCS[@]}"; do
-  objs=$(echo "$objs" | grep -v "/$s.o")
+  objs=$(echo "$objs" | grep -v "/$s\.o$")
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $flags \
     -I include -I ert-conditional-diffusion-model_amd/csrc -c ert-conditional-diffusion-model_amd/csrc/$s.hip \
     -o ab/obj/$s.$$.o
