@@ -132,6 +132,37 @@ __device__ __forceinline__ void wino4s_fold_tail(const GnFold& f, int lane, int 
   }
 }
 
+#ifdef WINO4S_STAMP
+// Diagnostic build only (tools/wino4s_stamps.py): per-wave s_memtime stamps of
+// workgroups 0..255, stored by lane 0 with vector stores.  Per wave (S4_SPW
+// words): [0] s_memrealtime at entry (low 32 bits), [1] s_memtime at entry,
+// [2] barrier (A) passed; MFMA waves: per item il < 8 [3 + 3 il] item start,
+// [4 + 3 il] last chunk barrier passed, [5 + 3 il] epilogue stores issued;
+// [27] exit; [28 + g] chunk g's barrier passed (g < 32, the first item(s));
+// producer waves: [3] prologue staged (before (A)), [27] exit.
+constexpr int S4_SPW = 64;
+__device__ unsigned g_w4s_stamps[256 * 12 * S4_SPW];
+#define W4S_STAMP(slot)                                                                            \
+  do {                                                                                             \
+    if (blockIdx.x < 256 && lane == 0)                                                             \
+      g_w4s_stamps[(blockIdx.x * 12 + wave) * S4_SPW + (slot)] = (unsigned)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define W4S_STAMP_ENTRY()                                                                          \
+  do {                                                                                             \
+    if (blockIdx.x < 256 && lane == 0) {                                                           \
+      g_w4s_stamps[(blockIdx.x * 12 + wave) * S4_SPW] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
+      g_w4s_stamps[(blockIdx.x * 12 + wave) * S4_SPW + 1] = (unsigned)__builtin_amdgcn_s_memtime(); \
+    }                                                                                              \
+  } while (0)
+#else
+#define W4S_STAMP(slot) \
+  do {                  \
+  } while (0)
+#define W4S_STAMP_ENTRY() \
+  do {                    \
+  } while (0)
+#endif
+
 // item it -> (K half, co group, 16-tile block): the K halves of a (co group,
 // block) adjacent, then co group, then block
 struct Item {
@@ -162,12 +193,20 @@ struct ItemWalk {
 // operand-read and issue stalls; each computes the partial output transform
 // of its rows, the halves are exchanged through LDS across the item's last
 // barrier, and each wave finishes two of the lane's four channels
-template <int WO, int ACT, bool UP, int XS>
+// FOLD (diagnostic builds only, ERTD_UNET_GNFOLD): the GroupNorm fold's
+// write-through partial stores, arrival counts and finalize tail.  The shipped
+// instantiation (FOLD = false) has none of it: no static LDS word in front of
+// the dynamic V buffers, no per-item branches.
+template <int WO, int ACT, bool UP, int XS, bool FOLD>
 __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvArgs a, int nitems, int ksp) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* vbuf = smem;                  // [2][V_FL]
-  __shared__ int fold_items;         // GroupNorm fold: MFMA waves done with the current item
-  if (threadIdx.x == 0) fold_items = 0;
+  int* fold_items = nullptr;           // GroupNorm fold: MFMA waves done with the current item
+  if constexpr (FOLD) {
+    __shared__ int fold_lds;
+    fold_items = &fold_lds;
+    if (threadIdx.x == 0) fold_lds = 0;
+  }
 
   constexpr int TPR = WO / 4;
   constexpr int HW = WO * WO;
@@ -178,6 +217,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  W4S_STAMP_ENTRY();
   const int Cin = a.Cin, Ca = a.Ca;
   // ksp = 2 (XS = 2 only): an item runs half of the input channels, the
   // second half's sums go to a.ksplit_buf (no bias / emb / residual) and are
@@ -403,7 +443,9 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
       act_stage(1, 1);
       load_next(1);      // chunk 4
     }
+    W4S_STAMP(3);
     __syncthreads();   // (A) chunk 0 staged
+    W4S_STAMP(2);
     int g = 0;
     for (; g + 5 < gtot; g += 6) {
       slot(I2{}, I0{}, g);
@@ -418,6 +460,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     if (g + 2 < gtot) slot(I1{}, I0{}, g + 2);
     if (g + 3 < gtot) slot(I2{}, I1{}, g + 3);
     if (g + 4 < gtot) slot(I0{}, I0{}, g + 4);
+    W4S_STAMP(27);
     return;
   }
 
@@ -633,11 +676,11 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float2* d = a.gnp + ((size_t)smpl * a.Cout + co0 + i) * np + part;
-          if (a.fold.cnt) st_f2_wt(d, pr[i]);
+          if constexpr (FOLD) st_f2_wt(d, pr[i]);
           else *d = pr[i];
         }
       }
-      if (a.fold.cnt) gn_fold_item_done(a.fold, smpl, &fold_items, NMW, ln);
+      if constexpr (FOLD) gn_fold_item_done(a.fold, smpl, fold_items, NMW, ln);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -646,7 +689,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
                                                i * HW * 4 + r * WO * 4, 0);
   }
-  if (a.fold.cnt) wino4s_fold_tail(a.fold, lane, wave, NMW);
+  if constexpr (FOLD) wino4s_fold_tail(a.fold, lane, wave, NMW);
   } else {
   // =================== MFMA waves, xi split over two waves ===================
   constexpr int NP = 9;                        // xi pairs per wave
@@ -690,6 +733,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     u_advance();
   }
   __syncthreads();   // (A)
+  W4S_STAMP(2);
   auto chunk2 = [&](const float* vs) {
     constexpr int PD = WINO4S_PD;
     f32x2 rb[PD + 1];
@@ -717,6 +761,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
 #pragma unroll
     for (int x = 0; x < 2 * NP; ++x) acc[x] = f32x4{};
     f32x2 own[4][4];     // this wave's partial Y of its channel pair (pp = xh): [row][col]
+    if (il < 8) W4S_STAMP(3 + 3 * il);
     for (int k = 0; k < nchunk; ++k) {
       const int g = il * nchunk + k;
       int ln;
@@ -770,7 +815,11 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
         }
       }
       __syncthreads();   // (B)
+#ifdef WINO4S_STAMP
+      if (g < 32) W4S_STAMP(28 + g);
+#endif
     }
+    if (il < 8) W4S_STAMP(4 + 3 * il);
     // ---- finish this wave's channel pair: own partial + the partner's
     int ln;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
@@ -852,11 +901,11 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           float2* d = a.gnp + ((size_t)smpl * a.Cout + co0 + i) * np + part;
-          if (a.fold.cnt) st_f2_wt(d, pr[i]);
+          if constexpr (FOLD) st_f2_wt(d, pr[i]);
           else *d = pr[i];
         }
       }
-      if (a.fold.cnt) gn_fold_item_done(a.fold, smpl, &fold_items, 4 * XS, ln);
+      if constexpr (FOLD) gn_fold_item_done(a.fold, smpl, fold_items, 4 * XS, ln);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -864,8 +913,10 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
       for (int r = 0; r < 4; ++r)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y[i][r]), ro, vo,
                                                i * HW * 4 + r * WO * 4, 0);
+    if (il < 8) W4S_STAMP(5 + 3 * il);
   }
-  if (a.fold.cnt) wino4s_fold_tail(a.fold, lane, wave, 4 * XS);
+  W4S_STAMP(27);
+  if constexpr (FOLD) wino4s_fold_tail(a.fold, lane, wave, 4 * XS);
   }
 
 }
@@ -882,6 +933,18 @@ static int wino4s_xs() {
 }
 
 }  // namespace
+
+#ifdef WINO4S_STAMP
+extern "C" int ertd_diag_wino4s_stamps(unsigned* host, size_t n) {
+  const size_t cap = sizeof(g_w4s_stamps) / sizeof(unsigned);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4s_stamps), (n < cap ? n : cap) * sizeof(unsigned), 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int ertd_diag_wino4s_stamps_clear() {
+  static unsigned zero[256 * 12 * S4_SPW];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_w4s_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 // ERTD_WINO4S_KSPLIT=0: no K split (a 16x16 layer whose items fill only half
 // the CUs then runs F(2x2), as before)
@@ -907,11 +970,22 @@ namespace {
 template <int WO, int ACT, bool UP, int XS>
 hipError_t launch_wo4x(const ConvArgs& a, int B, hipStream_t s, int cus, int ksp) {
   constexpr size_t lds = WLDS + (XS == 2 ? (size_t)4 * 2 * 8 * 256 * sizeof(float) : 0);
-  static std::atomic<unsigned long long> attr{0};
-  set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS>, (int)lds, attr);
   const int nitems = wino4s_items(a.Cout, WO, B) * ksp;
   const int grid = nitems < cus ? nitems : cus;
-  conv_wino4s_kernel<WO, ACT, UP, XS><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp);
+#ifdef ERTD_DIAG
+  if (a.fold.cnt) {
+    static std::atomic<unsigned long long> attr{0};
+    set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS, true>, (int)lds, attr);
+    conv_wino4s_kernel<WO, ACT, UP, XS, true><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp);
+  } else
+#else
+  if (a.fold.cnt) return hipErrorInvalidValue;   // the fold is built into diagnostic libraries only
+#endif
+  {
+    static std::atomic<unsigned long long> attr{0};
+    set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS, false>, (int)lds, attr);
+    conv_wino4s_kernel<WO, ACT, UP, XS, false><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ksp == 1) return e;
   return launch_add_inplace(a.out, a.ksplit_buf, (size_t)B * a.Cout * WO * WO, s);

@@ -196,6 +196,12 @@ class TrainPlan:
         P = model.param_dim
         self.lr, self.b1, self.b2, self.eps = _adam_hparams(optimizer, self.params)
         self.alpha_bar = _lib.f32c(alpha_bar, "alpha_bar")
+        # the head kernel draws t in [0, T) and reads alpha_bar[t] on the device:
+        # a shorter schedule would read past its end (the reference's
+        # alpha_bar[t] raises IndexError instead, :96-99)
+        if self.alpha_bar.dim() != 1 or self.alpha_bar.numel() < self.T:
+            raise IndexError(f"ertdiff: alpha_bar has {self.alpha_bar.numel()} entries, "
+                             f"TrainPlan needs at least T = {self.T}")
         z = dict(dtype=torch.float32, device=dev)
         self.x0 = torch.zeros(B, P, **z)
         self.cond = torch.zeros(B, _lib.CIN, L, **z)
@@ -215,10 +221,11 @@ class TrainPlan:
         self._graphs = {}
         self._table_at(int(self._steps[0].item()))
         # warm-up outside any capture (module load, lazily created state): the
-        # forward + backward on the zero inputs -- parameters, Adam state and the
-        # generator are untouched
+        # forward + backward on the zero inputs, into scratch gradient buffers --
+        # parameters, p.grad, Adam state and the generator are untouched
         w = model.weights_struct()
         scratch = torch.empty((), **z)
+        scratch_grads = [torch.empty_like(p) for p in self.params]
         with torch.cuda.device(dev):
             for _ in range(max(1, int(warmup))):
                 _lib.check(_lib.lib().ertd_train_forward(
@@ -228,9 +235,10 @@ class TrainPlan:
                     _lib.stream_of(dev)), "train_forward")
                 _lib.check(_lib.lib().ertd_train_backward(
                     ctypes.byref(w), None, None, self.noise.data_ptr(), self.cond.data_ptr(), B, L,
-                    _lib.ptr_array(self.grads), scratch.data_ptr(), None, self.ws.data_ptr(),
+                    _lib.ptr_array(scratch_grads), scratch.data_ptr(), None, self.ws.data_ptr(),
                     self.ws.numel(), _lib.stream_of(dev)), "train_backward")
             torch.cuda.synchronize(dev)
+        del scratch_grads
 
     def _table_at(self, step0: int):
         """Adam scalars of steps step0+1 ... step0+TABLE; drops captured graphs
@@ -273,7 +281,13 @@ class TrainPlan:
 
     def _sync_step(self):
         """Follow Adam steps taken outside the plan (eager train_step, a
-        user's optimizer.step()): the step counters are host tensors."""
+        user's optimizer.step()) -- the step counters are host tensors -- and
+        edits of the optimizer's lr / betas / eps (a scheduler): the table of
+        Adam scalars is rebuilt from the current hyper-parameters."""
+        hp = _adam_hparams(self.optimizer, self.params)
+        if hp != (self.lr, self.b1, self.b2, self.eps):
+            self.lr, self.b1, self.b2, self.eps = hp
+            self._table_at(self.host_step)
         st = self._steps[0]
         if st.device.type != "cpu":
             return
@@ -299,6 +313,7 @@ class TrainPlan:
             if p.grad is not gr:
                 p.grad = gr
         self.model._packed_key = None  # parameters changed in place: re-pack for sampling
+        increment_version(self.params)  # ... and say so to autograd, as train_step does
 
     @torch.no_grad()
     def step(self, x0=None, cond=None, *, t=None, noise=None, return_tensor: bool = False):
@@ -314,7 +329,13 @@ class TrainPlan:
             raise RuntimeError("ertdiff: TrainPlan.step takes both t and noise, or neither")
         draw = t is None
         if not draw:
-            self.t.copy_(t.to(torch.int64))
+            if tuple(t.shape) != (self.B,) or tuple(noise.shape) != tuple(self.noise.shape):
+                raise RuntimeError(f"ertdiff: TrainPlan.step takes t of shape ({self.B},) and noise of "
+                                   f"shape {tuple(self.noise.shape)}")
+            tl = t.to(torch.int64)
+            if tl.numel() and (int(tl.min()) < 0 or int(tl.max()) >= self.alpha_bar.numel()):
+                raise IndexError(f"ertdiff: t out of range [0, {self.alpha_bar.numel()})")
+            self.t.copy_(tl)
             self.noise.copy_(noise)
         self._replay(draw)
         return self.loss.clone() if return_tensor else self.loss.item()

@@ -257,7 +257,11 @@ int ertd_train_step(const ertd_weights* w, float* packed, const float* x0, const
  * the step advances the device counter *step_dev (int32; the count of Adam
  * steps applied, as torch's state["step"]) and the update of step s uses the
  * 6-float entry adam_table[s - table_first] (device copy of ertd_adam_table's
- * output); s must lie in [table_first, table_first + table_len).
+ * output); s must lie in [table_first, table_first + table_len).  The device
+ * cannot report a step outside the table: it CLAMPS s to the nearest entry
+ * (wrong bias corrections, no error), so the caller re-builds the table before
+ * it runs out (ertdiff.TrainPlan does).  With draw = 1, alpha_bar must hold at
+ * least T entries (t is drawn in [0, T) and alpha_bar[t] read on the device).
  * draw = 0: t (B) / noise (B,P) are inputs.  draw = 1: the step draws them
  * itself into the same buffers (t ~ U{0..T-1}, noise ~ N(0,1), Philox4x32-10
  * keyed by (seed, member, step s): reproducible, independent of the grid).  */
