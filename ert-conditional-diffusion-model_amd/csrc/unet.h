@@ -95,6 +95,10 @@ struct ConvArgs {
                          // (fold.cnt null: none; conv_gn_fold_ok says where it is taken)
   unsigned* zero_words;  // conv_in: zero these zero_n words (the fold counters of the walk)
   int zero_n;
+  GnPartArgs gnc;        // fp32 Winograd F(4x4) consumers (gnc.pa non-null): the input's
+                         // GroupNorm finalize in the conv's own prologue (conv_gn_consume_ok):
+                         // the {scale, shift} of the sample the workgroup runs are merged from
+                         // these partials into LDS -- no finalize launch, gn unused
 };
 
 // GroupNorm statistics without a second read of the activation: the fp32
@@ -119,6 +123,10 @@ int wino_gn_parts(const ConvArgs& a, int B);
 bool conv_gn_fold_ok(int ks, int mode, int act, const ConvArgs& a, int B);
 // its MFMA-wave arrivals per sample (GnFold::target)
 int conv_gn_fold_target(const ConvArgs& a, int B);
+// true where the kernel launch_conv would dispatch (fp32) takes ConvArgs::gnc:
+// the Winograd F(4x4) register-weight kernel without a K split whose items
+// divide evenly over its workgroups with each workgroup's items in one sample
+bool conv_gn_consume_ok(int ks, int mode, int act, const ConvArgs& a, int B);
 
 // sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), the same bits in
 // every lane of the row (fixed pairing: quad swaps, then the half-row and row
@@ -144,84 +152,188 @@ __device__ __forceinline__ float2 ld_f2_wt(const float2* p) {
   return make_float2(__uint_as_float(__hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                      __uint_as_float(__hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
 }
-// running {count, mean, M2} in float64; chan_add merges a part (Chan et al.)
+// GroupNorm statistics of one group from its parts' {sum, M2 about the part
+// mean}, in float64 and a fixed order -- two passes over the parts:
+//   S = sum_k sum_k,  mean = S / N,  M2 = sum_k (M2_k + n_k (sum_k / n_k - mean)^2)
+// (N = cpg * HW pixels; n_k = HW / np pixels per part, 256 for every producer
+// here, so sum_k / n_k is exact).  GN_LPG lanes per group: lane sub takes the
+// parts k = sub + GN_LPG i (channel-major, A then B) in ascending i, and the
+// lanes' totals meet in an xor butterfly (a + b == b + a, so every lane ends
+// with the same bits).  gn_finalize_kernel, the consumer-side finalize of the
+// F(4x4) conv (gn_group_finalize_regs) and the diagnostic fold all run this
+// arithmetic, so a group's {scale, shift} has the same bits whichever runs it.
+// (Rounds 3-5 merged the parts with Chan's pairwise update: a float64
+// division per part and per butterfly level.)
 #ifndef FOLD_BATCH
-#define FOLD_BATCH 4   // parts loaded per round trip and lane (registers: the producer's epilogue)
+#define FOLD_BATCH 4   // parts loaded per round trip and lane
 #endif
-struct ChanAcc {
-  double n, mean, m2;
+constexpr int GN_LPG = 16;
+struct GnGroupGeom {
+  int c0, itemsA, items;          // first channel, parts of tensor A, all parts (0: dead lane group)
+  const float2* pa;               // (b, c0) of A
+  const float2* pb;               // (b, c0 + nA - Ca) of B
 };
-__device__ __forceinline__ void chan_add(ChanAcc& a, double nb, double meanb, double m2b) {
-  const double n = a.n + nb;
-  const double d = meanb - a.mean;
-  const double f = n > 0.0 ? nb / n : 0.0;   // two empty states stay empty
-  a.mean = a.mean + d * f;
-  a.m2 = a.m2 + m2b + d * d * a.n * f;
-  a.n = n;
+__device__ __forceinline__ GnGroupGeom gn_group_geom(const GnPartArgs& g, int b, int gi, bool live) {
+  const int cpg = (g.Ca + g.Cb) / g.groups;
+  GnGroupGeom q{};
+  if (!live) return q;
+  q.c0 = gi * cpg;
+  const int nA = q.c0 < g.Ca ? (g.Ca - q.c0 < cpg ? g.Ca - q.c0 : cpg) : 0;
+  q.itemsA = nA * g.npa;
+  q.items = q.itemsA + (cpg - nA) * (g.Cb > 0 ? g.npb : 0);
+  q.pa = g.pa + ((size_t)b * g.Ca + q.c0) * g.npa;
+  q.pb = g.Cb > 0 ? g.pb + ((size_t)b * g.Cb + (q.c0 + nA - g.Ca)) * g.npb : nullptr;
+  return q;
+}
+// sum over the 16 lanes of a DPP row in float64, the same bits in every lane
+// (row16_sum's pairing: quad swaps, then the half-row and row mirrors; each
+// level adds a lane's value and its partner's, and a + b == b + a)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double gn_lpg_sum(double v) {
+  static_assert(GN_LPG == 16, "one DPP row per group");
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x140>(v);
+  return v;
+}
+// pass-2 term of part k: its M2 plus its mean's deviation, weighted by its
+// count n (inv_n = 1 / n: exact for the 256-pixel parts)
+__device__ __forceinline__ double gn_part_q(float2 v, double n, double inv_n, double mean) {
+  const double d = (double)v.x * inv_n - mean;
+  return (double)v.y + n * (d * d);
+}
+// {mean, rstd} of the group from the lanes' S and Q totals
+__device__ __forceinline__ float2 gn_mean_rstd(double mean, double Q, double N) {
+  double var = Q / N;
+  var = var > 0.0 ? var : 0.0;
+  return make_float2((float)mean, (float)(1.0 / sqrt(var + GN_EPS)));
+}
+template <bool WT>
+__device__ __forceinline__ float2 gn_ld_part(const GnGroupGeom& q, int k) {
+  return k < q.itemsA ? (WT ? ld_f2_wt(q.pa + k) : q.pa[k]) : q.pb[k - q.itemsA];
 }
 // Groups [part * ceil(G / nparts), ...) of sample b finalized by the calling
-// wave -- the one GroupNorm finalize of the fp32 U-Net, run by
-// gn_finalize_kernel and by the producing convs' fold alike, so a group's
-// {scale, shift} has the same bits whichever runs it: GN_LPG lanes per group,
-// each streaming the group's parts k = sub, sub + GN_LPG, ... (channel-major,
-// A then B) through chan_add, then the lanes' states merged in a fixed
-// butterfly (the lower lane's state first, so every lane holds the same bits).
-// WT: the A partials were written in this launch (write-through loads).
-constexpr int GN_LPG = 16;
+// wave, parts streamed FOLD_BATCH per lane and round trip (the second pass
+// re-reads them: L2-hot).  WT: the A partials were written in this launch
+// (write-through loads).  orow: where {scale, shift} of sample b's channels go
+// (null: g.out + b * C).
 template <bool WT>
 __device__ __forceinline__ void gn_group_finalize(const GnPartArgs& g, int b, int lane, int part,
-                                                  int nparts) {
+                                                  int nparts, float2* orow = nullptr) {
   const int G = g.groups, C = g.Ca + g.Cb, cpg = C / G;
   const int gper = (G + nparts - 1) / nparts, gfirst = part * gper;
   const int gcnt = G - gfirst < gper ? G - gfirst : gper;
   if (gcnt <= 0) return;
   constexpr int LPG = GN_LPG;
   const double na = (double)(g.HW / g.npa), nb = g.Cb > 0 ? (double)(g.HW / g.npb) : 1.0;
+  const double ina = 1.0 / na, inb = 1.0 / nb;
+  const double N = (double)cpg * (double)g.HW;
   for (int gbase = 0; gbase < gcnt; gbase += 64 / LPG) {
     const int gl = gbase + lane / LPG, sub = lane % LPG;
     const bool live = gl < gcnt;
     const int gi = gfirst + gl;
-    const int c0 = live ? gi * cpg : 0;
-    const int nA = !live ? 0 : (c0 < g.Ca ? (g.Ca - c0 < cpg ? g.Ca - c0 : cpg) : 0);
-    const int itemsA = nA * g.npa, items = !live ? 0 : itemsA + (cpg - nA) * (g.Cb > 0 ? g.npb : 0);
-    const float2* pa = g.pa + ((size_t)b * g.Ca + c0) * g.npa;
-    const float2* pb = g.Cb > 0 && live ? g.pb + ((size_t)b * g.Cb + (c0 + nA - g.Ca)) * g.npb : nullptr;
-    ChanAcc acc{0.0, 0.0, 0.0};
-    for (int k0 = sub; k0 < items; k0 += FOLD_BATCH * LPG) {
+    const GnGroupGeom q = gn_group_geom(g, b, gi, live);
+    double S = 0.0;
+    for (int k0 = sub; k0 < q.items; k0 += FOLD_BATCH * LPG) {
       float2 v[FOLD_BATCH];
 #pragma unroll
       for (int j = 0; j < FOLD_BATCH; ++j) {
         const int k = k0 + j * LPG;
-        v[j] = k >= items ? make_float2(0.f, 0.f) : (k < itemsA ? (WT ? ld_f2_wt(pa + k) : pa[k]) : pb[k - itemsA]);
+        v[j] = k < q.items ? gn_ld_part<WT>(q, k) : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < FOLD_BATCH; ++j)
+        if (k0 + j * LPG < q.items) S += (double)v[j].x;
+    }
+    S = gn_lpg_sum(S);
+    const double mean = S / N;
+    double Q = 0.0;
+    for (int k0 = sub; k0 < q.items; k0 += FOLD_BATCH * LPG) {
+      float2 v[FOLD_BATCH];
+#pragma unroll
+      for (int j = 0; j < FOLD_BATCH; ++j) {
+        const int k = k0 + j * LPG;
+        v[j] = k < q.items ? gn_ld_part<WT>(q, k) : make_float2(0.f, 0.f);
       }
 #pragma unroll
       for (int j = 0; j < FOLD_BATCH; ++j) {
         const int k = k0 + j * LPG;
-        if (k < items) {
-          const double n = k < itemsA ? na : nb;
-          chan_add(acc, n, (double)v[j].x / n, (double)v[j].y);
-        }
+        if (k < q.items) Q += k < q.itemsA ? gn_part_q(v[j], na, ina, mean) : gn_part_q(v[j], nb, inb, mean);
       }
     }
-    for (int m = 1; m < LPG; m <<= 1) {
-      ChanAcc o{__shfl_xor(acc.n, m), __shfl_xor(acc.mean, m), __shfl_xor(acc.m2, m)};
-      const bool lower = (sub & m) == 0;
-      ChanAcc x = lower ? acc : o;
-      const ChanAcc y = lower ? o : acc;
-      chan_add(x, y.n, y.mean, y.m2);
-      acc = x;
-    }
+    Q = gn_lpg_sum(Q);
     if (!live) continue;
-    double var = acc.m2 / acc.n;
-    var = var > 0.0 ? var : 0.0;
-    const float rstd = (float)(1.0 / sqrt(var + GN_EPS));
-    const float mean = (float)acc.mean;
-    if (g.mr && sub == 0) g.mr[(size_t)b * G + gi] = make_float2(mean, rstd);
+    const float2 mr = gn_mean_rstd(mean, Q, N);
+    if (g.mr && sub == 0) g.mr[(size_t)b * G + gi] = mr;
     for (int cl = sub; cl < cpg; cl += LPG) {
-      const int c = c0 + cl;
-      const float scale = rstd * g.gamma[c];
-      const float shift = -scale * mean + g.beta[c];
-      g.out[(size_t)b * C + c] = make_float2(scale, shift);
+      const int c = q.c0 + cl;
+      const float scale = mr.y * g.gamma[c];
+      const float shift = -scale * mr.x + g.beta[c];
+      if (orow) orow[c] = make_float2(scale, shift);
+      else g.out[(size_t)b * C + c] = make_float2(scale, shift);
+    }
+  }
+}
+// The same finalize with every load issued before any arithmetic (one memory
+// latency for all of a wave's groups): the consumer conv's prologue.  Job j of
+// the calling wave (jobs wave, wave + nw, ... < njobs, at most JM) finalizes
+// groups 4 jg .. 4 jg + 3 of sample smp[j] into tab[row[j] * C + c]; the
+// caller guarantees cpg <= GN_LPG and at most KM parts per lane.
+template <int JM, int KM>
+__device__ __forceinline__ void gn_group_finalize_regs(const GnPartArgs& g, const int (&smp)[JM],
+                                                       const int (&jg)[JM], const int (&row)[JM],
+                                                       const bool (&jl)[JM], int lane, float2* tab) {
+  constexpr int LPG = GN_LPG;
+  const int G = g.groups, C = g.Ca + g.Cb, cpg = C / G, sub = lane % LPG;
+  const double na = (double)(g.HW / g.npa), nb = g.Cb > 0 ? (double)(g.HW / g.npb) : 1.0;
+  const double ina = 1.0 / na, inb = 1.0 / nb;
+  const double N = (double)cpg * (double)g.HW;
+  GnGroupGeom q[JM];
+  float2 v[JM][KM];
+  float ga[JM], be[JM];
+  bool live[JM];
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int gi = jg[j] * 4 + lane / LPG;
+    live[j] = jl[j] && gi < G;
+    q[j] = gn_group_geom(g, smp[j], gi, live[j]);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int kk = sub + LPG * k;
+      v[j][k] = kk < q[j].items ? gn_ld_part<false>(q[j], kk) : make_float2(0.f, 0.f);
+    }
+    const bool ch = live[j] && sub < cpg;
+    ga[j] = ch ? g.gamma[q[j].c0 + sub] : 0.f;
+    be[j] = ch ? g.beta[q[j].c0 + sub] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    double S = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (sub + LPG * k < q[j].items) S += (double)v[j][k].x;
+    S = gn_lpg_sum(S);
+    const double mean = S / N;
+    double Q = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int kk = sub + LPG * k;
+      if (kk < q[j].items)
+        Q += kk < q[j].itemsA ? gn_part_q(v[j][k], na, ina, mean) : gn_part_q(v[j][k], nb, inb, mean);
+    }
+    Q = gn_lpg_sum(Q);
+    if (live[j] && sub < cpg) {
+      const float2 mr = gn_mean_rstd(mean, Q, N);
+      const float scale = mr.y * ga[j];
+      const float shift = -scale * mr.x + be[j];
+      tab[(size_t)row[j] * C + q[j].c0 + sub] = make_float2(scale, shift);
     }
   }
 }
@@ -289,6 +401,7 @@ bool wino4_ksplit(int cin, int cout, int wo, int B);
 bool wino4s_ok(int cin, int ca, int cout, int wo, int B);
 int wino4s_items(int cout, int wo, int B);
 bool wino4s_fold_ok(const ConvArgs& a, bool up, int B);
+bool wino4s_gnc_ok(const ConvArgs& a, int B);
 int wino4s_fold_target(const ConvArgs& a);
 // the same kernel for the fp32 Upsample conv (MODE_UP, no activation; wo = the
 // OUTPUT width): conv3x3 of the nearest-x2 source through the F(4x4) packing

@@ -308,6 +308,16 @@ struct Walk {
     return v;
   }
 
+  // fp32: a GroupNorm finalize not yet launched -- the next conv either takes
+  // it into its prologue (conv_gn_consume_ok) or launches it first
+  GnPartArgs pend_fin{};
+  bool has_pend_fin = false;
+  void flush_fin() {
+    if (!has_pend_fin) return;
+    has_pend_fin = false;
+    chk(launch_gn_finalize(pend_fin, B, s));
+  }
+
   // fp32: GroupNorm partials per activation tensor (unet.h, GnPartArgs) --
   // emitted by the Winograd convs' epilogues, else computed once by a
   // partials pass (conv_in, Downsample, Upsample outputs) -- so a GroupNorm
@@ -371,7 +381,11 @@ struct Walk {
       if (dry) return;
       GnPartArgs g{ra.p, ra.np, Ca, rb.p, rb.np, Cb, HW, c->groups, P(n + ".weight"), P(n + ".bias"),
                    out, nullptr};
-      chk(launch_gn_finalize(g, B, s));
+      // deferred to the consuming conv: its own prologue finalizes (fp32
+      // Winograd F(4x4) consumers, ConvArgs::gnc), else it launches this first
+      flush_fin();
+      pend_fin = g;
+      has_pend_fin = true;
       return;
     }
     if (dry) return;
@@ -480,6 +494,18 @@ struct Walk {
       a.fold.B = B;
       pfold = PendFold{fold_at[ev], tgt};
     }
+    if (has_pend_fin) {
+      ConvArgs t = a;
+      t.gnc = pend_fin;
+      t.gnc.out = nullptr;
+      t.gn = nullptr;
+      if (act != ACT_NONE && a.gn == pend_fin.out && conv_gn_consume_ok(ks, mode, act, t, B)) {
+        a = t;
+        has_pend_fin = false;
+      } else {
+        flush_fin();
+      }
+    }
     if (has_pend) {
       has_pend = false;
       if (bimg && ks == 3 && mode == MODE_S1 && act == ACT_GN_SILU) {
@@ -575,6 +601,7 @@ struct Walk {
     }
     gn_stats(h, ch, nullptr, 0, Hh * Hh, "norm_out");
     conv("conv_out", 3, MODE_S1, ACT_GN_SILU, h, ch, nullptr, 0, Hh, Hh, nullptr, nullptr, eps);
+    if (!dry) flush_fin();   // (every GroupNorm has its consumer: nothing is pending here)
   }
 
   int max_cin() const {

@@ -524,6 +524,12 @@ bool conv_gn_fold_ok(int ks, int mode, int act, const ConvArgs& a, int B) {
   return false;
 }
 
+bool conv_gn_consume_ok(int ks, int mode, int act, const ConvArgs& a, int B) {
+  if (ks != 3 || mode != MODE_S1 || act == ACT_NONE || a.Cout == 1 || !a.wpk_wino4) return false;
+  if (!wino_dispatchable(a, B) || !wino4s_ok(a.Cin, a.Ca, a.Cout, a.Wo, B)) return false;
+  return wino4s_gnc_ok(a, B);
+}
+
 int conv_gn_fold_target(const ConvArgs& a, int B) {
   (void)B;
   return wino4s_fold_target(a);
@@ -533,6 +539,8 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
   if (a.gnp && conv_gn_parts(ks, mode, act, a, B) == 0) return hipErrorInvalidValue;
   if (a.fold.cnt && (!a.gnp || a.fold.g.pa != a.gnp || !conv_gn_fold_ok(ks, mode, act, a, B)))
+    return hipErrorInvalidValue;
+  if (a.gnc.pa && (a.gnc.Ca + a.gnc.Cb != a.Cin || !conv_gn_consume_ok(ks, mode, act, a, B)))
     return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);
   if (a.Wo != expect) return hipErrorInvalidValue;

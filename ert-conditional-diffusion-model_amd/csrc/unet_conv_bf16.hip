@@ -856,7 +856,7 @@ int conv_bf16_gn_parts(int ks, int mode, int act, const ConvArgs& a, int B) {
 }
 
 hipError_t launch_conv_bf16(int ks, int mode, int act, const ConvArgs& a, int B, hipStream_t s) {
-  if (a.fold.cnt) return hipErrorInvalidValue;   // the fold rides on the fp32 Winograd kernels only
+  if (a.fold.cnt || a.gnc.pa) return hipErrorInvalidValue;   // the fold rides on the fp32 Winograd kernels only
   if (a.Ho != a.Wo || a.Hs != a.Ws || a.Cin != a.Ca + a.Cb) return hipErrorInvalidValue;
   if (a.gnp && (!a.bimg || conv_bf16_gn_parts(ks, mode, act, a, B) == 0)) return hipErrorInvalidValue;
   const int expect = mode == MODE_S2 ? a.Ws / 2 : (mode == MODE_UP ? a.Ws * 2 : a.Ws);

@@ -227,6 +227,10 @@ __global__ __launch_bounds__(1024) void conv_out_kernel(ConvArgs a) {
 #ifndef CO64_PF
 #define CO64_PF 3
 #endif
+#ifndef CO64_PACK
+#define CO64_PACK 1   // packed-fp32 activation pairs and output-row pairs (0: the scalar loop)
+#endif
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 __device__ __forceinline__ float wave_shr1(float v) {   // lane i <- lane i - 1, lane 0 <- 0
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, true));
 }
@@ -257,14 +261,22 @@ __global__ __launch_bounds__(256) void conv_out64_kernel(ConvArgs a) {
     const float* src = c < Ca ? a.srcA + ((size_t)b * Ca + c) * plane : a.srcB + ((size_t)b * a.Cb + (c - Ca)) * plane;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
+      // clamped rows, no branches: the padding rows' values are replaced by
+      // zero after the activation (the conv pads the activated tensor)
       const int iy = y0 - 1 + r;
-      v[r] = (iy >= 0 && iy < W) ? src[iy * W + lane] : 0.f;
+      v[r] = src[(iy < 0 ? 0 : (iy >= W ? W - 1 : iy)) * W + lane];
     }
   };
   float ring[PF + 1][NR];
   float acc[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[j] = 0.f;
+#if CO64_PACK
+  static_assert(R % 2 == 0 && NR % 2 == 0, "row pairs");
+  f32x2 acc2[R / 2];
+#pragma unroll
+  for (int j = 0; j < R / 2; ++j) acc2[j] = f32x2{0.f, 0.f};
+#endif
 #pragma unroll
   for (int q = 0; q < PF; ++q) ldrows(wave + NW * q, ring[q]);
   __syncthreads();   // weights and the GroupNorm table
@@ -286,6 +298,55 @@ __global__ __launch_bounds__(256) void conv_out64_kernel(ConvArgs a) {
       float w[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) w[t] = wp[t];
+#if CO64_PACK
+      // packed fp32 on row pairs (m, m + R/2): output rows j and j + 4 are one
+      // v_pk_fma accumulator pair, and their ky-th input rows j + ky, j + 4 + ky
+      // are the pair P[j + ky] -- rows 0-3 / 4-7 and 8 / 9 are activated as five
+      // aligned pairs A, P[4] = {4, 8} and P[5] = {5, 9} are re-paired from them
+      // (the same fma / mul / add per element as the scalar loop, so the same
+      // bits; exp and rcp have no packed form; per output the taps still run in
+      // (ky, kx) order)
+      static_assert(R == 8, "row pairs (m, m + 4)");
+      f32x2 A[5];
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        f32x2 v = m < 4 ? f32x2{ring[q][m], ring[q][m + 4]} : f32x2{ring[q][8], ring[q][9]};
+        if constexpr (ACT != ACT_NONE) {
+          v = __builtin_elementwise_fma(v, f32x2{g0, g0}, f32x2{g1, g1});
+          if constexpr (ACT == ACT_GN_SILU) {
+            // __expf(-y) = exp2(y * -log2 e): the same v_mul + v_exp as the scalar code
+            f32x2 e = v * f32x2{-1.44269504088896340736f, -1.44269504088896340736f};
+            e = f32x2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)} + f32x2{1.0f, 1.0f};
+            v = v * f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+          }
+        }
+        if constexpr (BF) v = f32x2{round_bf16(v.x), round_bf16(v.y)};
+        A[m] = v;
+      }
+      if (y0 == 0) A[0].x = 0.f;                           // the padding rows (after the activation)
+      if (y0 + R == W) A[4].y = 0.f;
+      f32x2 P[6], PL[6], PR[6];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) P[m] = A[m];
+      P[4] = f32x2{A[0].y, A[4].x};
+      P[5] = f32x2{A[1].y, A[4].y};
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        PL[m] = f32x2{wave_shr1(P[m].x), wave_shr1(P[m].y)};
+        PR[m] = f32x2{wave_shl1(P[m].x), wave_shl1(P[m].y)};
+      }
+#pragma unroll
+      for (int j = 0; j < R / 2; ++j) {
+        f32x2 s2 = acc2[j];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          s2 = __builtin_elementwise_fma(f32x2{w[ky * 3], w[ky * 3]}, PL[j + ky], s2);
+          s2 = __builtin_elementwise_fma(f32x2{w[ky * 3 + 1], w[ky * 3 + 1]}, P[j + ky], s2);
+          s2 = __builtin_elementwise_fma(f32x2{w[ky * 3 + 2], w[ky * 3 + 2]}, PR[j + ky], s2);
+        }
+        acc2[j] = s2;
+      }
+#else
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const int iy = y0 - 1 + r;
@@ -307,8 +368,13 @@ __global__ __launch_bounds__(256) void conv_out64_kernel(ConvArgs a) {
           }
         }
       }
+#endif
     }
   }
+#if CO64_PACK
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc[j] = j < R / 2 ? acc2[j].x : acc2[j - R / 2].y;
+#endif
 #pragma unroll
   for (int j = 0; j < R; ++j) red[(wave * R + j) * 64 + lane] = acc[j];
   __syncthreads();

@@ -49,6 +49,9 @@ constexpr int VKS = 18 * 128;                 // V floats per k-step: [xi/2 18][
 constexpr int V_FL = 2 * VKS;                 // per chunk (4608 floats = 18 KB)
 constexpr size_t WLDS = (size_t)2 * V_FL * sizeof(float);   // 36 KB
 constexpr int NRS = 3;                        // producer register sets
+constexpr int GNC_JM = 4;                     // consumer-side finalize: jobs per MFMA wave
+constexpr int GNC_KM = 6;                     //   parts per lane and group
+constexpr int GNC_TAB = 4096;                 //   table entries (item x channel): 32 KB of LDS
 #ifndef WINO4S_PPRIO
 #define WINO4S_PPRIO 2
 #endif
@@ -139,7 +142,8 @@ __device__ __forceinline__ void wino4s_fold_tail(const GnFold& f, int lane, int 
 // [2] barrier (A) passed; MFMA waves: per item il < 8 [3 + 3 il] item start,
 // [4 + 3 il] last chunk barrier passed, [5 + 3 il] epilogue stores issued;
 // [27] exit; [28 + g] chunk g's barrier passed (g < 32, the first item(s));
-// producer waves: [3] prologue staged (before (A)), [27] exit.
+// producer waves: [3] prologue staged (before (A)), [27] exit; GNC: [25]
+// table done (MFMA) / first loads issued (producers), [26] barrier (A0) passed.
 constexpr int S4_SPW = 64;
 __device__ unsigned g_w4s_stamps[256 * 12 * S4_SPW];
 #define W4S_STAMP(slot)                                                                            \
@@ -197,8 +201,19 @@ struct ItemWalk {
 // write-through partial stores, arrival counts and finalize tail.  The shipped
 // instantiation (FOLD = false) has none of it: no static LDS word in front of
 // the dynamic V buffers, no per-item branches.
-template <int WO, int ACT, bool UP, int XS, bool FOLD>
-__global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvArgs a, int nitems, int ksp) {
+// GNC: the input's GroupNorm finalize runs in this kernel's prologue
+// (ConvArgs::gnc, conv_gn_consume_ok): before the first chunk the 8 MFMA waves
+// -- idle until the producers stage chunk 0 -- merge the partials of every
+// item's sample into an LDS table of {scale, shift} per (item, channel)
+// (gn_group_finalize_regs: the arithmetic of gn_finalize_kernel, so the same
+// bits, with all loads issued first), while the producers' first input loads
+// are in flight; the producers read the table instead of ConvArgs::gn.  One
+// launch (3.3 us of the step graph, measured) per GroupNorm fewer.
+// cw > 0 (diagnostic A/B only): contiguous walk -- workgroup bid runs items
+// bid * cw .. bid * cw + cw - 1 (nitems == grid * cw); 0: items bid, bid + grid, ...
+template <int WO, int ACT, bool UP, int XS, bool FOLD, bool GNC>
+__global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvArgs a, int nitems, int ksp, int cw) {
+  static_assert(!GNC || (XS == 2 && !UP && ACT != ACT_NONE && !FOLD), "GNC: the xi-split GN+act kernel");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* vbuf = smem;                  // [2][V_FL]
   int* fold_items = nullptr;           // GroupNorm fold: MFMA waves done with the current item
@@ -235,8 +250,10 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   const int G = gridDim.x;
   const int bid = (WINO4S_XCD && G % 8 == 0 && ncog <= 2)
                       ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const ItemWalk wk{bid, G, ncog, ksp};
-  const int nloc = bid < nitems ? (nitems - bid + G - 1) / G : 0;
+  const ItemWalk wk = cw ? ItemWalk{bid * cw, 1, ncog, ksp} : ItemWalk{bid, G, ncog, ksp};
+  const int nloc = cw ? (bid * cw < nitems ? min(cw, nitems - bid * cw) : 0)
+                      : (bid < nitems ? (nitems - bid + G - 1) / G : 0);
+  float2* const gtab = reinterpret_cast<float2*>(smem + 2 * V_FL + 4 * 2 * 8 * 256);   // GNC: [item][Cin]
   const int gtot = nloc * nchunk;
 
   if (wave >= 4 * XS) {
@@ -251,6 +268,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     const unsigned choff = (unsigned)(chb * HWS * 4);
     float2 raw[NRS][6];
     float2 gnv[NRS];
+    int gch[NRS];
     f32x4 pad[NRS];
     int cur_g = 0, cur_k = 0, cur_b = 0, cur_il = 0, cur_k0 = 0;
     unsigned roff[6];   // per window row (UP: per distinct source row, 4)
@@ -282,7 +300,8 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     auto load_next = [&](const int set) {
       const int cg = (cur_k0 + cur_k) * CCH + 2 * q;   // wave-uniform first channel of the pair
       pad[set] = cur_pad;
-      if constexpr (ACT != ACT_NONE) gnv[set] = a.gn[(size_t)cur_b * Cin + cg + chb];
+      if constexpr (GNC) gch[set] = cur_il * Cin + cg + chb;   // the table entry, read at the activation
+      else if constexpr (ACT != ACT_NONE) gnv[set] = a.gn[(size_t)cur_b * Cin + cg + chb];
       const bool inA = cg < Ca;               // Ca even: both channels on one side
       const float* p = inA ? a.srcA + ((size_t)cur_b * Ca + cg) * HWS
                            : a.srcB + ((size_t)cur_b * a.Cb + (cg - Ca)) * HWS;
@@ -325,6 +344,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     f32x2 act2[2][6];
     float actn[2][6];
     auto act_stage = [&](const int set, const int ab) {
+      if constexpr (GNC) gnv[set] = gtab[gch[set]];
       f32x2 m[6];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
@@ -352,6 +372,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
 #else
     float act[2][3][6];
     auto act_stage = [&](const int set, const int ab) {
+      if constexpr (GNC) gnv[set] = gtab[gch[set]];
       float cx[6], cy[6];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
@@ -437,6 +458,13 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
       load_next(0);
       load_next(1);
       load_next(2);
+    }
+    if constexpr (GNC) {
+      W4S_STAMP(25);
+      __syncthreads();   // (A0) the MFMA waves' GroupNorm table is in LDS
+      W4S_STAMP(26);
+    }
+    if (gtot > 0) {
       act_stage(0, 0);
       tr_stage(0, vbuf);
       load_next(0);      // chunk 3
@@ -732,6 +760,26 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     for (int p = 0; p < NP; ++p) u_load(ub[0], p);
     u_advance();
   }
+  if constexpr (GNC) {
+    // job j = item il, groups 4 jg .. 4 jg + 3 (ng4 = ceil(G / 4) jobs per item):
+    // wave w of the 8 takes jobs w, w + 8, ... (conv_gn_consume_ok: <= 4 each)
+    constexpr int JM = GNC_JM;
+    const int ng4 = (a.gnc.groups + 3) / 4;
+    int smp[JM], jg[JM], row[JM];
+    bool jl[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const int job = wave + 4 * XS * j, il = job / ng4;
+      jl[j] = il < nloc;
+      row[j] = jl[j] ? il : 0;
+      jg[j] = job - il * ng4;
+      smp[j] = jl[j] ? wk.at(il).blk * 16 / TS : 0;
+    }
+    gn_group_finalize_regs<JM, GNC_KM>(a.gnc, smp, jg, row, jl, lane, gtab);
+    W4S_STAMP(25);
+    __syncthreads();   // (A0)
+    W4S_STAMP(26);
+  }
   __syncthreads();   // (A)
   W4S_STAMP(2);
   auto chunk2 = [&](const float* vs) {
@@ -965,26 +1013,69 @@ bool wino4s_ksplit(int cin, int cout, int wo, int B) {
   return nchunk % 2 == 0 && nchunk >= 4 && items < cus && 2 * items >= cus;
 }
 
+// contiguous walk (items bid * cw ...), diagnostic builds only:
+// ERTD_WINO4S_CWALK=1 takes it for every xi-split layer that can.  Measured
+// (U2 B=64, same box): 249.4 -> 243.8 steps/s -- the strided walk keeps the
+// concurrently running items in a few samples (16 of 64 at 64x64), the
+// contiguous one spreads them over all 64 at a 1-MB sample stride
+static int wino4s_cwalk_env() {
+  static const int v = [] {
+    return ERTD_KNOB("WINO4S_CWALK", 0);
+  }();
+  return v;
+}
+
+// items per workgroup of the contiguous walk, or 0 where it does not apply:
+// the xi-split kernel (Cin >= 16) without a K split, items an exact multiple of
+// the grid, each workgroup's run inside one sample
+static int wino4s_cw_geom(const ConvArgs& a, int wo, int B, int ksp, int cus) {
+  if (ksp != 1 || wino4s_xs() != 2 || a.Cin < 16 || a.Cout % 64) return 0;
+  const int nitems = wino4s_items(a.Cout, wo, B);
+  const int grid = nitems < cus ? nitems : cus;
+  if (grid < 1 || nitems % grid) return 0;
+  const int cw = nitems / grid;
+  const int per_sample = (wo / 4) * (wo / 4) / 16 * (a.Cout / 64);
+  return per_sample % cw == 0 ? cw : 0;
+}
+
 namespace {
+
+int wino4s_cwalk(const ConvArgs& a, int wo, int B, int ksp, int cus) {
+  if (wino4s_cwalk_env() == 0 || a.fold.cnt) return 0;
+  return wino4s_cw_geom(a, wo, B, ksp, cus);
+}
 
 template <int WO, int ACT, bool UP, int XS>
 hipError_t launch_wo4x(const ConvArgs& a, int B, hipStream_t s, int cus, int ksp) {
   constexpr size_t lds = WLDS + (XS == 2 ? (size_t)4 * 2 * 8 * 256 * sizeof(float) : 0);
   const int nitems = wino4s_items(a.Cout, WO, B) * ksp;
   const int grid = nitems < cus ? nitems : cus;
+  const int cw = wino4s_cwalk(a, WO, B, ksp, cus);
 #ifdef ERTD_DIAG
   if (a.fold.cnt) {
     static std::atomic<unsigned long long> attr{0};
-    set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS, true>, (int)lds, attr);
-    conv_wino4s_kernel<WO, ACT, UP, XS, true><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp);
+    set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS, true, false>, (int)lds, attr);
+    conv_wino4s_kernel<WO, ACT, UP, XS, true, false><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp, cw);
   } else
 #else
   if (a.fold.cnt) return hipErrorInvalidValue;   // the fold is built into diagnostic libraries only
 #endif
+  if constexpr (XS == 2 && !UP && ACT != ACT_NONE) {
+    if (a.gnc.pa) {
+      const int nlocmax = (nitems + grid - 1) / grid;
+      const size_t ldsg = lds + (size_t)(cw ? cw : nlocmax) * a.Cin * sizeof(float2);
+      static std::atomic<unsigned long long> attr{0};
+      set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS, false, true>,
+                       (int)(lds + GNC_TAB * sizeof(float2)), attr);
+      conv_wino4s_kernel<WO, ACT, UP, XS, false, true><<<grid, 64 * (4 * XS + NPW), ldsg, s>>>(a, nitems, ksp, cw);
+      return hipGetLastError();
+    }
+  }
+  if (a.gnc.pa) return hipErrorInvalidValue;
   {
     static std::atomic<unsigned long long> attr{0};
-    set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS, false>, (int)lds, attr);
-    conv_wino4s_kernel<WO, ACT, UP, XS, false><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp);
+    set_max_lds_once((const void*)conv_wino4s_kernel<WO, ACT, UP, XS, false, false>, (int)lds, attr);
+    conv_wino4s_kernel<WO, ACT, UP, XS, false, false><<<grid, 64 * (4 * XS + NPW), lds, s>>>(a, nitems, ksp, cw);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ksp == 1) return e;
@@ -1029,6 +1120,34 @@ bool wino4s_fold_ok(const ConvArgs& a, bool up, int B) {
   return true;
 }
 int wino4s_fold_target(const ConvArgs& a) { return (a.Wo / 4) * (a.Wo / 4) / 16 * (a.Cout / 64); }
+
+// the consumer-side GroupNorm finalize (ConvArgs::gnc): a GN+act layer of the
+// xi-split kernel without a K split (stride-1 only: the Upsample convs take no
+// activation) whose finalize jobs fit the MFMA waves' registers and whose
+// per-item tables fit the LDS; ERTD_UNET_GNC=0 (diagnostic builds) keeps the launches
+bool wino4s_gnc_ok(const ConvArgs& a, int B) {
+  static const int env = [] {
+    return ERTD_KNOB("UNET_GNC", 1);
+  }();
+  const GnPartArgs& g = a.gnc;
+  if (!env || wino4s_xs() != 2 || a.Cin < 16 || a.Cin % CCH || a.Ca % 2 || a.Cout % 64) return false;
+  if (a.Wo != 16 && a.Wo != 32 && a.Wo != 64) return false;
+  if (!g.pa || g.groups < 1 || g.Ca + g.Cb != a.Cin || a.Cin % g.groups || g.npa < 1 ||
+      (g.Cb > 0 && (!g.pb || g.npb < 1)) || g.HW != a.Wo * a.Wo || g.HW % g.npa ||
+      (g.Cb > 0 && g.HW % g.npb))
+    return false;
+  const int cus = device_cu_count();
+  const bool spl = wino4s_ksplit(a.Cin, a.Cout, a.Wo, B) && wino4s_items(a.Cout, a.Wo, B) < cus;
+  if (spl) return false;
+  const int nitems = wino4s_items(a.Cout, a.Wo, B);
+  const int grid = nitems < cus ? nitems : cus;
+  const int nloc = wino4s_cwalk_env() ? wino4s_cw_geom(a, a.Wo, B, 1, cus) : (nitems + grid - 1) / grid;
+  const int cpg = a.Cin / g.groups;
+  const int np = g.npa > g.npb ? g.npa : g.npb;
+  if (env == 2 && nloc > 1) return false;   // (diagnostic: single-item workgroups only)
+  return nloc > 0 && nloc * ((g.groups + 3) / 4) <= 8 * GNC_JM && cpg <= GN_LPG &&
+         cpg * np <= GN_LPG * GNC_KM && nloc * a.Cin <= GNC_TAB;
+}
 
 // ERTD_WINO4S_UP=0 keeps the sub-pixel direct kernel for the Upsample convs (A/B)
 bool wino4s_up_ok(int cin, int ca, int cout, int wo, int B) {

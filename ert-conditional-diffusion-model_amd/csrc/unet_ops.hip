@@ -158,6 +158,10 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(GnPartArgs a, int B) {
   gn_group_finalize<false>(a, b, lane, wv - b * nparts, nparts);
 }
 
+#ifdef GN_FIN_TWICE
+__global__ void gn_fin_nop_kernel() {}
+#endif
+
 hipError_t launch_gn_finalize(const GnPartArgs& a, int B, hipStream_t s) {
   const int C = a.Ca + a.Cb;
   if (!a.pa || a.npa < 1 || a.Ca < 1 || (a.Cb > 0 && (!a.pb || a.npb < 1)) || a.groups < 1 ||
@@ -165,6 +169,13 @@ hipError_t launch_gn_finalize(const GnPartArgs& a, int B, hipStream_t s) {
     return hipErrorInvalidValue;
   const int n = B * ((a.groups + 64 / GN_LPG - 1) / (64 / GN_LPG));   // one wave each
   gn_finalize_kernel<<<(n + 3) / 4, 256, 0, s>>>(a, B);
+#ifdef GN_FIN_TWICE   // diagnostic variants only: the cost of one more launch in the step graph
+#if GN_FIN_TWICE == 1
+  gn_finalize_kernel<<<(n + 3) / 4, 256, 0, s>>>(a, B);
+#else
+  gn_fin_nop_kernel<<<1, 64, 0, s>>>();
+#endif
+#endif
   return hipGetLastError();
 }
 

@@ -7,8 +7,15 @@
 set -eu
 cd "$(dirname "$0")/.."
 src=$1; flags=$2; out=$3
-python3 ert-conditional-diffusion-model_amd/build.py > /dev/null
-B=ert-conditional-diffusion-model_amd/build; mkdir -p "$(dirname "$out")" ab/obj
+# DIAG=1: start from the diagnostic build (build.py --diag: reads the ERTD_* knobs)
+if [ "${DIAG:-0}" = 1 ]; then
+  python3 ert-conditional-diffusion-model_amd/build.py --diag > /dev/null
+  B=ert-conditional-diffusion-model_amd/build/diag; flags="$flags -DERTD_DIAG"
+else
+  python3 ert-conditional-diffusion-model_amd/build.py > /dev/null
+  B=ert-conditional-diffusion-model_amd/build
+fi
+mkdir -p "$(dirname "$out")" ab/obj
 IFS=',' read -ra SRCS <<< "$src"
 objs=$(ls $B/*.o); new=""
 for s in "${SRCS[@]}"; do

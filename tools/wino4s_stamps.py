@@ -33,7 +33,12 @@ def main():
     ap.add_argument("--H", type=int, default=64)
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--res", action="store_true")
+    ap.add_argument("--unet", default=None,
+                    help="stamp the LAST F(4x4) launch of one U-Net forward of this config instead "
+                         "(U2: u0r2.conv2, 64->64 @64, its GroupNorm from the walk)")
     a = ap.parse_args()
+    if a.unet:
+        return unet_stamps(a)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     x = torch.randn(a.B, a.Cin, a.H, a.H, device=dev)
@@ -62,6 +67,33 @@ def main():
     analyze(buf)
 
 
+def unet_stamps(a):
+    import ertdiff
+    dev = torch.device("cuda", 0)
+    torch.set_grad_enabled(False)
+    m = ertdiff.ConditionalUNet.from_config(a.unet, seed=0).to(dev).eval()
+    cond = torch.rand(a.B, 14, 4693, device=dev)
+    x = torch.randn(a.B, m.param_dim, device=dev)
+    t = torch.full((a.B,), 500, dtype=torch.long, device=dev)
+    lib = _lib.lib()
+    lib.ertd_diag_wino4s_stamps.restype = ctypes.c_int
+    lib.ertd_diag_wino4s_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    lib.ertd_diag_wino4s_stamps_clear.restype = ctypes.c_int
+    for _ in range(3):
+        m(x, t, cond)
+    torch.cuda.synchronize()
+    assert lib.ertd_diag_wino4s_stamps_clear() == 0
+    m(x, t, cond)
+    torch.cuda.synchronize()
+    n = 256 * 12 * SPW
+    buf = np.zeros(n, dtype=np.uint32)
+    assert lib.ertd_diag_wino4s_stamps(buf.ctypes.data, n) == 0
+    tag = f"unet_{a.unet}_{a.B}_gnc{os.environ.get('ERTD_UNET_GNC', '1')}"
+    np.save(os.path.join(ROOT, "gpurun_out", f"w4s_stamps_{tag}.npy"), buf)
+    print(f"== {tag} (last F(4x4) launch of the forward)")
+    analyze(buf)
+
+
 def analyze(buf):
     st = buf.reshape(256, 12, SPW).astype(np.int64)
     live = np.nonzero(st[:, 0, 1])[0]
@@ -74,6 +106,9 @@ def analyze(buf):
     med = lambda v: float(np.median(v))
     print(f"MFMA wave 0: entry -> barrier A {med(rel(2)):.0f}; producer wave 8: entry -> staged "
           f"{med(d(st[live, 8, 1], st[live, 8, 3])):.0f}, -> A {med(d(st[live, 8, 1], st[live, 8, 2])):.0f}")
+    if (st[live, 0, 25] != 0).any():
+        print(f"  GNC: MFMA table done {med(rel(25)):.0f}, A0 passed {med(rel(26)):.0f}; producer loads issued "
+              f"{med(d(st[live, 8, 1], st[live, 8, 25])):.0f}, A0 passed {med(d(st[live, 8, 1], st[live, 8, 26])):.0f}")
     items = 0
     for il in range(8):
         s0 = st[live, 0, 3 + 3 * il]
