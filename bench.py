@@ -1106,19 +1106,37 @@ def main():
                             "executed_flop_per_launch": dom["executed_flop"],
                             "timing": "HIP events around 20 launches through ertd_conv2d_run (no packing)",
                             "hbm_gbs": dom["hbm_gbs"], "hbm_frac": dom["hbm_frac"]}
+    # BASELINE configs[2] / configs[4] name bf16; the north star asks for outputs
+    # within 1e-4 rel-L2 of the fp32 reference.  The mode reported under
+    # configs*_bf16 is the bf16-MFMA mode that meets it: split-bf16 operands
+    # (bf16x3: hi + lo planes, three bf16 MFMAs per product; T = 1000 chains
+    # 2.1-2.9e-6 vs the fp32 spec, gated at 1e-4 by
+    # tests/test_gpu_unet.py::test_unet_bf16x3_sampler_full_chain_vs_fp32_golden).
+    # Plain bf16 operands (one MFMA per product) are reported beside it as
+    # *_bf16_plain: faster, but 1.3-1.5e-3 after T = 1000 -- OUTSIDE the 1e-4
+    # tolerance, so not the configs[2]/[4] number.
+    tol = {"north_star_tolerance": "1e-4 rel-L2 vs the fp32 spec after T = 1000",
+           "meets_tolerance": True,
+           "measured_rel_l2_T1000": "2.1-2.9e-6 (profiles/r06_parity_errors.jsonl)"}
+    tol_plain = {"north_star_tolerance": "1e-4 rel-L2 vs the fp32 spec after T = 1000",
+                 "meets_tolerance": False,
+                 "measured_rel_l2_T1000": "1.3-1.5e-3 (profiles/r06_parity_errors.jsonl): single bf16 "
+                                          "operand roundings per conv, not within 1e-4"}
     if not a.no_u3:
-        extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev,
+        extra["configs2_u3_bf16"] = bench_unet_extra("U3", 256, "bf16x3", 20, 3, T, rank, world, dev,
                                                      None if a.no_cpu_baseline else a.cpu_unet_seconds)
-        # split-bf16 operands: the same config inside the north star's 1e-4
-        # (tests/test_gpu_unet.py::test_unet_bf16x3_sampler_full_chain_vs_fp32_golden)
-        extra["configs2_u3_bf16x3"] = bench_unet_extra("U3", 256, "bf16x3", 20, 3, T, rank, world, dev)
+        extra["configs2_u3_bf16"].update(tol)
+        extra["configs2_u3_bf16_plain"] = bench_unet_extra("U3", 256, "bf16", 20, 3, T, rank, world, dev)
+        extra["configs2_u3_bf16_plain"].update(tol_plain)
     if not a.no_ensemble:
         extra["configs3_ensemble"] = bench_ensemble(a.ensemble, "U2", a.ensemble_steps, 2, T, rank,
                                                     world, dev)
     if not a.no_u5:
-        extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev,
+        extra["configs4_u5_bf16"] = bench_unet_extra("U5", 64, "bf16x3", 10, 2, T, rank, world, dev,
                                                      None if a.no_cpu_baseline else a.cpu_unet_seconds)
-        extra["configs4_u5_bf16x3"] = bench_unet_extra("U5", 64, "bf16x3", 10, 2, T, rank, world, dev)
+        extra["configs4_u5_bf16"].update(tol)
+        extra["configs4_u5_bf16_plain"] = bench_unet_extra("U5", 64, "bf16", 10, 2, T, rank, world, dev)
+        extra["configs4_u5_bf16_plain"].update(tol_plain)
     if not a.no_hbm_kernels:
         extra["hbm_kernels"] = bench_hbm_kernels(dev)
     if not a.no_unet_train:

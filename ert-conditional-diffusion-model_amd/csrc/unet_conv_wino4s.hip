@@ -67,6 +67,10 @@ constexpr int GNC_TAB = 4096;                 //   table entries (item x channel
 #ifndef WINO4S_PACK
 #define WINO4S_PACK 1                         // producer stage on packed fp32 pairs
 #endif
+#ifndef WINO4S_RPF
+#define WINO4S_RPF 0                          // residual L2 prefetch this many chunks before the epilogue
+                                              // (0: none; 2: 250.2 vs 252.2 steps/s U2 B=64, same box)
+#endif
 // Ablations for a diagnostic build only (tools/build_variant.sh ... -DWINO4S_ABL=n;
 // results WRONG, never in the shipped library): bit 0 the producers skip the
 // activation and transform, bit 1 every U load reads the first k-step (L2-hot),
@@ -186,6 +190,7 @@ struct ItemWalk {
   int base, stride, ncog, ksp;
   __device__ __forceinline__ Item at(int il) const { return item_of(base + il * stride, ncog, ksp); }
 };
+__device__ __forceinline__ int itm_half(const ItemWalk& w, int il) { return w.at(il).half; }
 
 // UP: the Upsample conv, conv3x3 of the nearest-x2 upsampled source (WO / 2)^2:
 // the window rows 4ty-1 .. 4ty+4 of the upsampled image are source rows 2ty-1,
@@ -810,10 +815,31 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
     for (int x = 0; x < 2 * NP; ++x) acc[x] = f32x4{};
     f32x2 own[4][4];     // this wave's partial Y of its channel pair (pp = xh): [row][col]
     if (il < 8) W4S_STAMP(3 + 3 * il);
+    unsigned rpf[2] = {0u, 0u};   // the residual prefetch's destinations (kept until the epilogue)
     for (int k = 0; k < nchunk; ++k) {
       const int g = il * nchunk + k;
       int ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+#if WINO4S_RPF
+      // the epilogue's residual tile into L2 WINO4S_RPF chunks ahead (its HBM
+      // latency was the epilogue's critical path): one dword per 16-B segment of
+      // tiles 0, 8 / 4, 12 of each (channel, row) -- every 128-B line of the
+      // wave's residual rows at 64x64, 32x32 and 16x16
+      if (k == (nchunk > WINO4S_RPF ? nchunk - WINO4S_RPF : 0) && a.res && itm_half(wk, il) == 0) {
+        const Item pit = wk.at(il);
+        const int pflat = pit.blk * 16, psm = pflat / TS;
+        const int pco = pit.cog * 64 + cb * 16 + 4 * (ln >> 4) + 2 * xh + ((ln >> 3) & 1);
+        const int pr = (ln >> 1) & 3;
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.res) + (size_t)psm * a.Cout * HW, (short)0, (unsigned)(a.Cout * HW * 4), 0x00020000);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ptg = pflat % TS + (ln & 1) * 8 + h * 4;
+          const int pty = ptg / TPR, ptx = ptg - pty * TPR;
+          rpf[h] = __builtin_amdgcn_raw_buffer_load_b32(rp, (pco * HW + (4 * pty + pr) * WO + 4 * ptx) * 4, 0, 0);
+        }
+      }
+#endif
       chunk2(vbuf + (g & 1) * V_FL + ln * 2);
 #pragma unroll
       for (int x = 0; x < 2 * NP; ++x) asm volatile("" : "+v"(acc[x]));
@@ -925,6 +951,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[i][r] = y[i][r] + rv[i][r];
     }
+    asm volatile("" ::"v"(rpf[0]), "v"(rpf[1]));   // (younger than the prefetch: it has landed)
     if (a.gnp && !part2) {
       float2 pr[2];
 #pragma unroll
@@ -1124,10 +1151,14 @@ int wino4s_fold_target(const ConvArgs& a) { return (a.Wo / 4) * (a.Wo / 4) / 16 
 // the consumer-side GroupNorm finalize (ConvArgs::gnc): a GN+act layer of the
 // xi-split kernel without a K split (stride-1 only: the Upsample convs take no
 // activation) whose finalize jobs fit the MFMA waves' registers and whose
-// per-item tables fit the LDS; ERTD_UNET_GNC=0 (diagnostic builds) keeps the launches
+// per-item tables fit the LDS, and whose workgroups run at most two items: the
+// table costs the MFMA waves' prologue 2-4 us at four items per workgroup (the
+// 64x64 layers, U2 B=64), more than the 3.3 us launch it replaces.  Same box,
+// U2 B=64, three alternations: 250.1 steps/s without (ERTD_UNET_GNC=0), 251.9
+// on every eligible layer (1), 252.1 at <= 2 items (3, the default; 2: one item)
 bool wino4s_gnc_ok(const ConvArgs& a, int B) {
   static const int env = [] {
-    return ERTD_KNOB("UNET_GNC", 1);
+    return ERTD_KNOB("UNET_GNC", 3);
   }();
   const GnPartArgs& g = a.gnc;
   if (!env || wino4s_xs() != 2 || a.Cin < 16 || a.Cin % CCH || a.Ca % 2 || a.Cout % 64) return false;
@@ -1145,6 +1176,7 @@ bool wino4s_gnc_ok(const ConvArgs& a, int B) {
   const int cpg = a.Cin / g.groups;
   const int np = g.npa > g.npb ? g.npa : g.npb;
   if (env == 2 && nloc > 1) return false;   // (diagnostic: single-item workgroups only)
+  if (env == 3 && nloc > 2) return false;   // (diagnostic: at most two items per workgroup)
   return nloc > 0 && nloc * ((g.groups + 3) / 4) <= 8 * GNC_JM && cpg <= GN_LPG &&
          cpg * np <= GN_LPG * GNC_KM && nloc * a.Cin <= GNC_TAB;
 }

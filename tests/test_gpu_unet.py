@@ -115,7 +115,12 @@ def test_unet_forward_batch_split_consistency(cuda_dev):
 
 
 SAMPLER_TOL = 1e-4
-# bf16-operand budget at T = 1000 (configs[2]): against the bf16 spec (same
+# PLAIN bf16 operands (precision="bf16": one bf16 MFMA per product) are NOT the
+# mode the bench reports for configs[2] / configs[4] -- that is split-bf16
+# (bf16x3, gated at the north star's 1e-4 below, BF16X3_SAMPLER_TOL).  Plain
+# bf16 is kept as a faster, lower-accuracy mode (bench extra *_bf16_plain,
+# "meets_tolerance": false); these budgets bound its drift, they are not a
+# parity claim.  Budget at T = 1000: against the bf16 spec (same
 # operand rounding, another fp32 summation order: flips of single bf16
 # roundings cascade through ~40 convs per step and 1000 steps) and against the
 # fp32 spec (the price of bf16 operands itself).

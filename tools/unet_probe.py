@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--L", type=int, default=4693)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "bf16x3"])
     a = ap.parse_args()
     torch.set_grad_enabled(False)   # inference forward (not the autograd train-mode path)
     dev = torch.device("cuda", 0)
