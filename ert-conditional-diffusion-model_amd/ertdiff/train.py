@@ -126,6 +126,8 @@ def train_step(model, optimizer, x0, cond, T, alpha_bar, *, t=None, noise=None,
     noise = _lib.f32c(noise, "noise")
     cond = _lib.f32c(cond, "condition")
     ab = _lib.f32c(alpha_bar, "alpha_bar")
+    if ab.dim() != 1 or ab.numel() < int(T):   # the device reads alpha_bar[t], t < T
+        raise IndexError(f"ertdiff: alpha_bar has {ab.numel()} entries, T = {T}")
     tt = t.to(device=dev, dtype=torch.int64).contiguous()
     model._check_inputs(x0, tt, cond)
     lr, b1, b2, eps = _adam_hparams(optimizer, params)
@@ -213,7 +215,16 @@ class TrainPlan:
             if p.grad is None:
                 p.grad = torch.empty_like(p)
         self.grads = [p.grad for p in self.params]
+        # the 12 step counters become views of ONE CPU tensor: a replay bumps them
+        # with one add_ instead of a 12-tensor foreach (host time per step);
+        # torch.optim.Adam reads and bumps state["step"] in place alike
+        self._step_base = torch.tensor([float(optimizer.state[p]["step"]) for p in self.params],
+                                       dtype=torch.float32)
+        for i, p in enumerate(self.params):
+            optimizer.state[p]["step"] = self._step_base[i]
         self._steps = [optimizer.state[p]["step"] for p in self.params]
+        g0 = optimizer.param_groups[0]
+        self._hp_raw = (g0["lr"], g0["betas"], g0["eps"])
         self.ws = torch.empty(max(_lib.lib().ertd_workspace_bytes(B, L, P, 0, _lib.OP_TRAIN), 256),
                               dtype=torch.uint8, device=dev)
         self.freq = timestep_frequencies(_lib.HIDDEN, dev)
@@ -284,10 +295,14 @@ class TrainPlan:
         user's optimizer.step()) -- the step counters are host tensors -- and
         edits of the optimizer's lr / betas / eps (a scheduler): the table of
         Adam scalars is rebuilt from the current hyper-parameters."""
-        hp = _adam_hparams(self.optimizer, self.params)
-        if hp != (self.lr, self.b1, self.b2, self.eps):
-            self.lr, self.b1, self.b2, self.eps = hp
-            self._table_at(self.host_step)
+        g0 = self.optimizer.param_groups[0]
+        raw = (g0["lr"], g0["betas"], g0["eps"])
+        if raw != self._hp_raw:
+            self._hp_raw = raw
+            hp = _adam_hparams(self.optimizer, self.params)
+            if hp != (self.lr, self.b1, self.b2, self.eps):
+                self.lr, self.b1, self.b2, self.eps = hp
+                self._table_at(self.host_step)
         st = self._steps[0]
         if st.device.type != "cpu":
             return
@@ -308,7 +323,7 @@ class TrainPlan:
         with torch.cuda.device(self.dev):
             g.replay()
         self.host_step += 1
-        torch._foreach_add_(self._steps, 1.0)
+        self._step_base.add_(1.0)   # every state["step"] is a view of it
         for p, gr in zip(self.params, self.grads):
             if p.grad is not gr:
                 p.grad = gr

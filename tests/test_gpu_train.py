@@ -249,3 +249,42 @@ def test_train_plan_philox_draws(golden_weights, cuda_dev):
     assert abs(float(z.mean())) < 0.05 and abs(float(z.std()) - 1.0) < 0.05
     tv = torch.cat(tt).double()
     assert abs(float(tv.mean()) - (T - 1) / 2) < 0.06 * T
+
+
+def test_train_plan_input_checks_and_state(golden_weights, cuda_dev):
+    """TrainPlan guards: a schedule shorter than T and an out-of-range
+    or misshapen t raise before anything reaches the device; building a plan
+    leaves p.grad untouched; an lr edited between steps (a scheduler) is
+    followed exactly as the eager step follows it; a replay bumps the
+    parameters' autograd version counters."""
+    B, L, T = 4, 256, 100
+    x0, cond, ts, ns = _train_inputs(B, L, T, 640, cuda_dev)
+    _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
+    m2 = _fresh_model(golden_weights, cuda_dev)
+    o2 = torch.optim.Adam(m2.parameters(), lr=1e-4)
+    with pytest.raises(IndexError):
+        ertdiff.TrainPlan(m2, o2, B, L, T + 1, ab)
+    for p in m2.parameters():
+        p.grad = torch.full_like(p, 3.0)
+    plan = ertdiff.TrainPlan(m2, o2, B, L, T, ab)
+    assert all(bool((p.grad == 3.0).all()) for p in m2.parameters())
+    bad_t = ts[0].clone()
+    bad_t[1] = T
+    with pytest.raises(IndexError):
+        plan.step(x0, cond, t=bad_t, noise=ns[0])
+    with pytest.raises(RuntimeError):
+        plan.step(x0, cond, t=ts[0][:2], noise=ns[0])
+    m1 = _fresh_model(golden_weights, cuda_dev)
+    o1 = torch.optim.Adam(m1.parameters(), lr=1e-4)
+    v0 = [p._version for p in m2.parameters()]
+    for i in range(4):
+        if i == 2:
+            for o in (o1, o2):
+                o.param_groups[0]["lr"] = 3e-4
+        la = ertdiff.train_step(m1, o1, x0, cond, T, ab, t=ts[i], noise=ns[i])
+        lb = plan.step(x0, cond, t=ts[i], noise=ns[i])
+        assert la == lb, i
+    assert all(p._version > v for p, v in zip(m2.parameters(), v0))
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p1, p2), k
+        assert float(o1.state[p1]["step"]) == float(o2.state[p2]["step"]) == 4.0
