@@ -565,4 +565,20 @@ int ertd_train_step_dev(const ertd_weights* w, const float* x0, int64_t* t, floa
                               exp_avg_sq, adam, loss_out, (float*)ws, (hipStream_t)stream));
 }
 
+int ertd_train_steps_dev(const ertd_weights* w, const float* x0, int64_t* t, float* noise,
+                         const float* cond, const float* alpha_bar, int B, int L, const float* freq,
+                         float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                         int* step_dev, const float* adam_table, int table_first, int table_len,
+                         int draw, int T, uint64_t seed, int nsteps, float* loss_out, void* ws,
+                         size_t ws_bytes, void* stream) {
+  if (nsteps < 1 || !draw) return ERTD_EINVAL;
+  for (int i = 0; i < nsteps; ++i) {
+    const int r = ertd_train_step_dev(w, x0, t, noise, cond, alpha_bar, B, L, freq, grads, exp_avg,
+                                      exp_avg_sq, step_dev, adam_table, table_first, table_len, draw,
+                                      T, seed, loss_out, ws, ws_bytes, stream);
+    if (r != ERTD_OK) return r;
+  }
+  return ERTD_OK;
+}
+
 }  // extern "C"

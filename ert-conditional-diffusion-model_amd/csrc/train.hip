@@ -1340,6 +1340,7 @@ hipError_t launch_train_step(const ertd_weights& w, const float* x0, const int64
                              float* ws, hipStream_t s) {
   TrainWs W;
   ws_layout(B, L, true, ws, &W);
+
   const int P = w.param_dim;
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
   const float two_over_n = (float)(2.0 / ((double)B * P));

@@ -90,6 +90,8 @@ SIGNATURES = {
     "ertd_train_conv_backward": (_I, [_VP, _I, _I, _VP, _SZ, _VP]),
     "ertd_train_step_dev": (_I, [_W, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I,
                                  _I, _I, _I, _U64, _VP, _VP, _SZ, _VP]),
+    "ertd_train_steps_dev": (_I, [_W, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I,
+                                  _I, _I, _I, _U64, _I, _VP, _VP, _SZ, _VP]),
     "ertd_postprocess": (_I, [_VP, ctypes.c_longlong, _I, ctypes.c_double, ctypes.c_double, _VP,
                               _VP, _VP, _VP, _VP, _VP]),
     "ertd_conv2d_run": (_I, [_VP, _I, _VP, _I, _I, _I, _VP, _I, _I, _I, _VP, _I, _VP, _I, _VP, _VP, _I,

@@ -265,8 +265,22 @@ class TrainPlan:
         self.host_step = step0
         self._graphs = {}
 
-    def _body(self, draw: bool):
+    def _body(self, draw: bool, k: int = 1):
         dev_draw = draw and self.rng == "philox"
+        if dev_draw and k > 1:   # k steps in ONE call: no gap between them in the graph
+            w = self.model.weights_struct()
+            _lib.check(_lib.lib().ertd_train_steps_dev(
+                ctypes.byref(w), self.x0.data_ptr(), self.t.data_ptr(), self.noise.data_ptr(),
+                self.cond.data_ptr(), self.alpha_bar.data_ptr(), self.B, self.L, self.freq.data_ptr(),
+                _lib.ptr_array(self.grads), _lib.ptr_array(self.exp_avg), _lib.ptr_array(self.exp_avg_sq),
+                self.step_dev.data_ptr(), self.table.data_ptr(), self.table_first, self.TABLE,
+                1, self.T, self.seed, k, self.loss.data_ptr(), self.ws.data_ptr(),
+                self.ws.numel(), _lib.stream_of(self.dev)), "train_steps_dev")
+            return
+        if k > 1:
+            for _ in range(k):
+                self._body(draw)
+            return
         if draw and not dev_draw:
             self.t.random_(0, self.T)   # torch.randint(0, T, (B,)) (:312)
             self.noise.normal_()        # torch.randn_like(x0) (:313)
@@ -279,15 +293,18 @@ class TrainPlan:
             1 if dev_draw else 0, self.T, self.seed, self.loss.data_ptr(), self.ws.data_ptr(),
             self.ws.numel(), _lib.stream_of(self.dev)), "train_step_dev")
 
-    def _graph(self, draw: bool):
-        g = self._graphs.get(draw)
+    def _graph(self, draw: bool, k: int = 1):
+        """The step graph, or k consecutive steps in one graph (run(): the
+        device advances the Adam step count and draws per step, so the k steps
+        of one replay are k ordinary steps)."""
+        g = self._graphs.get((draw, k))
         if g is None:
             with torch.cuda.device(self.dev):
                 torch.cuda.synchronize(self.dev)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                    self._body(draw)
-            self._graphs[draw] = g
+                    self._body(draw, k)
+            self._graphs[(draw, k)] = g
         return g
 
     def _sync_step(self):
@@ -315,15 +332,15 @@ class TrainPlan:
                 self._table_at(s)
 
     @torch.no_grad()
-    def _replay(self, draw: bool):
+    def _replay(self, draw: bool, k: int = 1):
         self._sync_step()
-        if self.host_step + 1 >= self.table_first + self.TABLE:
+        if self.host_step + k >= self.table_first + self.TABLE:
             self._table_at(self.host_step)
-        g = self._graph(draw)
+        g = self._graph(draw, k)
         with torch.cuda.device(self.dev):
             g.replay()
-        self.host_step += 1
-        self._step_base.add_(1.0)   # every state["step"] is a view of it
+        self.host_step += k
+        self._step_base.add_(float(k))   # every state["step"] is a view of it
         for p, gr in zip(self.params, self.grads):
             if p.grad is not gr:
                 p.grad = gr
@@ -355,11 +372,20 @@ class TrainPlan:
         self._replay(draw)
         return self.loss.clone() if return_tensor else self.loss.item()
 
+    RUN_STEPS = 8   # steps per graph replay in run(), launched by ONE C call
+                    # (ertd_train_steps_dev): the ~8 us gap at every call boundary
+                    # of a graph (rocprofv3 trace, B = 32) is paid once per 8 steps
+
     @torch.no_grad()
     def run(self, n: int):
         """n steps on the plan's inputs with fresh draws; no per-step host sync
-        (the loss of the last step stays in plan.loss)."""
-        for _ in range(int(n)):
+        (the loss of the last step stays in plan.loss).  Replays an 8-step graph
+        n // 8 times and the 1-step graph for the rest."""
+        n = int(n)
+        k = self.RUN_STEPS
+        for _ in range(n // k):
+            self._replay(True, k)
+        for _ in range(n % k):
             self._replay(True)
 
 

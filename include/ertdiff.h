@@ -272,6 +272,19 @@ int ertd_train_step_dev(const ertd_weights* w, const float* x0, int64_t* t, floa
                         int draw, int T, uint64_t seed, float* loss_out, void* ws, size_t ws_bytes,
                         void* stream);
 
+/* nsteps consecutive ertd_train_step_dev steps (draw = 1 only: each step draws
+ * its own t / noise from the device step count) in one call.  For graph
+ * capture: a graph holding n steps of ONE call replays them back to back,
+ * where n single-step calls captured one after another leave an ~8 us gap at
+ * every call boundary of the graph (rocprofv3 trace, B = 32 -- measured, cause
+ * in the runtime's graph, not in the kernels).  ertdiff.TrainPlan.run.  */
+int ertd_train_steps_dev(const ertd_weights* w, const float* x0, int64_t* t, float* noise,
+                         const float* cond, const float* alpha_bar, int B, int L, const float* freq,
+                         float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                         int* step_dev, const float* adam_table, int table_first, int table_len,
+                         int draw, int T, uint64_t seed, int nsteps, float* loss_out, void* ws,
+                         size_t ws_bytes, void* stream);
+
 /* The condition encoder's conv backward alone (the Conv1d part of
  * loss.backward(), :317), re-run on the state the last ertd_train_step /
  * ertd_train_step_dev / ertd_train_backward left in ws (same B, L, cond): it
