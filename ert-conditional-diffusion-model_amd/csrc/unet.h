@@ -416,6 +416,9 @@ hipError_t launch_pack_conv_wino(const float* w, int cin, int cout, float* dst, 
 // unet_conv1x1.hip): per-sample GEMM, weights and input by LDS-DMA
 bool conv1x1_ok(const ConvArgs& a, int act, int B);
 hipError_t launch_conv1x1(const ConvArgs& a, int B, hipStream_t s);
+// the 1x1 skip convs as a batched GEMM on 32x32x2 fp32 MFMAs (unet_skip_gemm.hip)
+bool skip_gemm_ok(const ConvArgs& a, int ks, int mode, int act, int B);
+hipError_t launch_skip_gemm(const ConvArgs& a, int B, hipStream_t s);
 // training: the fp32 3x3 stride-1 weight gradient by Winograd F(4x4,3x3)
 // (unet_wgrad_wino.hip); scratch floats it needs (0 = not eligible: Cin, Cout
 // multiples of 64, H in {16, 32, 64}; ERTD_WGRAD_WINO=0 disables)

@@ -564,6 +564,7 @@ hipError_t launch_conv(int ks, int mode, int act, const ConvArgs& a, int B, hipS
       default: return hipErrorInvalidValue;
     }
   }
+  if (skip_gemm_ok(a, ks, mode, act, B)) return launch_skip_gemm(a, B, s);
   if (ks == 1 && mode == MODE_S1 && act == ACT_NONE && conv1x1_ok(a, act, B)) return launch_conv1x1(a, B, s);
   if (ks == 1 && mode == MODE_S1 && act == ACT_NONE) return launch_t<1, MODE_S1, ACT_NONE>(a, B, s);
   if (ks == 1 && mode == MODE_S1 && act == ACT_GN) return launch_t<1, MODE_S1, ACT_GN>(a, B, s);

@@ -195,6 +195,28 @@ def test_conv_input_grad_wino4s_ksplit_accumulate(cuda_dev):
     assert err < 1e-5, err
 
 
+# every 1x1 skip shape of U2 (Ca, Cb, Cout, H): the batched-GEMM kernel
+# (unet_skip_gemm.hip) -- 128 x 128, 128 x 64 and 64 x 256 tiles, concatenated
+# inputs split inside a 32-channel chunk or on its boundary
+SKIP_SHAPES = [(64, 0, 128, 32, 4), (128, 0, 256, 16, 4), (256, 256, 256, 16, 64), (256, 128, 256, 16, 4),
+               (256, 128, 128, 32, 64), (128, 128, 128, 32, 4), (128, 64, 128, 32, 4), (128, 64, 64, 64, 4),
+               (64, 64, 64, 64, 8), (96, 32, 128, 32, 3)]
+
+
+@pytest.mark.parametrize("Ca,Cb,Cout,H,B", SKIP_SHAPES)
+def test_conv2d_skip_gemm_shapes(Ca, Cb, Cout, H, B, cuda_dev):
+    x = _rand((B, Ca, H, H), 70 + Ca)
+    x2 = _rand((B, Cb, H, H), 71 + Cb) if Cb else None
+    w, b = _rand((Cout, Ca + Cb, 1, 1), 72, 1.0 / np.sqrt(Ca + Cb)), _rand((Cout,), 73, 0.1)
+    out = conv2d(x.to(cuda_dev), w.to(cuda_dev), b.to(cuda_dev),
+                 x2=None if x2 is None else x2.to(cuda_dev)).cpu()
+    xin = x if x2 is None else torch.cat([x, x2], 1)
+    ref = F.conv2d(xin.double(), w.double(), b.double())
+    err = RN.rel_l2(out.double().numpy(), ref.numpy())
+    record_error(f"conv2d_skip_gemm_{Ca}+{Cb}_{Cout}_{H}_B{B}", err)
+    assert err < 1e-5, err
+
+
 @pytest.mark.parametrize("B", [2, 64])
 def test_conv2d_1x1_skip_kernel(B, cuda_dev):
     """The 1x1 skip conv kernel (unet_conv1x1.hip: LDS-DMA'd input and gathered

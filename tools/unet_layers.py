@@ -57,7 +57,7 @@ def walk():
 
 
 layers = walk()
-KEYS = ("conv_kernel<", "conv_out_kernel<", "conv_out64_kernel<", "conv_in_kernel<", "conv_wino_kernel<", "conv_wino4_kernel<", "conv_wino4s_kernel<", "conv1x1_kernel<",
+KEYS = ("conv_kernel<", "skip_gemm_kernel<", "conv_out_kernel<", "conv_out64_kernel<", "conv_in_kernel<", "conv_wino_kernel<", "conv_wino4_kernel<", "conv_wino4s_kernel<", "conv1x1_kernel<",
         "conv_bf16_kernel<")
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if any(k in r["Kernel_Name"] for k in KEYS)]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
