@@ -309,6 +309,18 @@ def train_bench(dev, steps=200, B=32, T=500, reps=200):
                           "t / noise drawn in the graph)",
            "train_eager_steps_per_s": round(steps / el_eager, 1),
            "train_eager_final_loss": round(float(loss), 5)}
+    # the whole step on the same basis: forward (encoder convs + Linear
+    # layers) + the encoder convs' backward + the Linear layers' backward (2x their
+    # forward: input and weight gradients), per member, over the step's wall time
+    step_flop = (STEP_FLOP_PER_MEMBER + CONV_BWD_FLOP_PER_MEMBER
+                 + 2 * (STEP_FLOP_PER_MEMBER - CONV_FLOP_PER_MEMBER)) * B
+    step_tf = step_flop / (el / steps) / 1e12
+    out["train_step_roofline"] = {
+        "bound": "mfma", "achieved": round(step_tf, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(step_tf / PEAK_FP32_TFLOPS, 4), "flop_per_step": step_flop,
+        "traffic": _traffic(f"train_step_B{B}"),
+        "basis": "algorithmic FLOP of one step (forward + backward) / TrainPlan.run wall time per step; "
+                 "traffic: PMC bytes of the step's four kernels (tools/pmc_train.sh)"}
     # train_roofline: the conv backward alone on the state the plan's last step left
     stream = torch.cuda.current_stream(dev)
     lib = _lib.lib()

@@ -9,6 +9,16 @@ KERNELS = {  # json key -> kernel-name substring (bench.py R2 shape, fp32)
     "chain_B64_T1000": "faithful_chain_kernel",
     "strip_B64_fp32": "enc_fp32_kernel<false>",
 }
+# TRAIN=1 (tools/pmc_train.sh: tools/train_ref_probe.py --plan-only, B = 32):
+# the reference train step's kernels, and their sum per step
+TRAIN_KERNELS = {
+    "train_conv_bwd_B32": "conv_bwd_kernel",
+    "train_enc_B32": "enc_train_kernel",
+    "train_head_B32": "train_head_kernel<2>",
+    "train_final_B32": "train_final_kernel",
+}
+if os.environ.get("TRAIN"):
+    KERNELS = TRAIN_KERNELS
 
 
 def per_launch(d, counter, name):
@@ -37,9 +47,17 @@ for key, name in ({} if os.environ.get("UNET_KEY") else KERNELS).items():
         "launches": [len(fk), len(wk)],
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
                   "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
-        "workload": "bench.py R2 faithful, B=64, L=4693, T=1000 (chain: one launch = 1000 steps)",
+        "workload": ("tools/train_ref_probe.py --plan-only, B=32, L=4693 (TrainPlan)" if os.environ.get("TRAIN")
+                     else "bench.py R2 faithful, B=64, L=4693, T=1000 (chain: one launch = 1000 steps)"),
     }
     print(key, json.dumps(rec[key]))
+if os.environ.get("TRAIN") and all(k in rec for k in TRAIN_KERNELS):
+    rec["train_step_B32"] = {
+        "kernel": "enc_train + train_head<2> + conv_bwd + train_final (one step)",
+        "hbm_bytes_per_launch": sum(rec[k]["hbm_bytes_per_launch"] for k in TRAIN_KERNELS),
+        "method": "sum of the four kernels' per-launch medians (same passes)",
+        "workload": "tools/train_ref_probe.py --plan-only, B=32, L=4693 (TrainPlan)"}
+    print("train_step_B32", json.dumps(rec["train_step_B32"]))
 # U-Net: every ertd::unet:: kernel of the run, summed, per denoising step
 unet_steps = int(os.environ.get("UNET_STEPS", "0"))
 unet_key = os.environ.get("UNET_KEY", "unet_U2_B64_step")
