@@ -62,6 +62,7 @@ STRIPS_MEAS = -(-(((L_MEAS + 2 - 3) // 2 + 1 + 2 - 3) // 2 + 1) // 63)   # encod
 # conv2 input-gradient + conv2 weight-gradient (each = conv2's forward MACs x2)
 # + conv1 weight-gradient (= conv1's forward); conv1's input gradient is not needed
 CONV_BWD_FLOP_PER_MEMBER = 2 * 14_426_112 + 6_308_736
+CHAIN_FLOP_PER_MEMBER = 14_426_112 + 6_308_736   # conv_bwd_kernel<false>: conv2 dX + conv1 dW
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
 PEAK_BF16_TFLOPS = 2500.0    # dense bf16 MFMA
 PEAK_HBM_GBS = 8000.0
@@ -321,7 +322,9 @@ def train_bench(dev, steps=200, B=32, T=500, reps=200):
         "traffic": _traffic(f"train_step_B{B}"),
         "basis": "algorithmic FLOP of one step (forward + backward) / TrainPlan.run wall time per step; "
                  "traffic: PMC bytes of the step's four kernels (tools/pmc_train.sh)"}
-    # train_roofline: the conv backward alone on the state the plan's last step left
+    # train_roofline: the conv backward's dz1 chain kernel alone on the state the
+    # plan's last step left (conv2 dX + conv1 dW; conv2 dW = g x M runs in the
+    # head kernel's M workgroups and the final kernel)
     stream = torch.cuda.current_stream(dev)
     lib = _lib.lib()
 
@@ -340,13 +343,13 @@ def train_bench(dev, steps=200, B=32, T=500, reps=200):
         torch.cuda.synchronize(dev)
         rounds.append(e0.elapsed_time(e1) / reps)
     avg_ms = sum(rounds) / len(rounds)
-    flop = CONV_BWD_FLOP_PER_MEMBER * B
-    # per (member, strip): 448 v_mfma_f32_32x32x2 + 64 v_mfma_f32_16x16x4 (the dW1 edge
-    # columns, half the FLOP each) over its chain and dW2 workgroups
-    executed = (448 + 64 // 2) * 2 * 32 * 32 * 2 * B * STRIPS_MEAS
+    flop = CHAIN_FLOP_PER_MEMBER * B
+    # per (member, strip): 256 v_mfma_f32_32x32x2 + 64 v_mfma_f32_16x16x4 (the dW1 edge
+    # columns, half the FLOP each)
+    executed = (256 + 64 // 2) * 2 * 32 * 32 * 2 * B * STRIPS_MEAS
     ach = flop / (avg_ms * 1e-3) / 1e12
     out["train_roofline"] = {
-        "kernel": "conv_bwd_kernel", "bound": "mfma", "achieved": round(ach, 3),
+        "kernel": "conv_bwd_kernel<false> (the dz1 chain)", "bound": "mfma", "achieved": round(ach, 3),
         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
         "executed_frac": round(executed / (avg_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
         "traffic": _traffic(f"train_conv_bwd_B{B}"),
@@ -354,7 +357,7 @@ def train_bench(dev, steps=200, B=32, T=500, reps=200):
         "timing": f"HIP events around {reps} back-to-back launches x 5 rounds on the launching stream "
                   "(includes the ~1 us dispatch gap)",
         "algorithmic_flop_per_launch": flop,
-        "flop_basis": f"{CONV_BWD_FLOP_PER_MEMBER} FLOP per member (conv2 dX + conv2 dW + conv1 dW at "
+        "flop_basis": f"{CHAIN_FLOP_PER_MEMBER} FLOP per member (conv2 dX + conv1 dW at "
                       f"L={L_MEAS}) x {B} members",
         "executed_flop_per_launch": executed}
     return out

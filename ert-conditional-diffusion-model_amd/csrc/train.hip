@@ -47,6 +47,14 @@ constexpr int NG_W2 = C1 * K1;
 constexpr int NG_B1 = NG_W2 + C2 * K2;
 constexpr int NG_B2 = NG_B1 + C1;
 constexpr int NG = NG_B2 + C2;  // 7584 (every region a multiple of 4 floats)
+// the reference train step splits the row: conv_bwd's chain rows [dW1 | db1]
+// (NG1) per (member, strip), and w2m_body's rows [M | mask counts] (NG2) per
+// (member, group of W2M_NS strips) with dW2 = sum_b g_b[o] M_b[o][n] (dz2 =
+// g * mask: dW2 is linear in g, so M needs no g and runs beside the head)
+constexpr int NG1 = C1 * K1 + C1;   // 1376
+constexpr int NG2 = C2 * K2 + C2;   // 6208
+constexpr int W2M_NS = 3;           // strips per w2m workgroup
+__host__ __device__ inline int w2m_groups(int S) { return (S + W2M_NS - 1) / W2M_NS; }
 
 // saved activations per (member, strip): the conv1 images E[c][m] = a1(p = 2m),
 // O[c][m] = a1(p = 2m+1) at conv1 positions i = 2*j0 - 1 + p, p < 128 (zero
@@ -61,7 +69,8 @@ constexpr int WT_WT = WT_W3 + C2 * H;       // [128][128]  time_embed.0
 constexpr int WT_W0 = WT_WT + H * H;        // [K0][128]   mlp.0 (K0 = P + 256 <= 288)
 constexpr int WT_W2 = WT_W0 + (PMAX + 2 * H) * H;  // [128][32] mlp.2: W2T[k][o]
 constexpr int WT_W0B = WT_W2 + H * PMAX;    // [128][256]  mlp.0 columns P.. (16-B aligned rows): W0[j][P + k]
-constexpr int WT_FLOATS = WT_W0B + H * 2 * H;
+constexpr int WT_W5 = WT_W0B + H * 2 * H;   // [PMAX][128]  mlp.2 rows, zero past P
+constexpr int WT_FLOATS = WT_W5 + PMAX * H;
 
 constexpr int W2B_FRAG = 3 * 32 * 64;  // transposed-conv2 fragments (conv_bwd)
 #ifndef ENC_ABL
@@ -70,13 +79,16 @@ constexpr int W2B_FRAG = 3 * 32 * 64;  // transposed-conv2 fragments (conv_bwd)
 // train_final_kernel's conv-column reduction (see there)
 constexpr int FIN_CB_COLS = 64;                                  // float4 columns per block
 constexpr int FIN_NCB = (NG / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;  // 30 column blocks
+constexpr int FIN_NCB1 = (NG1 / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;  // split rows: 6 + 25
+constexpr int FIN_NCB2 = (NG2 / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;
 #ifndef FIN_RB_N
 #define FIN_RB_N 4
 #endif
 constexpr int FIN_RB = FIN_RB_N;                                 // row blocks
 constexpr int FIN_MAXR = FIN_RB < 8 ? 48 : 384 / FIN_RB;   // rows per wave held in flight
 constexpr int FIN_CNT_WORDS = 64;
-static_assert(FIN_NCB <= FIN_CNT_WORDS, "counter words");
+static_assert(FIN_NCB <= FIN_CNT_WORDS && FIN_NCB1 + FIN_NCB2 <= FIN_CNT_WORDS, "counter words");
+static_assert(NG1 + NG2 == NG, "split rows cover the gradient row");
 
 // ---------------------------------------------------------------------------
 // training forward of the condition encoder
@@ -117,9 +129,12 @@ __global__ __launch_bounds__(256) void enc_train_kernel(
       } else if (e < WT_W0B) {
         const int i = e - WT_W2, o = i & (PMAX - 1);
         v = o < P ? wd.mlp2_w[o * H + (i >> 5)] : 0.f;
-      } else {
+      } else if (e < WT_W5) {
         const int i = e - WT_W0B;
         v = wd.mlp0_w[(size_t)(i >> 8) * K0 + P + (i & 255)];
+      } else {
+        const int i = e - WT_W5, o = i >> 7;
+        v = o < P ? wd.mlp2_w[i] : 0.f;
       }
       wt[e] = v;
     }
@@ -315,31 +330,36 @@ template <int NOUT, int NQ, int KCM>
 struct SplitK4 {
   static_assert(NOUT / 4 * NQ <= HT, "threads");
   float4 w[KCM];
-  int k0, k1;
-  __device__ __forceinline__ void load(const float* __restrict__ Wp, int sk, int K, int tid) {
+  int k0, k1, kb;
+  // every load unconditional: the KCM rows from kb = min(k0, K - KCM) (rows
+  // outside [k0, k1) are never read by part(); idle threads load the last
+  // rows at one common address) -- no select on a loaded value, so nothing
+  // waits for the loads before their use, and one base address per slice
+  // (R >= KCM rows of Wp are readable; R >= K)
+  __device__ __forceinline__ void load(const float* __restrict__ Wp, int sk, int K, int R, int tid) {
     constexpr int NJ = NOUT / 4;
     const int j4 = tid % NJ, q = tid / NJ;
     const int kc = (K + NQ - 1) / NQ;
     k0 = q * kc;
     k1 = q < NQ ? min(K, k0 + kc) : k0;
+    kb = min(k0, R - KCM);
+    const float* wp = Wp + (q < NQ ? 4 * j4 : 0) + (size_t)kb * sk;
 #pragma unroll
-    for (int i = 0; i < KCM; ++i) {
-      const int k = k0 + i;
-      w[i] = k < k1 ? *reinterpret_cast<const float4*>(Wp + (size_t)k * sk + 4 * j4)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int i = 0; i < KCM; ++i) w[i] = *reinterpret_cast<const float4*>(wp + (size_t)i * sk);
   }
   __device__ __forceinline__ void part(const float* x, float4* part4, int tid) const {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int i = 0; i < KCM; ++i)
-      if (k0 + i < k1) {
-        const float xv = x[k0 + i];
+    for (int i = 0; i < KCM; ++i) {
+      const int k = kb + i;
+      if (k >= k0 && k < k1) {
+        const float xv = x[k];
         acc.x = fmaf(w[i].x, xv, acc.x);
         acc.y = fmaf(w[i].y, xv, acc.y);
         acc.z = fmaf(w[i].z, xv, acc.z);
         acc.w = fmaf(w[i].w, xv, acc.w);
       }
+    }
     if (tid < NOUT / 4 * NQ) part4[tid] = acc;
   }
   // output j: the NQ group partials in group order
@@ -371,29 +391,47 @@ struct HeadRng {  // the train step's own draws (TrainPlan): t ~ U{0..T-1}, nois
 };
 constexpr uint32_t RNG_TAG_T = 0x7A11u, RNG_TAG_NOISE = 0x7A12u;
 
+// the backward layers' weight slices (W itself: rows contiguous in the output index)
+struct HeadBwdW {
+  SplitK4<H, 8, PMAX / 8> w5;      // dz5: W2 rows (o), 128 columns (the zero-padded copy)
+  SplitK4<2 * H, 16, H / 16> w0;   // dhcat: W0B rows (j), 256 columns
+  SplitK4<C2, 16, H / 16> w3;      // g: W3 rows (j), 64 columns
+};
+
+template <bool PRE>
 __device__ __forceinline__ void head_forward(
     const ertd_weights& w, const float* __restrict__ wt, const float* __restrict__ x_in,
     const float* __restrict__ x0, const float* __restrict__ noise,
     const float* __restrict__ alpha_bar, const int64_t* __restrict__ t_vec,
     const float* __restrict__ freq, const float* __restrict__ partial, int S, int L2,
-    float* __restrict__ V, float* __restrict__ eps_out, const HeadRng* rng, HeadSmem& s, int b,
-    int tid) {
+    float* __restrict__ V, float* __restrict__ eps_out, HeadRng rng, HeadSmem& s, int b,
+    int tid, HeadBwdW& bw) {
   HSTAMP(0);
   const int P = w.param_dim;
+  // the pool partials first (the first barrier waits for these loads only):
+  // strips k = q, q + 16, ... of channel c summed per group q, the groups in order
+  const int pc = tid & 63, pq = tid >> 6;
+  float pv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = pq + (HT / 64) * u;
+    pv[u] = 0.f;
+    if (k < S) pv[u] = partial[((size_t)b * S + k) * C2 + pc];
+  }
   // this member's t, known to every thread (no LDS round trip before the
   // loads that depend on it)
   int tme;
-  if (rng) {  // Philox keyed (seed, member, step): independent of the grid and of the schedule
-    const uint32_t st = (uint32_t)*rng->step;
-    const u32x4 r = philox4x32_10(u32x4{0u, (uint32_t)b, st, RNG_TAG_T}, (uint32_t)rng->seed,
-                                  (uint32_t)(rng->seed >> 32));
-    tme = (int)(((uint64_t)r.x * (uint64_t)rng->T) >> 32);
-    if (tid == 0) rng->t_out[b] = tme;
+  if (rng.step) {  // Philox keyed (seed, member, step): independent of the grid and of the schedule
+    const uint32_t st = (uint32_t)*rng.step;
+    const u32x4 r = philox4x32_10(u32x4{0u, (uint32_t)b, st, RNG_TAG_T}, (uint32_t)rng.seed,
+                                  (uint32_t)(rng.seed >> 32));
+    tme = (int)(((uint64_t)r.x * (uint64_t)rng.T) >> 32);
+    if (tid == 0) rng.t_out[b] = tme;
     if (tid >= 64 && tid < 64 + P) {
       const int o = tid - 64;
-      const float z = philox_normal(rng->seed, (uint32_t)b, st, RNG_TAG_NOISE, o);
+      const float z = philox_normal(rng.seed, (uint32_t)b, st, RNG_TAG_NOISE, o);
       s.nz[o] = z;
-      rng->noise_out[(size_t)b * P + o] = z;
+      rng.noise_out[(size_t)b * P + o] = z;
     }
   } else {
     tme = (int)t_vec[b];
@@ -417,16 +455,17 @@ __device__ __forceinline__ void head_forward(
   // cond_emb (j4 < 32: outputs 0-127, K 64) and t_emb (j4 >= 32: 128-255, K 128) in one split:
   // 16 groups of 4 / 8 k each
   SplitK4<256, 16, 8> wce;
-  if ((tid & 63) < 32) wce.load(wt + WT_W3, H, C2, tid);
-  else wce.load(wt + WT_WT - H, H, H, tid);
+  {
+    const bool ce = (tid & 63) < 32;
+    wce.load(ce ? wt + WT_W3 : wt + WT_WT - H, H, ce ? C2 : H, ce ? C2 : H, tid);
+  }
   SplitK4<128, 32, (PMAX + 2 * H + 31) / 32> wh;
-  wh.load(wt + WT_W0, H, K0, tid);
-  SplitK4<PMAX, 32, H / 32> we;
-  we.load(wt + WT_W2, PMAX, H, tid);
-  {  // pool: strips k = q, q + 16, ... summed per group q, the groups in order
-    const int c = tid & 63, q = tid >> 6;
-    float acc = 0.f;
-    for (int k = q; k < S; k += HT / 64) acc += partial[((size_t)b * S + k) * C2 + c];
+  wh.load(wt + WT_W0, H, K0, K0, tid);
+  {  // pool: the group sums (strips past 4 * 16: a plain loop)
+    float acc = pv[0];
+#pragma unroll
+    for (int u = 1; u < 4; ++u) acc += pv[u];
+    for (int k = pq + 4 * (HT / 64); k < S; k += HT / 64) acc += partial[((size_t)b * S + k) * C2 + pc];
     s.part[tid] = acc;
   }
   __syncthreads(); HSTAMP(1);
@@ -452,6 +491,11 @@ __device__ __forceinline__ void head_forward(
   __syncthreads(); HSTAMP(2);
   // cond_emb = relu(W3 m + b3) (outputs 0-127), t_emb = relu(Wt e + bt) (128-255)
   wce.part((tid & 63) < 32 ? s.m : s.e, s.part4, tid);
+  // the later layers' slices into the registers wce leaves (each load lands
+  // during the phases before its use; a barrier waits for LDS only)
+  SplitK4<PMAX, 32, H / 32> we;
+  we.load(wt + WT_W2, PMAX, H, H, tid);
+  if constexpr (PRE) bw.w5.load(wt + WT_W5, H, P, PMAX, tid);
   __syncthreads(); HSTAMP(3);
   if (tid < 2 * H) {
     const float y = SplitK4<256, 16, 8>::sum(s.part4, tid);
@@ -466,10 +510,12 @@ __device__ __forceinline__ void head_forward(
   }
   __syncthreads(); HSTAMP(4);
   wh.part(s.hc, s.part4, tid);   // h = relu(W0 hcat + b0)
+  if constexpr (PRE) bw.w0.load(wt + WT_W0B, 2 * H, H, H, tid);
   __syncthreads(); HSTAMP(5);
   if (tid < H) s.h[tid] = fmaxf(SplitK4<128, 32, (PMAX + 2 * H + 31) / 32>::sum(s.part4, tid) + bh, 0.f);
   __syncthreads(); HSTAMP(6);
   we.part(s.h, s.part4, tid);    // eps = W2 h + b2
+  if constexpr (PRE) bw.w3.load(w.enc6_w, C2, H, H, tid);
   __syncthreads(); HSTAMP(7);
   if (tid < P) {
     const float y = SplitK4<PMAX, 32, H / 32>::sum(s.part4, tid) + be;
@@ -493,17 +539,19 @@ __device__ __forceinline__ void head_backward(
     const ertd_weights& w, const float* __restrict__ wt, const float* __restrict__ dout_in,
     const float* nz_v, float two_over_n,
     int L2, float* __restrict__ V, float* __restrict__ dx_out, const float* eps_v, const float* h_v,
-    const float* hcat_v, HeadSmem& s, int b, int tid) {
+    const float* hcat_v, HeadSmem& s, int b, int tid, HeadBwdW& bw, bool loaded) {
   const int P = w.param_dim;
   const int K0 = P + 2 * H;
-  // every backward layer's weight slice into registers now (W itself: rows
-  // contiguous in the output index)
-  SplitK4<H, 8, PMAX / 8> w5;            // dz5: W2 rows (o), 128 columns
-  w5.load(w.mlp2_w, H, P, tid);
-  SplitK4<2 * H, 16, H / 16> w0;          // dhcat: W0B rows (j), 256 columns
-  w0.load(wt + WT_W0B, 2 * H, H, tid);
-  SplitK4<C2, 16, H / 16> w3;             // g: W3 rows (j), 64 columns
-  w3.load(w.enc6_w, C2, H, tid);
+  // every backward layer's weight slice into registers (the fused step issued
+  // them during the forward)
+  if (!loaded) {
+    bw.w5.load(wt + WT_W5, H, P, PMAX, tid);
+    bw.w0.load(wt + WT_W0B, 2 * H, H, H, tid);
+    bw.w3.load(w.enc6_w, C2, H, H, tid);
+  }
+  const auto& w5 = bw.w5;
+  const auto& w0 = bw.w0;
+  const auto& w3 = bw.w3;
   if (tid < PMAX) {
     float d = 0.f, sq = 0.f;
     if (tid < P) {
@@ -560,33 +608,6 @@ __device__ __forceinline__ void head_backward(
   if (tid < C2) V[TV_G + tid] = SplitK4<C2, 16, H / 16>::sum(s.part4, tid) / (float)L2;
 }
 
-// MODE 0: forward only; 1: backward only (of the last forward's saved row);
-// 2: both (the train step; rng != null: the step draws its own t and noise)
-template <int MODE>
-__global__ __launch_bounds__(HT) void train_head_kernel(
-    ertd_weights w, const float* __restrict__ wt, const float* __restrict__ x_in,
-    const float* __restrict__ x0, const float* __restrict__ noise,
-    const float* __restrict__ alpha_bar, const int64_t* __restrict__ t_vec,
-    const float* __restrict__ freq, const float* __restrict__ partial, int S, int L2,
-    float* __restrict__ vec, float* __restrict__ eps_out, const float* __restrict__ dout_in,
-    float two_over_n, float* __restrict__ dx_out, HeadRng rng) {
-  __shared__ HeadSmem s;
-  const int b = blockIdx.x, tid = threadIdx.x;
-  float* V = vec + (size_t)b * TV;
-  const HeadRng* rp = rng.step ? &rng : nullptr;
-  if constexpr (MODE != 1)
-    head_forward(w, wt, x_in, x0, noise, alpha_bar, t_vec, freq, partial, S, L2, V, eps_out, rp, s, b,
-                 tid);
-  if constexpr (MODE == 2) {
-    __syncthreads(); HSTAMP(17);
-    head_backward(w, wt, dout_in, s.nz, two_over_n, L2, V, dx_out, s.eps, s.h, s.hc, s, b, tid);
-  }
-  if constexpr (MODE == 1) {
-    head_backward(w, wt, dout_in, noise ? noise + (size_t)b * w.param_dim : nullptr, two_over_n, L2, V,
-                  dx_out, V + TV_EPS, V + TV_H, V + TV_HCAT, s, b, tid);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // conv backward: two 256-thread workgroups per (member, strip of J conv2
 // outputs), one launch -- the first B*S blocks the dz1 chain, the next B*S the
@@ -603,7 +624,7 @@ __global__ __launch_bounds__(HT) void train_head_kernel(
 // the dW1 halves take their place: 51.6 KB -> 3 workgroups per CU.
 // ---------------------------------------------------------------------------
 #ifndef CBW_ABL
-#define CBW_ABL 0  // diagnostic variants only (tools/cbw_abl.sh): bit mask of skipped phases
+#define CBW_ABL 0  // diagnostic variants only (tools/cbw_abl.sh): bit mask of skipped phases (16: no dW2 blocks)
 #endif
 constexpr int DZ2P = 65;   // dz2 row pitch (column reads conflict-free)
 constexpr int DZ1P = 129;  // dz1 row pitch
@@ -684,7 +705,8 @@ __device__ __forceinline__ void dw2_tile(const ConvBwdSmem& sm, int tt, int h, i
 
 // the a1 images (the forward's float4 rows) and dz2 = g * mask (+ the db2
 // partial sums of the four q' classes) into LDS
-__device__ __forceinline__ void conv_bwd_images(ConvBwdSmem& sm, const float* __restrict__ a1s,
+template <bool ONES = false, class SM>
+__device__ __forceinline__ void conv_bwd_images(SM& sm, const float* __restrict__ a1s,
                                                 const uint32_t* __restrict__ m2w,
                                                 const float* __restrict__ g, int g_stride, int b,
                                                 int item, int strip, int S, int tid) {
@@ -703,7 +725,7 @@ __device__ __forceinline__ void conv_bwd_images(ConvBwdSmem& sm, const float* __
   }
   {
     const int o = tid & 63, qb = tid >> 6;
-    const float go = g[(size_t)b * g_stride + o];
+    const float go = ONES ? 1.f : g[(size_t)b * g_stride + o];
     const uint32_t* mw = m2w + (size_t)item * M2W_WORDS + (o >> 5);
     const bool next = strip + 1 < S;
     uint32_t wd[17];  // every word loaded up front (unconditional, clamped), then used
@@ -727,6 +749,9 @@ __device__ __forceinline__ void conv_bwd_images(ConvBwdSmem& sm, const float* __
   }
 }
 
+// W2: the dW2 work too (dW2 blocks + two tiles per chain block, rows of NG);
+// else the chain alone, rows [dW1 | db1] of NG1 (the reference train step)
+template <bool W2>
 __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     const float* __restrict__ w2b, const float* __restrict__ cond, const float* __restrict__ a1s,
     const uint32_t* __restrict__ m2w, const float* __restrict__ g, int g_stride, int L, int L1,
@@ -737,13 +762,15 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
   // dispatch order: all chain blocks, then all dW2 blocks (CBW_ORDER = 1: chain
   // items [0, c1), dW2 items [0, c2), the remaining chain items, the remaining
   // dW2 items, c1 = 2 and c2 = 1 per CU -- measured slower)
-  const int nit = (int)gridDim.x / 2, bi = (int)blockIdx.x;
-  const bool w2blk = CBW_ORDER ? (bi >= c1 && bi < c1 + c2) || bi >= nit + c2 : bi >= nit;
+  constexpr bool WB = W2 && (CBW_ABL & 16) == 0;   // dW2 blocks in the grid
+  const int nit = WB ? (int)gridDim.x / 2 : (int)gridDim.x, bi = (int)blockIdx.x;
+  const bool w2blk = !WB ? false : CBW_ORDER ? (bi >= c1 && bi < c1 + c2) || bi >= nit + c2 : bi >= nit;
   const int item = !CBW_ORDER ? (w2blk ? bi - nit : bi)
                  : bi < c1 ? bi : bi < c1 + c2 ? bi - c1 : bi < nit + c2 ? bi - c2 : bi - nit;
   const int b = item / S, strip = item - b * S;
   const int j0 = strip * J;
-  float* G = gpart + (size_t)item * NG;
+  float* G = gpart + (size_t)item * (W2 ? NG : NG1);
+  constexpr int GB1 = W2 ? NG_B1 : C1 * K1;   // db1 offset in the row
 
   if (w2blk) {
     conv_bwd_images(sm, a1s, m2w, g, g_stride, b, item, strip, S, tid);
@@ -810,7 +837,7 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
       sm.DZ1[c][r] = (owned && act > 0.f) ? acc[k] : 0.f;
     }
   }
-  if constexpr ((CBW_ABL & 2) == 0) {
+  if constexpr (W2 && (CBW_ABL & 2) == 0) {
     if (!oddw) dw2_tile(sm, wave, h, l32, G);   // tiles 0, 1 (2-5: the dW2 blocks)
   }
   __syncthreads();
@@ -887,7 +914,7 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     for (int i = 0; i < 4; ++i) {
       const int o = 16 * (wave - 2) + 4 * (lane >> 4) + i;
       if (n1 < K1) G[NG_W1 + o * K1 + n1] = acc1[i];
-      else if (n1 == K1) G[NG_B1 + o] = acc1[i];
+      else if (n1 == K1) G[GB1 + o] = acc1[i];
     }
   }
   __syncthreads();
@@ -926,8 +953,148 @@ __global__ __launch_bounds__(256, 3) void conv_bwd_kernel(
     const int nt = n >> 5, col = n & 31;
     G[NG_W1 + idx] = sm.red[nt][o][col] + sm.red[2 + nt][o][col];
   }
-  if (tid < C1) G[NG_B1 + tid] = sm.red[1][tid][K1 - 32] + sm.red[3][tid][K1 - 32];
+  if (tid < C1) G[GB1 + tid] = sm.red[1][tid][K1 - 32] + sm.red[3][tid][K1 - 32];
 #endif
+}
+
+// k-half kh of dW2 tile tt (k-steps 16 kh .. 16 kh + 15 of dw2_tile), added to acc
+template <class SM>
+__device__ __forceinline__ void dw2_half(const SM& sm, int tt, int kh, int h, int l32,
+                                         f32x16& acc) {
+  const int ot = tt / 3, nt = tt - 3 * (tt / 3);
+  const int n = nt * 32 + l32, c = n / 3, kk = n - 3 * (n / 3);
+  const float* ab = (kk == 1 ? &sm.AO[c][h] : &sm.AE[c][h + (kk == 2 ? 1 : 0)]) + 32 * kh;
+  const float* zb = &sm.DZ2[ot * 32 + l32][h] + 32 * kh;
+  const int qb = 32 * kh + h;
+  mfma_pipe<16, CBW_AHEAD>(acc, [&](int s) { return zb[2 * s]; },
+                           // q' = 63 is the halo: excluded
+                           [&](int s) { return (qb + 2 * s < J) ? ab[2 * s] : 0.f; });
+}
+
+// M = dW2 / g of a group of W2M_NS strips of one member (dz2 = mask: the same
+// images and tiles as the dW2 blocks with g = 1), and the mask counts (db2 /
+// g).  Three slots of 4 waves take one strip each; a slot's 6 tiles x 2
+// k-halves: wave w owns half tiles w, w + 4, w + 8 (tile hv / 2, half hv % 2).
+// The odd waves' halves go to their partner through LDS, then slots 1 and 2
+// to slot 0, in a fixed order.  Reads only the forward's a1s / m2w: workgroups
+// of the head kernel's launch run it beside the per-member head blocks.
+struct W2mSmem {
+  float AE[C1][HS];
+  float AO[C1][HS];
+  float DZ2[C2][DZ2P];
+  float db2p[4][C2];
+};
+static_assert(W2M_NS == 3, "one slot per strip");
+static_assert(sizeof(W2mSmem) >= (6 * 1024 + C2) * sizeof(float), "exchange buffer");
+__device__ __forceinline__ void w2m_body(W2mSmem (&msm)[W2M_NS], const float* __restrict__ a1s,
+                                         const uint32_t* __restrict__ m2w, int S,
+                                         float* __restrict__ mrows, int mb, int tid) {
+  const int slot = tid >> 8, t = tid & 255, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int ng = w2m_groups(S);
+  const int b = mb / ng;
+  const int st = (mb - b * ng) * W2M_NS + slot;   // this slot's strip
+  const bool act = st < S;
+  W2mSmem& sm = msm[slot];
+  f32x16 acc[3] = {};
+  float cnt = 0.f;
+  if (act) conv_bwd_images<true>(sm, a1s, m2w, nullptr, 0, b, b * S + st, st, S, t);
+  __syncthreads();
+  if (act) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int hv = wave + 4 * u;
+      dw2_half(sm, hv >> 1, hv & 1, h, l32, acc[u]);
+    }
+    if (t < C2) cnt = (sm.db2p[0][t] + sm.db2p[1][t]) + (sm.db2p[2][t] + sm.db2p[3][t]);
+  }
+  __syncthreads();
+  float* xb = reinterpret_cast<float*>(&sm);   // the slot's dead images
+  const int pair = wave >> 1;
+  if (wave & 1) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xb[(pair * 3 + u) * 1024 + r * 64 + lane] = acc[u][r];
+  }
+  __syncthreads();
+  if ((wave & 1) == 0) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][r] += xb[(pair * 3 + u) * 1024 + r * 64 + lane];
+  }
+  __syncthreads();
+  if (slot > 0) {
+    if ((wave & 1) == 0) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xb[(pair * 3 + u) * 1024 + r * 64 + lane] = acc[u][r];
+    }
+    if (t < C2) xb[6 * 1024 + t] = cnt;
+  }
+  __syncthreads();
+  if (slot != 0) return;
+  const float* x1 = reinterpret_cast<const float*>(&msm[1]);
+  const float* x2 = reinterpret_cast<const float*>(&msm[2]);
+  float* M = mrows + (size_t)mb * NG2;
+  if ((wave & 1) == 0) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int tt = (wave + 4 * u) >> 1, ot = tt / 3, nt = tt - 3 * (tt / 3);
+      const int n = nt * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ot * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int xi = (pair * 3 + u) * 1024 + r * 64 + lane;
+        M[o * K2 + n] = (acc[u][r] + x1[xi]) + x2[xi];
+      }
+    }
+  }
+  if (t < C2) M[C2 * K2 + t] = (cnt + x1[6 * 1024 + t]) + x2[6 * 1024 + t];
+}
+
+// MODE 1 / 2 with mw.mrows: workgroups B .. B + B * w2m_groups(S) - 1 of the
+// launch run w2m_body (waves 0-11; the others leave at once) on the CUs the B
+// head blocks leave idle
+struct W2mArgs {
+  const float* a1s;
+  const uint32_t* m2w;
+  float* mrows;   // null: head blocks only
+  int nb;         // head blocks (B)
+};
+template <int MODE>
+__global__ __launch_bounds__(HT) void train_head_kernel(
+    ertd_weights w, const float* __restrict__ wt, const float* __restrict__ x_in,
+    const float* __restrict__ x0, const float* __restrict__ noise,
+    const float* __restrict__ alpha_bar, const int64_t* __restrict__ t_vec,
+    const float* __restrict__ freq, const float* __restrict__ partial, int S, int L2,
+    float* __restrict__ vec, float* __restrict__ eps_out, const float* __restrict__ dout_in,
+    float two_over_n, float* __restrict__ dx_out, HeadRng rng, W2mArgs mw) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if constexpr (MODE != 0) {
+    if (mw.mrows && b >= mw.nb) {
+      __shared__ __attribute__((aligned(16))) W2mSmem msm[W2M_NS];
+      if (tid >= 256 * W2M_NS) return;
+      w2m_body(msm, mw.a1s, mw.m2w, S, mw.mrows, b - mw.nb, tid);
+      return;
+    }
+  }
+  __shared__ HeadSmem s;
+  float* V = vec + (size_t)b * TV;
+  HeadBwdW bw;
+  if constexpr (MODE != 1)
+    head_forward<MODE == 2>(w, wt, x_in, x0, noise, alpha_bar, t_vec, freq, partial, S, L2, V, eps_out, rng,
+                            s, b, tid, bw);
+  if constexpr (MODE == 2) {
+    __syncthreads(); HSTAMP(17);
+    head_backward(w, wt, dout_in, s.nz, two_over_n, L2, V, dx_out, s.eps, s.h, s.hc, s, b, tid, bw, true);
+  }
+  if constexpr (MODE == 1) {
+    head_backward(w, wt, dout_in, noise ? noise + (size_t)b * w.param_dim : nullptr, two_over_n, L2, V,
+                  dx_out, V + TV_EPS, V + TV_H, V + TV_HCAT, s, b, tid, bw, false);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -985,6 +1152,11 @@ struct FinalArgs {
   const int* step_ctr;
   int tab_first, tab_len;
   int conv_off;          // diagnostic variants only (FIN_ABL): block index offset
+  // split rows (the reference train step): gpart rows are [dW1 | db1] (NG1),
+  // mpart's rows2 rows [M | counts] (NG2) of member row / ngrp, weighted by
+  // that member's g = vec[TV_G ..]
+  const float* mpart;
+  int rows2, ngrp;
 };
 
 __device__ __forceinline__ AdamHyper fetch_hyper(const FinalArgs& a) {
@@ -1004,23 +1176,34 @@ __device__ __forceinline__ float ld_wt(const float* p) {    // sc1 load (L2, not
                                            __HIP_MEMORY_SCOPE_AGENT));
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   __shared__ float4 red[4][FIN_CB_COLS];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Adam's scalars first: their (dependent) loads overlap the gradient loads
   const AdamHyper hy = a.param[0] ? fetch_hyper(a) : AdamHyper{};
+  constexpr int NCB = SPLIT ? FIN_NCB1 + FIN_NCB2 : FIN_NCB;
   const int bx = blockIdx.x + a.conv_off;
-  if (bx < FIN_NCB * FIN_RB) {
+  if (bx < NCB * FIN_RB) {
     const int cb = bx / FIN_RB, rb = bx - cb * FIN_RB;
-    const int col4 = cb * FIN_CB_COLS + lane;
-    const bool ok = col4 < NG / 4;
+    const bool seg2 = SPLIT && cb >= FIN_NCB1;   // the M rows
+    const int col4 = (seg2 ? cb - FIN_NCB1 : cb) * FIN_CB_COLS + lane;
+    const int ncol4 = !SPLIT ? NG / 4 : seg2 ? NG2 / 4 : NG1 / 4;   // row pitch (float4)
+    const bool ok = col4 < ncol4;
     const int e0 = col4 * 4;
+    const int fcol = (seg2 ? NG1 : 0) + e0;      // column of the row-block sums
     int k, off;
-    if (e0 < NG_W2) { k = 0; off = e0 - NG_W1; }        // condition_encoder.0.weight
-    else if (e0 < NG_B1) { k = 2; off = e0 - NG_W2; }   // condition_encoder.2.weight
-    else if (e0 < NG_B2) { k = 1; off = e0 - NG_B1; }   // condition_encoder.0.bias
-    else { k = 3; off = e0 - NG_B2; }                   // condition_encoder.2.bias
+    if constexpr (!SPLIT) {
+      if (e0 < NG_W2) { k = 0; off = e0 - NG_W1; }        // condition_encoder.0.weight
+      else if (e0 < NG_B1) { k = 2; off = e0 - NG_W2; }   // condition_encoder.2.weight
+      else if (e0 < NG_B2) { k = 1; off = e0 - NG_B1; }   // condition_encoder.0.bias
+      else { k = 3; off = e0 - NG_B2; }                   // condition_encoder.2.bias
+    } else if (!seg2) {
+      if (e0 < C1 * K1) { k = 0; off = e0; } else { k = 1; off = e0 - C1 * K1; }
+    } else {
+      if (e0 < C2 * K2) { k = 2; off = e0; } else { k = 3; off = e0 - C2 * K2; }
+    }
     // Adam's operands of the lane's 4 elements, prefetched (used by the last block only)
     float pv[4] = {}, mv[4] = {}, vv[4] = {};
     if (a.param[0] && ok && wave == 0) {
@@ -1031,21 +1214,47 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
         vv[q] = a.v[k][off + q];
       }
     }
-    const int rpb = (a.rows + FIN_RB - 1) / FIN_RB;
-    const int r0 = rb * rpb, r1 = min(a.rows, r0 + rpb);
+    const int rows = seg2 ? a.rows2 : a.rows;
+    const int rpb = (rows + FIN_RB - 1) / FIN_RB;
+    const int r0 = rb * rpb, r1 = min(rows, r0 + rpb);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok) {
+    if (ok && !seg2) {
       const float4* src = reinterpret_cast<const float4*>(a.gpart) + col4;
       for (int rbase = r0 + wave; rbase < r1; rbase += 4 * FIN_MAXR) {
         float4 x[FIN_MAXR];
 #pragma unroll
         for (int i = 0; i < FIN_MAXR; ++i) {
           const int r = rbase + 4 * i;
-          x[i] = r < r1 ? src[(size_t)r * (NG / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
+          x[i] = r < r1 ? src[(size_t)r * ncol4] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int i = 0; i < FIN_MAXR; ++i) {
           acc.x += x[i].x; acc.y += x[i].y; acc.z += x[i].z; acc.w += x[i].w;
+        }
+      }
+    } else if (ok) {   // M rows times the member's g: one o for 4 weight columns, o .. o+3 for counts
+      constexpr int NR = 16;
+      const float4* src = reinterpret_cast<const float4*>(a.mpart) + col4;
+      const bool wcol = e0 < C2 * K2;
+      const int o0 = wcol ? e0 / K2 : e0 - C2 * K2, od = wcol ? 0 : 1;
+      const float* gv = a.vec + TV_G + o0;
+      for (int rbase = r0 + wave; rbase < r1; rbase += 4 * NR) {
+        float4 x[NR], gq[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int r = rbase + 4 * i;
+          x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+          gq[i] = x[i];
+          if (r < r1) {
+            x[i] = src[(size_t)r * ncol4];
+            const float* gp = gv + (size_t)(r / a.ngrp) * TV;
+            gq[i] = make_float4(gp[0], gp[od], gp[2 * od], gp[3 * od]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          acc.x += x[i].x * gq[i].x; acc.y += x[i].y * gq[i].y;
+          acc.z += x[i].z * gq[i].z; acc.w += x[i].w * gq[i].w;
         }
       }
     }
@@ -1059,7 +1268,7 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
         s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
       }
       if (ok) {
-        float* f = a.fin + (size_t)rb * NG + col4 * 4;
+        float* f = a.fin + (size_t)rb * NG + fcol;
         st_wt(f, s.x); st_wt(f + 1, s.y); st_wt(f + 2, s.z); st_wt(f + 3, s.w);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1077,7 +1286,7 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
     float gv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < FIN_RB; ++q) {
-      const float* f = a.fin + (size_t)q * NG + col4 * 4;
+      const float* f = a.fin + (size_t)q * NG + fcol;
 #pragma unroll
       for (int e = 0; e < 4; ++e) gv[e] += ld_wt(f + e);
     }
@@ -1098,7 +1307,7 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   }
   // dense layers: one thread per element, a chain over the members
   const int H0 = a.P + 2 * H;
-  int i = (bx - FIN_NCB * FIN_RB) * 256 + tid;
+  int i = (bx - NCB * FIN_RB) * 256 + tid;
   int dz_off, in_off, kdim, k;
   bool bias = false;
   if (i < H * C2) { dz_off = TV_DZ3; in_off = TV_M; kdim = C2; k = 4; }
@@ -1201,6 +1410,7 @@ struct TrainWs {
   float* vec;      // (B, TV); the reference train step only
   float* wt;       // (WT_FLOATS) k-major dense weights; the reference train step only
   float* w2b;      // (W2B_FRAG) transposed-conv2 fragments
+  float* mpart;    // (B * w2m_groups(S), NG2) w2m rows; the reference train step only
 };
 
 // the encoder part (also the U-Net's condition branch), then the member rows
@@ -1220,6 +1430,7 @@ size_t ws_layout(int B, int L, bool with_vec, float* base, TrainWs* out) {
   if (with_vec) {
     w.vec = base + o; o += al((size_t)B * TV);
     w.wt = base + o; o += al(WT_FLOATS);
+    w.mpart = base + o; o += al((size_t)B * w2m_groups(S) * NG2);
   }
   if (out) *out = w;
   return o;
@@ -1233,9 +1444,12 @@ int dense_count(int P) { return H * C2 + H + H * H + H + H * (P + 2 * H) + H + P
 #endif
 hipError_t launch_final(FinalArgs& a, bool dense, hipStream_t s) {
   if ((FIN_ABL & 1) != 0) dense = false;
-  int blocks = FIN_NCB * FIN_RB + (dense ? (dense_count(a.P) + 255) / 256 : 0);
-  if ((FIN_ABL & 2) != 0) { a.conv_off = FIN_NCB * FIN_RB; blocks -= FIN_NCB * FIN_RB; }
-  train_final_kernel<<<blocks, 256, 0, s>>>(a);
+  const bool split = a.mpart != nullptr;
+  const int ncb = (split ? FIN_NCB1 + FIN_NCB2 : FIN_NCB) * FIN_RB;
+  int blocks = ncb + (dense ? (dense_count(a.P) + 255) / 256 : 0);
+  if ((FIN_ABL & 2) != 0) { a.conv_off = ncb; blocks -= ncb; }
+  if (split) train_final_kernel<true><<<blocks, 256, 0, s>>>(a);
+  else train_final_kernel<false><<<blocks, 256, 0, s>>>(a);
   return hipGetLastError();
 }
 
@@ -1271,14 +1485,29 @@ hipError_t launch_enc(const float* w1, const float* b1, const float* w2, const f
 }
 
 // (the W2 fragments are the ones the forward on this workspace wrote)
+// w2: with the dW2 work (rows of NG); else the chain alone (rows of NG1)
 hipError_t launch_conv_bwd(const float* cond, const TrainWs& W, const float* g, int g_stride, int B,
-                           int L, hipStream_t s) {
+                           int L, bool w2, hipStream_t s) {
   const int L1 = conv_len(L), L2 = conv_len(L1), S = n_strips(L2);
   const int nit = B * S, cus = device_cu_count();
   const int c1 = nit < 2 * cus ? nit : 2 * cus, c2 = nit < cus ? nit : cus;
-  conv_bwd_kernel<<<dim3((unsigned)(2 * nit)), 256, 0, s>>>(W.w2b, cond, W.a1s, W.m2w, g, g_stride, L, L1,
-                                                            L2, S, W.gpart, c1, c2);
+  if (w2)
+    conv_bwd_kernel<true><<<dim3((unsigned)((CBW_ABL & 16) ? nit : 2 * nit)), 256, 0, s>>>(
+        W.w2b, cond, W.a1s, W.m2w, g, g_stride, L, L1, L2, S, W.gpart, c1, c2);
+  else
+    conv_bwd_kernel<false><<<dim3((unsigned)nit), 256, 0, s>>>(W.w2b, cond, W.a1s, W.m2w, g, g_stride,
+                                                              L, L1, L2, S, W.gpart, c1, c2);
   return hipGetLastError();
+}
+
+W2mArgs w2m_args(const TrainWs& W, int B) { return W2mArgs{W.a1s, W.m2w, W.mpart, B}; }
+int head_grid(int B, int L) { return B + B * w2m_groups(n_strips(conv_len(conv_len(L)))); }
+
+void set_split(FinalArgs& a, const TrainWs& W, int B, int L) {
+  const int S = n_strips(conv_len(conv_len(L)));
+  a.mpart = W.mpart;
+  a.ngrp = w2m_groups(S);
+  a.rows2 = B * a.ngrp;
 }
 
 }  // namespace
@@ -1290,7 +1519,7 @@ size_t train_ws_floats(int B, int L) { return ws_layout(B, L, true, nullptr, nul
 hipError_t launch_train_conv_backward(const float* cond, int B, int L, float* ws, hipStream_t s) {
   TrainWs W;
   ws_layout(B, L, true, ws, &W);
-  return launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, s);
+  return launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, false, s);
 }
 
 void adam_table_host(int step_first, int n, float lr, float beta1, float beta2, float eps,
@@ -1311,7 +1540,7 @@ hipError_t launch_train_forward(const ertd_weights& w, const float* x_in, const 
   hipError_t e = launch_enc(w.enc0_w, w.enc0_b, w.enc2_w, w.enc2_b, cond, B, L, W, nullptr, &w, s);
   if (e != hipSuccess) return e;
   train_head_kernel<0><<<B, HT, 0, s>>>(w, W.wt, x_in, x0, noise, alpha_bar, t, freq, W.partial, S, L2,
-                                        W.vec, eps_out, nullptr, 0.f, nullptr, HeadRng{});
+                                        W.vec, eps_out, nullptr, 0.f, nullptr, HeadRng{}, W2mArgs{});
   return hipGetLastError();
 }
 
@@ -1323,13 +1552,16 @@ hipError_t launch_train_backward(const ertd_weights& w, const float* dout, const
   const int P = w.param_dim;
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
   const float two_over_n = (float)(2.0 / ((double)B * P));
-  train_head_kernel<1><<<B, HT, 0, s>>>(w, W.wt, nullptr, nullptr, noise, nullptr, nullptr, nullptr,
-                                        nullptr, S, L2, W.vec, nullptr, dout, two_over_n, dx_out,
-                                        HeadRng{});
-  hipError_t e = launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, s);
+  train_head_kernel<1><<<head_grid(B, L), HT, 0, s>>>(w, W.wt, nullptr, nullptr, noise, nullptr, nullptr,
+                                                      nullptr, nullptr, S, L2, W.vec, nullptr, dout,
+                                                      two_over_n, dx_out, HeadRng{}, w2m_args(W, B));
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, false, s);
   if (e != hipSuccess) return e;
   FinalArgs a = final_args(W, B * S);
   set_dense(a, w, W, B, grads, loss_out);
+  set_split(a, W, B, L);
   return launch_final(a, true, s);
 }
 
@@ -1355,12 +1587,16 @@ hipError_t launch_train_step(const ertd_weights& w, const float* x0, const int64
     rng.t_out = const_cast<int64_t*>(t);
     rng.noise_out = const_cast<float*>(noise);
   }
-  train_head_kernel<2><<<B, HT, 0, s>>>(w, W.wt, nullptr, x0, noise, alpha_bar, t, freq, W.partial, S,
-                                        L2, W.vec, nullptr, nullptr, two_over_n, nullptr, rng);
-  e = launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, s);
+  train_head_kernel<2><<<head_grid(B, L), HT, 0, s>>>(w, W.wt, nullptr, x0, noise, alpha_bar, t, freq,
+                                                      W.partial, S, L2, W.vec, nullptr, nullptr,
+                                                      two_over_n, nullptr, rng, w2m_args(W, B));
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_conv_bwd(cond, W, W.vec + TV_G, TV, B, L, false, s);
   if (e != hipSuccess) return e;
   FinalArgs a = final_args(W, B * S);
   set_dense(a, w, W, B, grads, loss_out);
+  set_split(a, W, B, L);
   param_list(w, a.param);
   for (int k = 0; k < 12; ++k) {
     a.m[k] = exp_avg[k];
@@ -1400,7 +1636,7 @@ hipError_t launch_encoder_conv_backward(const float* w2, const float* cond, cons
   ws_layout(B, L, false, ws, &W);
   const int L2 = conv_len(conv_len(L)), S = n_strips(L2);
   (void)w2;  // the fragments of the forward on this workspace
-  hipError_t e = launch_conv_bwd(cond, W, g, C2, B, L, s);
+  hipError_t e = launch_conv_bwd(cond, W, g, C2, B, L, true, s);
   if (e != hipSuccess) return e;
   FinalArgs a = final_args(W, B * S);
   a.grad[0] = dw1;
