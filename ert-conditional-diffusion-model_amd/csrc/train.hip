@@ -79,15 +79,13 @@ constexpr int W2B_FRAG = 3 * 32 * 64;  // transposed-conv2 fragments (conv_bwd)
 // train_final_kernel's conv-column reduction (see there)
 constexpr int FIN_CB_COLS = 64;                                  // float4 columns per block
 constexpr int FIN_NCB = (NG / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;  // 30 column blocks
-constexpr int FIN_NCB1 = (NG1 / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;  // split rows: 6 + 25
-constexpr int FIN_NCB2 = (NG2 / 4 + FIN_CB_COLS - 1) / FIN_CB_COLS;
 #ifndef FIN_RB_N
 #define FIN_RB_N 4
 #endif
 constexpr int FIN_RB = FIN_RB_N;                                 // row blocks
 constexpr int FIN_MAXR = FIN_RB < 8 ? 48 : 384 / FIN_RB;   // rows per wave held in flight
 constexpr int FIN_CNT_WORDS = 64;
-static_assert(FIN_NCB <= FIN_CNT_WORDS && FIN_NCB1 + FIN_NCB2 <= FIN_CNT_WORDS, "counter words");
+static_assert(FIN_NCB <= FIN_CNT_WORDS, "counter words");
 static_assert(NG1 + NG2 == NG, "split rows cover the gradient row");
 
 // ---------------------------------------------------------------------------
@@ -1176,6 +1174,107 @@ __device__ __forceinline__ float ld_wt(const float* p) {    // sc1 load (L2, not
                                            __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// Split rows (the reference train step): one level.  Workgroup = 16 float4
+// columns of one segment ([dW1 | db1] over the rows chain rows, or [M |
+// counts] over the rows2 M rows weighted by their member's g); thread (rg,
+// col) sums rows rg, rg + 16, ... (all of its loads in flight), the 16 row
+// groups are added in order, and the same thread applies Adam.
+constexpr int FS_COLS = 16;
+constexpr int FS_NCB1 = (NG1 / 4 + FS_COLS - 1) / FS_COLS;   // 22
+constexpr int FS_NCB2 = (NG2 / 4 + FS_COLS - 1) / FS_COLS;   // 97
+constexpr int FS_NR = 40;                                      // rows per thread in flight
+__device__ __forceinline__ void final_split_conv(const FinalArgs& a, const AdamHyper& hy, int cb, int tid,
+                                                 float4 (*red)[FS_COLS]) {
+  const bool seg2 = cb >= FS_NCB1;
+  const int cl = tid & (FS_COLS - 1), rg = tid >> 4;
+  const int col4 = (seg2 ? cb - FS_NCB1 : cb) * FS_COLS + cl;
+  const int ncol4 = seg2 ? NG2 / 4 : NG1 / 4;
+  const bool ok = col4 < ncol4;
+  const int e0 = col4 * 4;
+  int k, off;
+  if (!seg2) {
+    if (e0 < C1 * K1) { k = 0; off = e0; } else { k = 1; off = e0 - C1 * K1; }
+  } else {
+    if (e0 < C2 * K2) { k = 2; off = e0; } else { k = 3; off = e0 - C2 * K2; }
+  }
+  // Adam's operands of the column's 4 elements, prefetched by the row group 0 threads
+  float pv[4] = {}, mv[4] = {}, vv[4] = {};
+  if (a.param[0] && ok && rg == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pv[q] = a.param[k][off + q];
+      mv[q] = a.m[k][off + q];
+      vv[q] = a.v[k][off + q];
+    }
+  }
+  const int rows = seg2 ? a.rows2 : a.rows;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok && !seg2) {
+    const float4* src = reinterpret_cast<const float4*>(a.gpart) + col4;
+    for (int rbase = rg; rbase < rows; rbase += 16 * FS_NR) {
+      float4 x[FS_NR];
+#pragma unroll
+      for (int i = 0; i < FS_NR; ++i) {
+        const int r = rbase + 16 * i;
+        x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < rows) x[i] = src[(size_t)r * ncol4];
+      }
+#pragma unroll
+      for (int i = 0; i < FS_NR; ++i) {
+        acc.x += x[i].x; acc.y += x[i].y; acc.z += x[i].z; acc.w += x[i].w;
+      }
+    }
+  } else if (ok) {   // M rows times the member's g: one o for 4 weight columns, o .. o+3 for counts
+    constexpr int NR = 16;
+    const float4* src = reinterpret_cast<const float4*>(a.mpart) + col4;
+    const bool wcol = e0 < C2 * K2;
+    const int o0 = wcol ? e0 / K2 : e0 - C2 * K2, od = wcol ? 0 : 1;
+    const float* gv = a.vec + TV_G + o0;
+    for (int rbase = rg; rbase < rows; rbase += 16 * NR) {
+      float4 x[NR], gq[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int r = rbase + 16 * i;
+        x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        gq[i] = x[i];
+        if (r < rows) {
+          x[i] = src[(size_t)r * ncol4];
+          const float* gp = gv + (size_t)(r / a.ngrp) * TV;
+          gq[i] = make_float4(gp[0], gp[od], gp[2 * od], gp[3 * od]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        acc.x += x[i].x * gq[i].x; acc.y += x[i].y * gq[i].y;
+        acc.z += x[i].z * gq[i].z; acc.w += x[i].w * gq[i].w;
+      }
+    }
+  }
+  red[rg][cl] = acc;
+  __syncthreads();
+  if (rg != 0 || !ok) return;
+  float4 sm4 = red[0][cl];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) {
+    const float4 x = red[q][cl];
+    sm4.x += x.x; sm4.y += x.y; sm4.z += x.z; sm4.w += x.w;
+  }
+  const float gvv[4] = {sm4.x, sm4.y, sm4.z, sm4.w};
+  float* gd = a.grad[k];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gd[off + q] = gvv[q];
+  if (a.param[0]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float mm = mv[q];
+      adam_vals(pv[q], mm, vv[q], gvv[q], hy);
+      a.param[k][off + q] = pv[q];
+      a.m[k][off + q] = mm;
+      a.v[k][off + q] = vv[q];
+    }
+  }
+}
+
 template <bool SPLIT>
 __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   __shared__ float4 red[4][FIN_CB_COLS];
@@ -1183,27 +1282,27 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Adam's scalars first: their (dependent) loads overlap the gradient loads
   const AdamHyper hy = a.param[0] ? fetch_hyper(a) : AdamHyper{};
-  constexpr int NCB = SPLIT ? FIN_NCB1 + FIN_NCB2 : FIN_NCB;
+  constexpr int NCB = SPLIT ? FS_NCB1 + FS_NCB2 : FIN_NCB * FIN_RB;   // conv workgroups
   const int bx = blockIdx.x + a.conv_off;
-  if (bx < NCB * FIN_RB) {
+  if constexpr (SPLIT) {
+    if (bx < NCB) {
+      __shared__ float4 reds[16][FS_COLS];
+      final_split_conv(a, hy, bx, tid, reds);
+      return;
+    }
+  }
+  if (!SPLIT && bx < NCB) {
     const int cb = bx / FIN_RB, rb = bx - cb * FIN_RB;
-    const bool seg2 = SPLIT && cb >= FIN_NCB1;   // the M rows
-    const int col4 = (seg2 ? cb - FIN_NCB1 : cb) * FIN_CB_COLS + lane;
-    const int ncol4 = !SPLIT ? NG / 4 : seg2 ? NG2 / 4 : NG1 / 4;   // row pitch (float4)
+    const int col4 = cb * FIN_CB_COLS + lane;
+    const int ncol4 = NG / 4;   // row pitch (float4)
     const bool ok = col4 < ncol4;
     const int e0 = col4 * 4;
-    const int fcol = (seg2 ? NG1 : 0) + e0;      // column of the row-block sums
+    const int fcol = e0;        // column of the row-block sums
     int k, off;
-    if constexpr (!SPLIT) {
-      if (e0 < NG_W2) { k = 0; off = e0 - NG_W1; }        // condition_encoder.0.weight
-      else if (e0 < NG_B1) { k = 2; off = e0 - NG_W2; }   // condition_encoder.2.weight
-      else if (e0 < NG_B2) { k = 1; off = e0 - NG_B1; }   // condition_encoder.0.bias
-      else { k = 3; off = e0 - NG_B2; }                   // condition_encoder.2.bias
-    } else if (!seg2) {
-      if (e0 < C1 * K1) { k = 0; off = e0; } else { k = 1; off = e0 - C1 * K1; }
-    } else {
-      if (e0 < C2 * K2) { k = 2; off = e0; } else { k = 3; off = e0 - C2 * K2; }
-    }
+    if (e0 < NG_W2) { k = 0; off = e0 - NG_W1; }        // condition_encoder.0.weight
+    else if (e0 < NG_B1) { k = 2; off = e0 - NG_W2; }   // condition_encoder.2.weight
+    else if (e0 < NG_B2) { k = 1; off = e0 - NG_B1; }   // condition_encoder.0.bias
+    else { k = 3; off = e0 - NG_B2; }                   // condition_encoder.2.bias
     // Adam's operands of the lane's 4 elements, prefetched (used by the last block only)
     float pv[4] = {}, mv[4] = {}, vv[4] = {};
     if (a.param[0] && ok && wave == 0) {
@@ -1214,11 +1313,10 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
         vv[q] = a.v[k][off + q];
       }
     }
-    const int rows = seg2 ? a.rows2 : a.rows;
-    const int rpb = (rows + FIN_RB - 1) / FIN_RB;
-    const int r0 = rb * rpb, r1 = min(rows, r0 + rpb);
+    const int rpb = (a.rows + FIN_RB - 1) / FIN_RB;
+    const int r0 = rb * rpb, r1 = min(a.rows, r0 + rpb);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok && !seg2) {
+    if (ok) {
       const float4* src = reinterpret_cast<const float4*>(a.gpart) + col4;
       for (int rbase = r0 + wave; rbase < r1; rbase += 4 * FIN_MAXR) {
         float4 x[FIN_MAXR];
@@ -1230,31 +1328,6 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
 #pragma unroll
         for (int i = 0; i < FIN_MAXR; ++i) {
           acc.x += x[i].x; acc.y += x[i].y; acc.z += x[i].z; acc.w += x[i].w;
-        }
-      }
-    } else if (ok) {   // M rows times the member's g: one o for 4 weight columns, o .. o+3 for counts
-      constexpr int NR = 16;
-      const float4* src = reinterpret_cast<const float4*>(a.mpart) + col4;
-      const bool wcol = e0 < C2 * K2;
-      const int o0 = wcol ? e0 / K2 : e0 - C2 * K2, od = wcol ? 0 : 1;
-      const float* gv = a.vec + TV_G + o0;
-      for (int rbase = r0 + wave; rbase < r1; rbase += 4 * NR) {
-        float4 x[NR], gq[NR];
-#pragma unroll
-        for (int i = 0; i < NR; ++i) {
-          const int r = rbase + 4 * i;
-          x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-          gq[i] = x[i];
-          if (r < r1) {
-            x[i] = src[(size_t)r * ncol4];
-            const float* gp = gv + (size_t)(r / a.ngrp) * TV;
-            gq[i] = make_float4(gp[0], gp[od], gp[2 * od], gp[3 * od]);
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < NR; ++i) {
-          acc.x += x[i].x * gq[i].x; acc.y += x[i].y * gq[i].y;
-          acc.z += x[i].z * gq[i].z; acc.w += x[i].w * gq[i].w;
         }
       }
     }
@@ -1307,7 +1380,7 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   }
   // dense layers: one thread per element, a chain over the members
   const int H0 = a.P + 2 * H;
-  int i = (bx - NCB * FIN_RB) * 256 + tid;
+  int i = (bx - NCB) * 256 + tid;
   int dz_off, in_off, kdim, k;
   bool bias = false;
   if (i < H * C2) { dz_off = TV_DZ3; in_off = TV_M; kdim = C2; k = 4; }
@@ -1335,14 +1408,20 @@ __global__ __launch_bounds__(256) void train_final_kernel(FinalArgs a) {
   }
   const int row = bias ? i : i / kdim, col = bias ? 0 : i - row * kdim;
   const float* pd = a.vec + dz_off + row;
-  const float* pi = a.vec + in_off + col;
+  const float* pi = a.vec + (bias ? dz_off + row : in_off + col);
   float acc = 0.f;
-  if (bias) {
-#pragma unroll 16
-    for (int b = 0; b < a.B; ++b) acc = acc + pd[(size_t)b * TV];
-  } else {
-#pragma unroll 16
-    for (int b = 0; b < a.B; ++b) acc = fmaf(pd[(size_t)b * TV], pi[(size_t)b * TV], acc);
+  // 32 members' operands in flight at a time (clamped rows past B, never used)
+  for (int b0 = 0; b0 < a.B; b0 += 32) {
+    float xd[32], xi[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const size_t r = (size_t)min(b0 + u, a.B - 1) * TV;
+      xd[u] = pd[r];
+      xi[u] = pi[r];
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (b0 + u < a.B) acc = bias ? acc + xd[u] : fmaf(xd[u], xi[u], acc);
   }
   a.grad[k][i] = acc;
   if (a.param[0]) {
@@ -1445,7 +1524,7 @@ int dense_count(int P) { return H * C2 + H + H * H + H + H * (P + 2 * H) + H + P
 hipError_t launch_final(FinalArgs& a, bool dense, hipStream_t s) {
   if ((FIN_ABL & 1) != 0) dense = false;
   const bool split = a.mpart != nullptr;
-  const int ncb = (split ? FIN_NCB1 + FIN_NCB2 : FIN_NCB) * FIN_RB;
+  const int ncb = split ? FS_NCB1 + FS_NCB2 : FIN_NCB * FIN_RB;
   int blocks = ncb + (dense ? (dense_count(a.P) + 255) / 256 : 0);
   if ((FIN_ABL & 2) != 0) { a.conv_off = ncb; blocks -= ncb; }
   if (split) train_final_kernel<true><<<blocks, 256, 0, s>>>(a);
