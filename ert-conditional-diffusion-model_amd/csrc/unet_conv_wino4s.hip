@@ -64,6 +64,9 @@ constexpr int GNC_TAB = 4096;                 //   table entries (item x channel
 #ifndef WINO4S_XCD
 #define WINO4S_XCD 1                          // XCD-aware item walk (0: blockIdx order)
 #endif
+#ifndef WINO4S_XCDMAX
+#define WINO4S_XCDMAX 2                       // ... for layers of at most this many co groups
+#endif
 #ifndef WINO4S_PACK
 #define WINO4S_PACK 1                         // producer stage on packed fp32 pairs
 #endif
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(64 * (4 * XS + NPW)) void conv_wino4s_kernel(ConvAr
   // them) per XCD (cog = bid % ncog), which saves more (PMC, U2 B=64:
   // profiles/r05_u2_layer_traffic.txt).
   const int G = gridDim.x;
-  const int bid = (WINO4S_XCD && G % 8 == 0 && ncog <= 2)
+  const int bid = (WINO4S_XCD && G % 8 == 0 && ncog <= WINO4S_XCDMAX)
                       ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const ItemWalk wk = cw ? ItemWalk{bid * cw, 1, ncog, ksp} : ItemWalk{bid, G, ncog, ksp};
   const int nloc = cw ? (bid * cw < nitems ? min(cw, nitems - bid * cw) : 0)

@@ -372,20 +372,22 @@ class TrainPlan:
         self._replay(draw)
         return self.loss.clone() if return_tensor else self.loss.item()
 
-    RUN_STEPS = 8   # steps per graph replay in run(), launched by ONE C call
-                    # (ertd_train_steps_dev): the ~8 us gap at every call boundary
-                    # of a graph (rocprofv3 trace, B = 32) is paid once per 8 steps
+    RUN_STEPS = (32, 8)   # steps per graph replay in run(), each launched by ONE C call
+                          # (ertd_train_steps_dev): the ~8 us gap at every call boundary
+                          # of a graph (rocprofv3 trace, B = 32) is paid once per replay
 
     @torch.no_grad()
     def run(self, n: int):
         """n steps on the plan's inputs with fresh draws; no per-step host sync
-        (the loss of the last step stays in plan.loss).  Replays an 8-step graph
-        n // 8 times and the 1-step graph for the rest."""
+        (the loss of the last step stays in plan.loss).  Replays a 32-step graph
+        n // 32 times, an 8-step graph for the rest // 8, and the 1-step graph
+        for what remains."""
         n = int(n)
-        k = self.RUN_STEPS
-        for _ in range(n // k):
-            self._replay(True, k)
-        for _ in range(n % k):
+        for k in self.RUN_STEPS:
+            for _ in range(n // k):
+                self._replay(True, k)
+            n %= k
+        for _ in range(n):
             self._replay(True)
 
 

@@ -291,9 +291,9 @@ def test_train_plan_input_checks_and_state(golden_weights, cuda_dev):
 
 
 def test_train_plan_run_multistep_graph_equals_steps(golden_weights, cuda_dev):
-    """run(n) replays an 8-step graph (RUN_STEPS) n // 8 times and the 1-step
-    graph for the rest; with Philox draws keyed by (seed, member, Adam step)
-    that is bitwise the same as n single replays."""
+    """run(n) replays a 32-step graph, then 8-step graphs (RUN_STEPS), then the
+    1-step graph for the rest; with Philox draws keyed by (seed, member, Adam
+    step) that is bitwise the same as n single replays."""
     B, L, T = 8, 4693, 1000
     x0, cond, _, _ = _train_inputs(B, L, T, 650, cuda_dev)
     _, _, ab = ertdiff.get_diffusion_schedule(T, device=cuda_dev)
@@ -305,13 +305,13 @@ def test_train_plan_run_multistep_graph_equals_steps(golden_weights, cuda_dev):
         p.x0.copy_(x0)
         p.cond.copy_(cond)
         ms.append(m); os_.append(o); plans.append(p)
-    plans[0].run(11)                       # one 8-step replay + three single steps
-    for _ in range(11):
+    plans[0].run(43)                       # one 32-step, one 8-step replay + three single steps
+    for _ in range(43):
         plans[1].step()
     torch.cuda.synchronize()
     assert torch.equal(plans[0].loss, plans[1].loss)
     for (k, p1), p2 in zip(ms[0].named_parameters(), ms[1].parameters()):
         assert torch.equal(p1, p2), k
         s1, s2 = os_[0].state[p1], os_[1].state[p2]
-        assert float(s1["step"]) == float(s2["step"]) == 11.0, k
+        assert float(s1["step"]) == float(s2["step"]) == 43.0, k
         assert torch.equal(s1["exp_avg"], s2["exp_avg"]) and torch.equal(s1["exp_avg_sq"], s2["exp_avg_sq"]), k
