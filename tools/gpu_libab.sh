@@ -14,7 +14,7 @@ for n in ${LIBS:?}; do
 import csv, sys
 out = []
 for r in csv.DictReader(open(sys.argv[1])):
-    if any(k in r["Name"] for k in ("conv_bwd", "enc_train", "final_kernel", "head_kernel<2>")):
+    if any(k in r["Name"] for k in ("conv_bwd", "enc_train", "final_kernel", "head_kernel<2>")) and int(r["Calls"]) > 10:
         out.append(f"{r['Name'].split('(')[0].split('::')[-1][:18]} {float(r['AverageNs'])/1e3:6.2f}")
 print("   ", " | ".join(out))
 PY
