@@ -297,7 +297,7 @@ def train_bench(dev, steps=200, B=32, T=500, reps=200):
     plan = ertdiff.TrainPlan(model, opt, B, L_MEAS, T, ab, seed=1234)
     plan.x0.copy_(x0)
     plan.cond.copy_(cond)
-    plan.run(20)
+    plan.run(40)   # warm-up: captures the 32- and 8-step graphs run() replays
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     plan.run(steps)

@@ -56,7 +56,7 @@ def main():
     plan = ertdiff.TrainPlan(m, opt, B, L, T, ab)
     plan.x0.copy_(x0)
     plan.cond.copy_(cond)
-    plan.run(20)
+    plan.run(40)   # warm-up: captures the 32- and 8-step graphs run() replays
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
